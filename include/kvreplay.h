@@ -1,0 +1,167 @@
+/*
+ * kvreplay.h — C ABI of the MI355X segment-replay + CRC32-verify engine.
+ *
+ * Drop-in boundary for the index-rebuild-on-restart path of whispem/mini-kvstore-v2
+ * (reference snapshot 0.3.0, read-only at /root/reference):
+ *
+ *   src/store/engine.rs:53-57   for (_id, path) in &segment_paths {
+ *                                   Self::replay_segment(path, &mut values)?;   }
+ *   src/store/engine.rs:79-154  replay_segment — the serial per-record walk this ABI replaces
+ *   src/volume/storage.rs:27    crc32fast::hash(data) — the CRC-32 definition (ETag)
+ *   src/store/index.rs:7        (segment_id, offset, length) — the target index shape
+ *
+ * The reference has no FFI of its own: the seam is source level.  A Rust
+ * caller declares these functions `extern "C"` with #[repr(C)] mirrors of the structs below
+ * (INTEGRATION.md shows the binding), sorts segments by id exactly as engine.rs:51 does, hands
+ * their bytes over, and folds the returned tuples into its index.
+ *
+ * Conventions
+ *   - All functions are synchronous (KVStore::open is a blocking constructor, engine.rs:24).
+ *   - The library never frees caller memory; device scratch belongs to the context.
+ *   - A context is not thread-safe; use one per thread (or per GPU).
+ *   - Return codes: KVR_OK (0), KVR_CORRUPTED (1, *err filled: the first error in
+ *     (segment order, offset) order — exactly the error engine.rs:56 would propagate),
+ *     KVR_CAPACITY (2, *n_out = required tuple count), negative = usage / HIP / IO failure.
+ */
+#ifndef KVREPLAY_H
+#define KVREPLAY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KVR_ABI_VERSION 1
+
+/* ---- status codes --------------------------------------------------------------------- */
+#define KVR_OK          0
+#define KVR_CORRUPTED   1   /* StoreError::CorruptedData (error.rs:11-12); *err filled     */
+#define KVR_CAPACITY    2   /* out[] too small; *n_out = tuples required                     */
+#define KVR_EINVAL     (-1) /* bad argument (unsorted segments, NULL pointer, ...)           */
+#define KVR_EHIP       (-2) /* HIP runtime failure (no device, launch failure, ...)          */
+#define KVR_EIO        (-3) /* host I/O failure                                              */
+#define KVR_ENOMEM     (-4) /* host or device allocation failure                             */
+
+/* ---- error kinds: one per CorruptedData site of engine.rs:79-154 (in check order) ------- */
+#define KVR_E_NONE      0
+#define KVR_E_OPEN      1   /* engine.rs:80-82   "Failed to open segment {path}: {io}"          */
+#define KVR_E_KEY_LEN   2   /* engine.rs:96-102  "Failed to read key length in {path}: ..."     */
+#define KVR_E_KEY       3   /* engine.rs:107-113 "Failed to read key in {path}: ..."            */
+#define KVR_E_UTF8      4   /* engine.rs:114-116 "Invalid UTF-8 key in {path}: {FromUtf8Error}" */
+#define KVR_E_VAL_LEN   5   /* engine.rs:121-127 "Failed to read val len in {path}: ..."        */
+#define KVR_E_VAL       6   /* engine.rs:130-136 "Failed to read val in {path}: ..."            */
+#define KVR_E_OPCODE    7   /* engine.rs:143-149 "Unknown opcode {op} in segment {path}"        */
+
+/* ---- replay flags --------------------------------------------------------------------- */
+#define KVR_SEGS_ON_DEVICE      0x1u  /* segs[i].bytes are device pointers on ctx's device      */
+#define KVR_OUT_ON_DEVICE       0x2u  /* out is a device pointer (tuples stay resident in HBM)  */
+#define KVR_EXPECTED_ON_DEVICE  0x4u  /* expected_crc is a device pointer                        */
+
+/* ---- tuple flags ---------------------------------------------------------------------- */
+#define KVR_TF_VERIFIED   0x1u  /* an expected CRC was supplied for this record (SET only)    */
+#define KVR_TF_CRC_FAIL   0x2u  /* crc32 != expected: the record fails verification           */
+
+/* One input segment.  Segments must be passed in ascending seg_id (the caller performs the
+ * engine.rs:51 sort); each is replayed from offset 0 exactly like replay_segment. */
+typedef struct kvr_segment {
+    uint64_t       seg_id;   /* id parsed from "segment-<id>.dat" (engine.rs:40-45)           */
+    const uint8_t *bytes;    /* segment bytes; host or device pointer (KVR_SEGS_ON_DEVICE)    */
+    uint64_t       len;      /* bytes in the file                                              */
+} kvr_segment;
+
+/* One record on the replay chain, in (segment, offset) order.  32 bytes, layout frozen.
+ * SET: framing [0][klen u32 LE][key][vlen u32 LE][value]  (engine.rs:169-173)
+ * DEL: framing [1][klen u32 LE][key]                      (engine.rs:191-193)
+ * key bytes live at rec_off + 5, value bytes at rec_off + 9 + key_len. */
+typedef struct kvr_tuple {
+    uint64_t rec_off;   /* offset of the op byte within the segment                          */
+    uint32_t seg_idx;   /* index into the caller's segs[] (map back to seg_id on the host)    */
+    uint32_t key_len;
+    uint32_t val_len;   /* 0 for DEL                                                          */
+    uint32_t crc32;     /* CRC-32/ISO-HDLC of the value bytes = crc32fast::hash (storage.rs:27); 0 for DEL */
+    uint32_t key_tag;   /* CRC-32/ISO-HDLC of the key bytes (hash tag for host-side folding)  */
+    uint8_t  op;        /* 0 = SET, 1 = DEL                                                    */
+    uint8_t  flags;     /* KVR_TF_*                                                            */
+    uint16_t reserved;
+} kvr_tuple;
+
+/* The first error in (segment, offset) order — the error KVStore::open returns. */
+typedef struct kvr_error {
+    int32_t  kind;      /* KVR_E_*                                                            */
+    uint32_t seg_idx;   /* segment index of the failing record                                */
+    uint64_t rec_off;   /* offset of the failing record's op byte                             */
+    uint64_t aux;       /* KVR_E_OPCODE: the opcode; KVR_E_UTF8: valid_up_to | (error_len << 32),
+                           error_len 0 meaning "incomplete" (Utf8Error::error_len() == None)  */
+} kvr_error;
+
+/* Per-call measurements of the last kvr_replay on a context (device timings via hipEvents on
+ * the context's stream). */
+typedef struct kvr_stats {
+    double   ms_total;          /* whole device pipeline, first kernel start -> last kernel end */
+    double   ms_replay;         /* the main replay kernel (first pass)                           */
+    double   ms_link;           /* stripe linking + re-walk passes                               */
+    double   ms_compact;        /* tuple compaction                                              */
+    uint64_t bytes_in;          /* segment bytes replayed                                        */
+    uint64_t n_records;         /* tuples produced                                               */
+    uint64_t n_crc_fail;        /* records whose CRC failed verification                         */
+    uint32_t n_stripes;         /* speculation units                                             */
+    uint32_t n_tiles;
+    uint32_t n_redo;            /* stripes re-walked after a failed speculation                   */
+    uint32_t n_link_passes;
+} kvr_stats;
+
+typedef struct kvr_ctx kvr_ctx;
+
+/* Context on one HIP device with its own stream and device arenas. */
+int  kvr_ctx_create(int device, kvr_ctx **out);
+void kvr_ctx_destroy(kvr_ctx *ctx);
+/* Run on a caller-provided hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL
+ * restores the context's own stream. */
+int  kvr_ctx_set_stream(kvr_ctx *ctx, void *hip_stream);
+int  kvr_ctx_device(const kvr_ctx *ctx);
+
+/* Replay n_segs segments (ascending seg_id) -> tuples in (segment, offset) order.
+ * expected_crc (optional, may be NULL): expected CRC per record in tuple order, e.g. the
+ * ETags BlobStorage::put returned (storage.rs:27); records with index < n_expected get
+ * KVR_TF_VERIFIED and, on mismatch, KVR_TF_CRC_FAIL.
+ * Returns KVR_OK, KVR_CORRUPTED (*err), KVR_CAPACITY (*n_out = required) or < 0. */
+int  kvr_replay(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint32_t flags,
+                const uint32_t *expected_crc, size_t n_expected,
+                kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err);
+
+int  kvr_last_stats(const kvr_ctx *ctx, kvr_stats *out);
+
+/* Host helpers. */
+const char *kvr_strerror(int code);
+/* CRC-32/ISO-HDLC, identical to crc32fast::hash (storage.rs:27) when crc == 0. */
+uint32_t kvr_crc32(uint32_t crc, const uint8_t *data, size_t len);
+/* Render the exact engine.rs CorruptedData message (without the "Corrupted data: " prefix of
+ * error.rs:11) for err and the segment's path.  Returns the length written (snprintf rules). */
+int  kvr_format_error(const kvr_error *err, const char *path, char *buf, size_t cap);
+
+/* ---- synthetic segment generator (device side; byte-identical to kvh_gen_segment) -------- */
+typedef struct kvr_gen_params {
+    uint64_t seed;
+    uint64_t seg_bytes;        /* target size: records are appended while the next one fits  */
+    uint32_t key_space_log2;   /* keys are "k%015u" over [0, 2^key_space_log2)                */
+    uint32_t key_dist;         /* 0 = uniform, 1 = Zipf-like (log-uniform bucket, P ~ 1/id)    */
+    uint32_t val_min;          /* value length: fixed if val_min == val_max, else log-uniform */
+    uint32_t val_max;
+    uint32_t del_permille;     /* share of DEL records (per mille)                             */
+    uint32_t flip_per_million; /* fault injection: one flipped value bit after the manifest    */
+} kvr_gen_params;
+
+/* Generate segment number seg_no (0-based) of a synthetic store into device memory d_buf
+ * (capacity cap bytes).  *len_out = bytes written; if d_expected != NULL, the manifest
+ * (expected CRC per record, 0 for DEL) is written to device memory d_expected (capacity
+ * exp_cap entries) and *n_rec_out = records in the segment. */
+int  kvr_gen_segment_device(kvr_ctx *ctx, const kvr_gen_params *p, uint64_t seg_no,
+                            uint8_t *d_buf, uint64_t cap, uint64_t *len_out,
+                            uint32_t *d_expected, uint64_t exp_cap, uint64_t *n_rec_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KVREPLAY_H */

@@ -1,0 +1,75 @@
+/*
+ * kvstore_host.h — host side of the drop-in: the KVStore::open path of
+ * whispem/mini-kvstore-v2 (src/store/engine.rs:24-76) rebuilt around kvr_replay.
+ *
+ *   kvh_discover      segment discovery + ordering        engine.rs:31-51
+ *   kvh_gen_segment   synthetic segments, framing writer  engine.rs:157-198 (byte-identical to
+ *                     kvr_gen_segment_device)
+ *   kvh_fold          last-writer-wins index fold         engine.rs:137 (insert), :141 (remove)
+ *   kvs_open / kvs_get / kvs_stats / kvs_close
+ *                     the crate-public KVStore surface the replay path feeds (lib.rs:2-3,
+ *                     engine.rs:24, :200, :232-259); the index has the shape of the reference's
+ *                     dead `Index` (src/store/index.rs:7): key -> (segment, offset, length).
+ *
+ * Status codes and kvr_error are those of kvreplay.h.
+ */
+#ifndef KVSTORE_HOST_H
+#define KVSTORE_HOST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "kvreplay.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* CPU generator: same bytes and manifest as kvr_gen_segment_device for (p, seg_no).
+ * buf may be NULL to only size the segment (*len_out, *n_rec_out). */
+int kvh_gen_segment(const kvr_gen_params *p, uint64_t seg_no, uint8_t *buf, uint64_t cap, uint64_t *len_out,
+                    uint32_t *expected, uint64_t exp_cap, uint64_t *n_rec_out);
+
+/* Discovery as engine.rs:31-51: entries of dir named "segment-<id>.dat" whose <id> parses as a
+ * Rust u64 (optional '+', ASCII digits, no overflow), in ascending id order (ties by name).
+ * Writes up to cap ids to ids[] and NUL-separated full paths into paths (path_cap bytes);
+ * *n_out = number of segments found.  Returns KVR_OK, KVR_CAPACITY or KVR_EIO. */
+int kvh_discover(const char *dir, uint64_t *ids, size_t cap, char *paths, size_t path_cap, size_t *n_out);
+
+/* Rust `u64::from_str` on [s, s+n): returns 1 and *out on success. */
+int kvh_parse_u64(const char *s, size_t n, uint64_t *out);
+
+/* Fold tuples (in (segment, offset) order) by last-writer-wins.  Keys are read from
+ * segs[t.seg_idx].bytes + t.rec_off + 5 (host memory).  live[i] = 1 iff tuple i is the final
+ * SET of its key.  Returns the number of live keys (stats().num_keys) and *total_bytes
+ * (stats().total_bytes, engine.rs:253-255). */
+uint64_t kvh_fold(const kvr_segment *segs, const kvr_tuple *t, size_t n, uint8_t *live, uint64_t *total_bytes);
+
+typedef struct kvs_store kvs_store;
+
+typedef struct kvs_stats {          /* StoreStats, src/store/stats.rs:3-10 */
+    uint64_t num_keys;
+    uint64_t num_segments;
+    uint64_t total_bytes;
+    uint64_t active_segment_id;
+    uint64_t oldest_segment_id;
+} kvs_stats;
+
+/* KVStore::open(dir): create the directory if missing, discover and read the segments,
+ * replay them on ctx's GPU, fold the index, create the next active segment file
+ * (engine.rs:59-68).  On KVR_CORRUPTED, *err and msg (the exact engine.rs message, without
+ * error.rs's "Corrupted data: " prefix) describe the first error. */
+int kvs_open(const char *dir, kvr_ctx *ctx, kvs_store **out, kvr_error *err, char *msg, size_t msg_cap);
+/* KVStore::get (engine.rs:200): 1 and the value bytes if live, 0 if absent. */
+int kvs_get(const kvs_store *s, const uint8_t *key, size_t klen, const uint8_t **val, size_t *vlen);
+/* Index entry (index.rs:7 shape): segment id, value offset inside that segment file, length. */
+int kvs_locate(const kvs_store *s, const uint8_t *key, size_t klen, uint64_t *seg_id, uint64_t *val_off, uint64_t *len);
+int kvs_stats_get(const kvs_store *s, kvs_stats *out);
+/* KVStore::list_keys: up to cap keys as (offset, length) pairs into the returned arena. */
+size_t kvs_num_keys(const kvs_store *s);
+void kvs_close(kvs_store *s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

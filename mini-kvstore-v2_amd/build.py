@@ -1,0 +1,67 @@
+"""Build the native libraries in-tree (they travel to the GPU box with the repo snapshot).
+
+  lib/libkvreplay.so   HIP kernels + the C ABI of include/kvreplay.h   (hipcc, gfx950)
+  lib/libkvhost.so     discovery, generator, fold, KVStore mirror      (g++, links libkvreplay)
+  ../oracle/liboracle.so   CPU restatement used only by tests / bench cpu_baseline (gcc)
+"""
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+LIB = os.path.join(PKG, "lib")
+CSRC = os.path.join(PKG, "csrc")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("KVR_OFFLOAD_ARCH", "gfx950")
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("build failed: " + " ".join(cmd))
+
+
+def _deps(*names):
+    inc = os.path.join(ROOT, "include")
+    out = [os.path.join(CSRC, n) for n in names]
+    out += [os.path.join(inc, f) for f in os.listdir(inc)]
+    return out
+
+
+def build(force=False, verbose=False):
+    os.makedirs(LIB, exist_ok=True)
+    rep = os.path.join(LIB, "libkvreplay.so")
+    deps = _deps("kvr_api.hip", "kvr_kernels.hip", "kvr_device.h", "kvr_gen_common.h")
+    if force or _newer(rep, deps):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+              "-Wall", "-Wno-unused-result", "-o", rep, os.path.join(CSRC, "kvr_api.hip")])
+        if verbose:
+            print("built", rep)
+    host = os.path.join(LIB, "libkvhost.so")
+    deps = _deps("kvr_host.cpp", "kvr_gen_common.h") + [rep]
+    if force or _newer(host, deps):
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-o", host,
+              os.path.join(CSRC, "kvr_host.cpp"), "-L", LIB, "-lkvreplay",
+              "-Wl,-rpath,$ORIGIN", "-Wl,--no-as-needed"])
+        if verbose:
+            print("built", host)
+    orc = os.path.join(ROOT, "oracle", "liboracle.so")
+    src = os.path.join(ROOT, "oracle", "replay_ref.c")
+    if force or _newer(orc, [src, os.path.join(ROOT, "include", "kvreplay.h")]):
+        _run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-Wall", "-o", orc, src])
+        if verbose:
+            print("built", orc)
+    return rep, host, orc
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)

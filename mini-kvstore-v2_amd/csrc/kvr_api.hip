@@ -1,0 +1,444 @@
+/*
+ * kvr_api.hip — the C ABI of include/kvreplay.h: contexts, device arenas, the launch
+ * pipeline of one replay call, the device-side generator and host helpers.
+ *
+ * One kvr_replay call:
+ *   [H2D of host segments]  k_replay(all stripes)  k_link  k_replay(re-walk list)  k_link
+ *   k_tsum  k_tscan  k_compact  [D2H of tuples]  — one stream, one host synchronisation in the
+ *   common case; more k_replay/k_link rounds only when a speculated stripe entry was wrong.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "kvr_kernels.hip"
+
+using namespace kvr;
+
+namespace {
+
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    int ensure(size_t m) {
+        if (m <= n && p) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        if (m == 0) m = 1;
+        if (hipMalloc(&p, m * sizeof(T)) != hipSuccess) { p = nullptr; return -1; }
+        n = m;
+        return 0;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+};
+
+constexpr uint32_t REDO_GRID = 1024;
+
+}  // namespace
+
+struct kvr_ctx {
+    int device = 0;
+    int n_cu = 256;
+    hipStream_t own = nullptr, stream = nullptr;
+    hipEvent_t ev[6] = {};
+    DevBuf<uint8_t> arena;
+    DevBuf<SegDesc> segs;
+    DevBuf<StripeDesc> stripes;
+    DevBuf<StripeRes> sres;
+    DevBuf<TileRes> tres;
+    DevBuf<kvr_tuple> pool, dense;
+    DevBuf<RedoEnt> redo;
+    DevBuf<LinkResult> link;
+    DevBuf<Counters> ctr;
+    DevBuf<uint32_t> seg_bad, seg_err, expected;
+    DevBuf<uint64_t> bsum;
+    DevBuf<uint32_t> crc, pw16, pw1;
+    DevBuf<GenRecDev> gen;
+    LinkResult *h_link = nullptr;
+    Counters *h_ctr = nullptr;
+    std::vector<SegDesc> h_segs;
+    std::vector<StripeDesc> h_stripes;
+    uint64_t pool_hint = 0;
+    kvr_stats stats{};
+};
+
+#define HIPCHK(x)                                   \
+    do {                                            \
+        if ((x) != hipSuccess) return KVR_EHIP;     \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------
+// tables: slice-by-16 CRC tables and the shift operators X(n) = x^(8n) mod P
+// ---------------------------------------------------------------------------------------
+static void build_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &pw16, std::vector<uint32_t> &pw1) {
+    crc.assign(16 * 256, 0);
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ POLY : (c >> 1);
+        crc[i] = c;
+    }
+    for (int t = 1; t < 16; ++t)
+        for (int i = 0; i < 256; ++i) {
+            const uint32_t prev = crc[(t - 1) * 256 + i];
+            crc[t * 256 + i] = (prev >> 8) ^ crc[prev & 0xFF];
+        }
+    pw1.assign(20, 0);
+    pw1[0] = 0x80000000u;                              // x^0
+    for (int i = 1; i < 20; ++i) pw1[i] = gf_mul(pw1[i - 1], 0x00800000u);   // * x^8
+    const uint32_t x16 = pw1[16];
+    pw16.assign(TILE / 16 + 4, 0);
+    pw16[0] = 0x80000000u;
+    for (size_t k = 1; k < pw16.size(); ++k) pw16[k] = gf_mul(pw16[k - 1], x16);
+}
+
+extern "C" {
+
+const char *kvr_strerror(int code) {
+    switch (code) {
+    case KVR_OK: return "ok";
+    case KVR_CORRUPTED: return "corrupted data";
+    case KVR_CAPACITY: return "output capacity too small";
+    case KVR_EINVAL: return "invalid argument";
+    case KVR_EHIP: return "HIP runtime error";
+    case KVR_EIO: return "I/O error";
+    case KVR_ENOMEM: return "out of memory";
+    default: return "unknown status";
+    }
+}
+
+uint32_t kvr_crc32(uint32_t crc, const uint8_t *data, size_t len) {
+    static uint32_t T[256];
+    static bool ready = false;
+    if (!ready) {
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ POLY : (c >> 1);
+            T[i] = c;
+        }
+        ready = true;
+    }
+    uint32_t c = ~crc;
+    for (size_t i = 0; i < len; ++i) c = (c >> 8) ^ T[(c ^ data[i]) & 0xFFu];
+    return ~c;
+}
+
+int kvr_format_error(const kvr_error *e, const char *path, char *buf, size_t cap) {
+    if (!e || !buf) return -1;
+    if (!path) path = "";
+    static const char *eof = "failed to fill whole buffer";   // std::io read_exact UnexpectedEof
+    switch (e->kind) {
+    case KVR_E_OPEN: {
+        const int code = (int)e->aux;
+        return snprintf(buf, cap, "Failed to open segment %s: %s (os error %d)", path, strerror(code), code);
+    }
+    case KVR_E_KEY_LEN: return snprintf(buf, cap, "Failed to read key length in %s: %s", path, eof);
+    case KVR_E_KEY: return snprintf(buf, cap, "Failed to read key in %s: %s", path, eof);
+    case KVR_E_UTF8: {
+        const unsigned long long vu = e->aux & 0xFFFFFFFFull;
+        const unsigned el = (unsigned)(e->aux >> 32);
+        if (el)
+            return snprintf(buf, cap, "Invalid UTF-8 key in %s: invalid utf-8 sequence of %u bytes from index %llu",
+                            path, el, vu);
+        return snprintf(buf, cap, "Invalid UTF-8 key in %s: incomplete utf-8 byte sequence from index %llu", path, vu);
+    }
+    case KVR_E_VAL_LEN: return snprintf(buf, cap, "Failed to read val len in %s: %s", path, eof);
+    case KVR_E_VAL: return snprintf(buf, cap, "Failed to read val in %s: %s", path, eof);
+    case KVR_E_OPCODE: return snprintf(buf, cap, "Unknown opcode %u in segment %s", (unsigned)e->aux, path);
+    default: return snprintf(buf, cap, "no error");
+    }
+}
+
+int kvr_ctx_create(int device, kvr_ctx **out) {
+    if (!out) return KVR_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return KVR_EHIP;
+    if (device < 0 || device >= ndev) return KVR_EINVAL;
+    HIPCHK(hipSetDevice(device));
+    kvr_ctx *c = new kvr_ctx();
+    c->device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->n_cu = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return KVR_EHIP; }
+    c->stream = c->own;
+    for (auto &e : c->ev) if (hipEventCreate(&e) != hipSuccess) { delete c; return KVR_EHIP; }
+    if (hipHostMalloc(reinterpret_cast<void **>(&c->h_link), sizeof(LinkResult)) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&c->h_ctr), sizeof(Counters)) != hipSuccess) { delete c; return KVR_ENOMEM; }
+    std::vector<uint32_t> crc, pw16, pw1;
+    build_tables(crc, pw16, pw1);
+    if (c->crc.ensure(crc.size()) || c->pw16.ensure(pw16.size()) || c->pw1.ensure(pw1.size()) ||
+        c->link.ensure(1) || c->ctr.ensure(1)) { kvr_ctx_destroy(c); return KVR_ENOMEM; }
+    if (hipMemcpy(c->crc.p, crc.data(), crc.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->pw16.p, pw16.data(), pw16.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->pw1.p, pw1.data(), pw1.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        kvr_ctx_destroy(c);
+        return KVR_EHIP;
+    }
+    *out = c;
+    return KVR_OK;
+}
+
+void kvr_ctx_destroy(kvr_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    c->arena.release(); c->segs.release(); c->stripes.release(); c->sres.release(); c->tres.release();
+    c->pool.release(); c->dense.release(); c->redo.release(); c->link.release(); c->ctr.release();
+    c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->bsum.release();
+    c->crc.release(); c->pw16.release(); c->pw1.release(); c->gen.release();
+    if (c->h_link) (void)hipHostFree(c->h_link);
+    if (c->h_ctr) (void)hipHostFree(c->h_ctr);
+    for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+int kvr_ctx_set_stream(kvr_ctx *c, void *s) {
+    if (!c) return KVR_EINVAL;
+    c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own;
+    return KVR_OK;
+}
+
+int kvr_ctx_device(const kvr_ctx *c) { return c ? c->device : -1; }
+
+int kvr_last_stats(const kvr_ctx *c, kvr_stats *out) {
+    if (!c || !out) return KVR_EINVAL;
+    *out = c->stats;
+    return KVR_OK;
+}
+
+static float ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
+    return ms;
+}
+
+int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, const uint32_t *expected,
+               size_t n_expected, kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err) {
+    if (!c || (!segs && n) || !n_out || (cap && !out)) return KVR_EINVAL;
+    if (err) memset(err, 0, sizeof(*err));
+    *n_out = 0;
+    memset(&c->stats, 0, sizeof(c->stats));
+    if (n == 0) return KVR_OK;
+    if (n >= 0xFFFFFFFFull) return KVR_EINVAL;
+    for (size_t i = 0; i < n; ++i) {
+        if (i && segs[i].seg_id < segs[i - 1].seg_id) return KVR_EINVAL;   // caller sorts (engine.rs:51)
+        if (segs[i].len && !segs[i].bytes) return KVR_EINVAL;
+    }
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+
+    // 1. segment bytes in HBM
+    std::vector<const uint8_t *> dptr(n);
+    uint64_t total_bytes = 0;
+    for (size_t i = 0; i < n; ++i) total_bytes += segs[i].len;
+    if (flags & KVR_SEGS_ON_DEVICE) {
+        for (size_t i = 0; i < n; ++i) dptr[i] = segs[i].bytes;
+    } else {
+        uint64_t need = 256;
+        for (size_t i = 0; i < n; ++i) need += (segs[i].len + 255) & ~255ull;
+        if (c->arena.ensure(need)) return KVR_ENOMEM;
+        uint64_t off = 0;
+        for (size_t i = 0; i < n; ++i) {
+            dptr[i] = c->arena.p + off;
+            if (segs[i].len) HIPCHK(hipMemcpyAsync(c->arena.p + off, segs[i].bytes, segs[i].len, hipMemcpyHostToDevice, st));
+            off += (segs[i].len + 255) & ~255ull;
+        }
+    }
+
+    // 2. tiles and stripes
+    c->h_segs.assign(n, SegDesc{});
+    uint64_t total_tiles = 0;
+    for (size_t i = 0; i < n; ++i) {
+        SegDesc &g = c->h_segs[i];
+        g.base = dptr[i];
+        g.len = segs[i].len;
+        g.d0 = (uint32_t)(reinterpret_cast<uintptr_t>(dptr[i]) & 15u);
+        g.n_tiles = g.len ? (uint32_t)((g.len + g.d0 + TILE - 1) / TILE) : 0u;
+        g.tile0 = (uint32_t)total_tiles;
+        total_tiles += g.n_tiles;
+    }
+    if (total_tiles >= 0xFFFFFFFFull) return KVR_EINVAL;
+    const uint64_t target = (uint64_t)c->n_cu * 8;
+    const uint64_t tps = std::max<uint64_t>(1, (total_tiles + target - 1) / target);
+    c->h_stripes.clear();
+    for (size_t i = 0; i < n; ++i) {
+        SegDesc &g = c->h_segs[i];
+        g.stripe0 = (uint32_t)c->h_stripes.size();
+        const uint64_t ns = g.n_tiles ? (g.n_tiles + tps - 1) / tps : 0;
+        for (uint64_t j = 0; j < ns; ++j)
+            c->h_stripes.push_back(StripeDesc{(uint32_t)i, (uint32_t)(j * g.n_tiles / ns),
+                                              (uint32_t)((j + 1) * g.n_tiles / ns), 0u});
+        g.n_stripes = (uint32_t)ns;
+    }
+    const uint32_t n_stripes = (uint32_t)c->h_stripes.size();
+    const uint32_t n_tiles = (uint32_t)total_tiles;
+    c->stats.bytes_in = total_bytes;
+    c->stats.n_stripes = n_stripes;
+    c->stats.n_tiles = n_tiles;
+    if (n_stripes == 0) return KVR_OK;   // only empty segments: nothing to replay
+
+    if (c->segs.ensure(n) || c->stripes.ensure(n_stripes) || c->sres.ensure(n_stripes) ||
+        c->tres.ensure(n_tiles) || c->redo.ensure(std::max<uint32_t>(n_stripes, REDO_GRID)) ||
+        c->seg_bad.ensure(n) || c->seg_err.ensure(n))
+        return KVR_ENOMEM;
+    HIPCHK(hipMemcpyAsync(c->segs.p, c->h_segs.data(), n * sizeof(SegDesc), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->stripes.p, c->h_stripes.data(), n_stripes * sizeof(StripeDesc), hipMemcpyHostToDevice, st));
+
+    const uint32_t nb = (n_tiles + CB - 1) / CB;
+    if (c->bsum.ensure(nb)) return KVR_ENOMEM;
+
+    const uint32_t *d_exp = nullptr;
+    if (expected && n_expected) {
+        if (flags & KVR_EXPECTED_ON_DEVICE) {
+            d_exp = expected;
+        } else {
+            if (c->expected.ensure(n_expected)) return KVR_ENOMEM;
+            HIPCHK(hipMemcpyAsync(c->expected.p, expected, n_expected * 4, hipMemcpyHostToDevice, st));
+            d_exp = c->expected.p;
+        }
+    }
+
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        const uint64_t pool_cap = std::max<uint64_t>(c->pool_hint, std::max<uint64_t>(65536, total_bytes / 192 + n));
+        if (c->pool.ensure(pool_cap)) return KVR_ENOMEM;
+        kvr_tuple *d_out;
+        uint64_t out_cap;
+        if (flags & KVR_OUT_ON_DEVICE) {
+            d_out = out;
+            out_cap = cap;
+        } else {
+            if (c->dense.ensure(pool_cap)) return KVR_ENOMEM;
+            d_out = c->dense.p;
+            out_cap = pool_cap;
+        }
+        HIPCHK(hipMemsetAsync(c->ctr.p, 0, sizeof(Counters), st));
+        HIPCHK(hipMemsetAsync(c->link.p, 0, sizeof(LinkResult), st));
+        HIPCHK(hipEventRecord(c->ev[0], st));
+        hipLaunchKernelGGL(k_replay, dim3(n_stripes), dim3(NT), 0, st, c->segs.p, c->stripes.p, c->sres.p, c->tres.p,
+                           c->pool.p, pool_cap, c->ctr.p, c->crc.p, c->pw16.p, c->pw1.p, c->redo.p, c->link.p, 0);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c->ev[1], st));
+        hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
+                           c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_replay, dim3(std::min(n_stripes, REDO_GRID)), dim3(NT), 0, st, c->segs.p, c->stripes.p,
+                           c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, c->crc.p, c->pw16.p, c->pw1.p,
+                           c->redo.p, c->link.p, 1);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
+                           c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c->ev[2], st));
+        hipLaunchKernelGGL(k_tsum, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->link.p);
+        hipLaunchKernelGGL(k_tscan, dim3(1), dim3(1024), 0, st, c->bsum.p, nb, c->ctr.p, c->link.p);
+        hipLaunchKernelGGL(k_compact, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->pool.p, pool_cap,
+                           d_out, out_cap, d_exp, (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c->ev[3], st));
+        HIPCHK(hipMemcpyAsync(c->h_link, c->link.p, sizeof(LinkResult), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        c->stats.ms_replay = ev_ms(c->ev[0], c->ev[1]);
+        c->stats.ms_link = ev_ms(c->ev[1], c->ev[2]);
+        c->stats.ms_compact = ev_ms(c->ev[2], c->ev[3]);
+        c->stats.ms_total = ev_ms(c->ev[0], c->ev[3]);
+
+        // rare: more re-walk rounds (a speculated entry was wrong twice in a row)
+        uint32_t guard = 0;
+        bool recompact = false;
+        while (c->h_link->status == 3 && guard++ < n_stripes + 4) {
+            hipLaunchKernelGGL(k_replay, dim3(std::min(n_stripes, REDO_GRID)), dim3(NT), 0, st, c->segs.p, c->stripes.p,
+                               c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, c->crc.p, c->pw16.p, c->pw1.p,
+                               c->redo.p, c->link.p, 1);
+            hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes,
+                               c->sres.p, c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(c->h_link, c->link.p, sizeof(LinkResult), hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            recompact = true;
+        }
+        if (c->h_link->status == 3) return KVR_EHIP;   // cannot happen: each round fixes one stripe
+        if (recompact && c->h_link->status == 0) {
+            hipLaunchKernelGGL(k_tsum, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->link.p);
+            hipLaunchKernelGGL(k_tscan, dim3(1), dim3(1024), 0, st, c->bsum.p, nb, c->ctr.p, c->link.p);
+            hipLaunchKernelGGL(k_compact, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->pool.p, pool_cap,
+                               d_out, out_cap, d_exp, (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+        }
+        c->stats.n_link_passes = c->h_link->passes;
+        if (c->h_ctr->overflow & 2u) return KVR_EHIP;   // stitch did not converge (bug trap)
+        if (c->h_ctr->overflow & 1u) {   // pool too small: grow to what this pass needed and run again
+            c->pool_hint = c->h_ctr->pool_cursor + c->h_ctr->pool_cursor / 8 + 4096;
+            continue;
+        }
+        if (c->h_link->status == 1) {
+            if (err) {
+                err->kind = (int32_t)c->h_link->err_kind;
+                err->seg_idx = c->h_link->err_seg;
+                err->rec_off = c->h_link->err_pos;
+                err->aux = c->h_link->err_aux;
+            }
+            return KVR_CORRUPTED;
+        }
+        const uint64_t total = c->h_ctr->total_tuples;
+        c->stats.n_records = total;
+        c->stats.n_crc_fail = c->h_ctr->crc_fail;
+        *n_out = total;
+        if (!(flags & KVR_OUT_ON_DEVICE) && cap) {
+            const uint64_t m = std::min<uint64_t>(total, cap);
+            if (m) {
+                HIPCHK(hipMemcpyAsync(out, c->dense.p, m * sizeof(kvr_tuple), hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+            }
+        }
+        return total > cap ? KVR_CAPACITY : KVR_OK;
+    }
+    return KVR_ENOMEM;
+}
+
+int kvr_gen_segment_device(kvr_ctx *c, const kvr_gen_params *p, uint64_t seg_no, uint8_t *d_buf, uint64_t cap,
+                           uint64_t *len_out, uint32_t *d_expected, uint64_t exp_cap, uint64_t *n_rec_out) {
+    if (!c || !p || !len_out) return KVR_EINVAL;
+    HIPCHK(hipSetDevice(c->device));
+    const uint64_t sbase = kvr_gen_sbase(p->seed, seg_no);
+    std::vector<GenRecDev> recs;
+    uint64_t off = 0;
+    for (uint64_t i = 0;; ++i) {
+        kvr_gen_rec r;
+        kvr_gen_record(p, sbase, i, &r);
+        const uint64_t sz = kvr_gen_rec_size(&r);
+        if (off + sz > p->seg_bytes) break;
+        recs.push_back(GenRecDev{off, r.key_id, r.vseed, r.flip_bit, r.op, r.vlen});
+        off += sz;
+    }
+    *len_out = off;
+    if (n_rec_out) *n_rec_out = recs.size();
+    if (off > cap || !d_buf) return KVR_CAPACITY;
+    if (d_expected && recs.size() > exp_cap) return KVR_CAPACITY;
+    if (recs.empty()) return KVR_OK;
+    if (c->gen.ensure(recs.size())) return KVR_ENOMEM;
+    hipStream_t st = c->stream;
+    HIPCHK(hipMemcpyAsync(c->gen.p, recs.data(), recs.size() * sizeof(GenRecDev), hipMemcpyHostToDevice, st));
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(recs.size(), 65536);
+    hipLaunchKernelGGL(k_gen_fill, dim3(grid), dim3(256), 0, st, c->gen.p, (uint64_t)recs.size(), d_buf);
+    HIPCHK(hipGetLastError());
+    if (d_expected) {
+        const uint32_t g2 = (uint32_t)std::min<uint64_t>((recs.size() + 255) / 256, 65536);
+        hipLaunchKernelGGL(k_gen_manifest, dim3(g2), dim3(256), 0, st, c->gen.p, (uint64_t)recs.size(), c->crc.p, d_expected);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    return KVR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,381 @@
+"""kvreplay — Python bindings over the C ABI (include/kvreplay.h, include/kvstore_host.h).
+
+This mirrors the reference's replay surface (whispem/mini-kvstore-v2):
+  KVStore.open(dir)   -> src/store/engine.rs:24   (index rebuild on restart, replay on the GPU)
+  KVStore.get(key)    -> engine.rs:200
+  KVStore.stats()     -> engine.rs:237-259 (StoreStats, src/store/stats.rs:3-10)
+  CorruptedData       -> StoreError::CorruptedData (src/store/error.rs:11-12), same messages
+and exposes the engine itself (Context.replay) plus the synthetic generator.
+
+The native libraries are required: importing a function that needs them raises if
+lib/libkvreplay.so / lib/libkvhost.so are missing (there is no Python fallback).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_LIB = os.path.join(_PKG, "lib")
+
+# ---- status / kinds (kvreplay.h) -------------------------------------------------------------
+OK, CORRUPTED, CAPACITY = 0, 1, 2
+EINVAL, EHIP, EIO, ENOMEM = -1, -2, -3, -4
+E_NONE, E_OPEN, E_KEY_LEN, E_KEY, E_UTF8, E_VAL_LEN, E_VAL, E_OPCODE = range(8)
+KIND_NAMES = {0: "NONE", 1: "OPEN", 2: "KEY_LEN", 3: "KEY", 4: "UTF8", 5: "VAL_LEN", 6: "VAL", 7: "OPCODE"}
+SEGS_ON_DEVICE, OUT_ON_DEVICE, EXPECTED_ON_DEVICE = 0x1, 0x2, 0x4
+TF_VERIFIED, TF_CRC_FAIL = 0x1, 0x2
+
+TUPLE_DTYPE = np.dtype([("rec_off", "<u8"), ("seg_idx", "<u4"), ("key_len", "<u4"), ("val_len", "<u4"),
+                        ("crc32", "<u4"), ("key_tag", "<u4"), ("op", "u1"), ("flags", "u1"),
+                        ("reserved", "<u2")])
+assert TUPLE_DTYPE.itemsize == 32
+
+
+class Segment(C.Structure):
+    _fields_ = [("seg_id", C.c_uint64), ("bytes", C.c_void_p), ("len", C.c_uint64)]
+
+
+class Error(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("seg_idx", C.c_uint32), ("rec_off", C.c_uint64), ("aux", C.c_uint64)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("ms_total", C.c_double), ("ms_replay", C.c_double), ("ms_link", C.c_double),
+                ("ms_compact", C.c_double), ("bytes_in", C.c_uint64), ("n_records", C.c_uint64),
+                ("n_crc_fail", C.c_uint64), ("n_stripes", C.c_uint32), ("n_tiles", C.c_uint32),
+                ("n_redo", C.c_uint32), ("n_link_passes", C.c_uint32)]
+
+
+class GenParams(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("seg_bytes", C.c_uint64), ("key_space_log2", C.c_uint32),
+                ("key_dist", C.c_uint32), ("val_min", C.c_uint32), ("val_max", C.c_uint32),
+                ("del_permille", C.c_uint32), ("flip_per_million", C.c_uint32)]
+
+
+class StoreStats(C.Structure):
+    _fields_ = [("num_keys", C.c_uint64), ("num_segments", C.c_uint64), ("total_bytes", C.c_uint64),
+                ("active_segment_id", C.c_uint64), ("oldest_segment_id", C.c_uint64)]
+
+
+# ---- library loading ---------------------------------------------------------------------------
+_rep = None
+_host = None
+
+
+def lib_paths():
+    return os.path.join(_LIB, "libkvreplay.so"), os.path.join(_LIB, "libkvhost.so")
+
+
+def _load():
+    global _rep, _host
+    if _rep is not None:
+        return _rep, _host
+    rp, hp = lib_paths()
+    if not (os.path.exists(rp) and os.path.exists(hp)):
+        raise RuntimeError(f"kvreplay native libraries missing ({rp}); run __graft_entry__.build()")
+    rep = C.CDLL(rp, mode=C.RTLD_GLOBAL)
+    host = C.CDLL(hp)
+    P, U64, U32, SZ, I = C.c_void_p, C.c_uint64, C.c_uint32, C.c_size_t, C.c_int
+    rep.kvr_ctx_create.argtypes = [I, C.POINTER(P)]
+    rep.kvr_ctx_destroy.argtypes = [P]
+    rep.kvr_ctx_destroy.restype = None
+    rep.kvr_ctx_set_stream.argtypes = [P, P]
+    rep.kvr_ctx_device.argtypes = [P]
+    rep.kvr_replay.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
+    rep.kvr_last_stats.argtypes = [P, C.POINTER(Stats)]
+    rep.kvr_strerror.argtypes = [I]
+    rep.kvr_strerror.restype = C.c_char_p
+    rep.kvr_crc32.argtypes = [U32, P, SZ]
+    rep.kvr_crc32.restype = U32
+    rep.kvr_format_error.argtypes = [C.POINTER(Error), C.c_char_p, C.c_char_p, SZ]
+    rep.kvr_gen_segment_device.argtypes = [P, C.POINTER(GenParams), U64, P, U64, C.POINTER(U64), P, U64,
+                                           C.POINTER(U64)]
+    host.kvh_gen_segment.argtypes = [C.POINTER(GenParams), U64, P, U64, C.POINTER(U64), P, U64, C.POINTER(U64)]
+    host.kvh_discover.argtypes = [C.c_char_p, P, SZ, P, SZ, C.POINTER(SZ)]
+    host.kvh_parse_u64.argtypes = [C.c_char_p, SZ, C.POINTER(U64)]
+    host.kvh_fold.argtypes = [C.POINTER(Segment), P, SZ, P, C.POINTER(U64)]
+    host.kvh_fold.restype = U64
+    host.kvs_open.argtypes = [C.c_char_p, P, C.POINTER(P), C.POINTER(Error), C.c_char_p, SZ]
+    host.kvs_get.argtypes = [P, P, SZ, C.POINTER(P), C.POINTER(SZ)]
+    host.kvs_locate.argtypes = [P, P, SZ, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]
+    host.kvs_stats_get.argtypes = [P, C.POINTER(StoreStats)]
+    host.kvs_num_keys.argtypes = [P]
+    host.kvs_num_keys.restype = SZ
+    host.kvs_close.argtypes = [P]
+    host.kvs_close.restype = None
+    _rep, _host = rep, host
+    return rep, host
+
+
+def native():
+    """(libkvreplay, libkvhost) ctypes handles; raises if they are not built."""
+    return _load()
+
+
+# ---- errors ------------------------------------------------------------------------------------
+class CorruptedData(Exception):
+    """StoreError::CorruptedData (src/store/error.rs:11-12)."""
+
+    def __init__(self, kind, seg_idx, rec_off, aux, message=""):
+        self.kind, self.seg_idx, self.rec_off, self.aux = kind, seg_idx, rec_off, aux
+        self.message = message
+        super().__init__(f"Corrupted data: {message}" if message else
+                         f"Corrupted data: {KIND_NAMES.get(kind, kind)} in segment #{seg_idx} at {rec_off}")
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def format_error(kind, seg_idx, rec_off, aux, path):
+    rep, _ = _load()
+    e = Error(kind, seg_idx, rec_off, aux)
+    buf = C.create_string_buffer(8192)
+    rep.kvr_format_error(C.byref(e), path.encode(), buf, len(buf))
+    return buf.value.decode()
+
+
+def crc32(data: bytes, crc: int = 0) -> int:
+    rep, _ = _load()
+    a = np.frombuffer(bytes(data), dtype=np.uint8)
+    return int(rep.kvr_crc32(crc, a.ctypes.data if a.size else None, a.size))
+
+
+# ---- generator ---------------------------------------------------------------------------------
+@dataclass
+class GenSpec:
+    seed: int = 0x6B767265706C6179
+    seg_bytes: int = 64 << 20
+    key_space_log2: int = 20
+    key_dist: int = 0
+    val_min: int = 1024
+    val_max: int = 1024
+    del_permille: int = 0
+    flip_per_million: int = 0
+
+    def c(self):
+        return GenParams(self.seed, self.seg_bytes, self.key_space_log2, self.key_dist, self.val_min,
+                         self.val_max, self.del_permille, self.flip_per_million)
+
+
+def gen_segment_cpu(spec: GenSpec, seg_no: int):
+    """(bytes as uint8 ndarray, manifest uint32 ndarray) — byte-identical to the device generator."""
+    _, host = _load()
+    p = spec.c()
+    ln, nr = C.c_uint64(), C.c_uint64()
+    rc = host.kvh_gen_segment(C.byref(p), seg_no, None, 0, C.byref(ln), None, 0, C.byref(nr))
+    if rc != OK:
+        raise NativeError(rc)
+    buf = np.zeros(max(ln.value, 1), dtype=np.uint8)
+    exp = np.zeros(max(nr.value, 1), dtype=np.uint32)
+    rc = host.kvh_gen_segment(C.byref(p), seg_no, buf.ctypes.data, buf.size, C.byref(ln), exp.ctypes.data,
+                              exp.size, C.byref(nr))
+    if rc != OK:
+        raise NativeError(rc)
+    return buf[:ln.value], exp[:nr.value]
+
+
+def parse_u64(s: str):
+    _, host = _load()
+    b = s.encode()
+    out = C.c_uint64()
+    return int(out.value) if host.kvh_parse_u64(b, len(b), C.byref(out)) else None
+
+
+def discover(dirpath: str):
+    _, host = _load()
+    n = C.c_size_t()
+    host.kvh_discover(dirpath.encode(), None, 0, None, 0, C.byref(n))
+    ids = np.zeros(max(n.value, 1), dtype=np.uint64)
+    pbuf = C.create_string_buffer(max(n.value, 1) * 4200)
+    rc = host.kvh_discover(dirpath.encode(), ids.ctypes.data, ids.size, pbuf, len(pbuf), C.byref(n))
+    if rc != OK:
+        raise NativeError(rc)
+    paths = pbuf.raw.split(b"\0")[: n.value]
+    return [(int(ids[i]), paths[i].decode()) for i in range(n.value)]
+
+
+def fold(segments, tuples):
+    """Native last-writer-wins fold: (live mask, num_keys, total_bytes)."""
+    _, host = _load()
+    arrs = [np.ascontiguousarray(np.frombuffer(s, dtype=np.uint8) if isinstance(s, (bytes, bytearray)) else s)
+            for s in segments]
+    segs = (Segment * max(len(arrs), 1))(*[Segment(i, a.ctypes.data if a.size else None, a.size)
+                                            for i, a in enumerate(arrs)])
+    t = np.ascontiguousarray(tuples, dtype=TUPLE_DTYPE)
+    live = np.zeros(max(len(t), 1), dtype=np.uint8)
+    tb = C.c_uint64()
+    nk = host.kvh_fold(segs, t.ctypes.data if len(t) else None, len(t), live.ctypes.data, C.byref(tb))
+    return live[: len(t)].astype(bool), int(nk), int(tb.value)
+
+
+# ---- the engine --------------------------------------------------------------------------------
+@dataclass
+class ReplayResult:
+    status: int
+    tuples: np.ndarray | None
+    n: int
+    error: Error | None
+    stats: Stats
+
+
+class Context:
+    """One kvr_ctx on one HIP device."""
+
+    def __init__(self, device: int = 0):
+        rep, _ = _load()
+        self._rep = rep
+        h = C.c_void_p()
+        rc = rep.kvr_ctx_create(device, C.byref(h))
+        if rc != OK:
+            raise NativeError(f"kvr_ctx_create({device}) failed: {rep.kvr_strerror(rc).decode()} ({rc})")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._rep.kvr_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr: int | None):
+        self._rep.kvr_ctx_set_stream(self.h, stream_ptr)
+
+    def last_stats(self) -> Stats:
+        s = Stats()
+        self._rep.kvr_last_stats(self.h, C.byref(s))
+        return s
+
+    def replay(self, segments, seg_ids=None, expected=None, cap=None, on_device=False, out_ptr=None,
+               expected_on_device=False):
+        """Replay host segments (list of bytes / uint8 arrays), or device segments given as
+        (ptr, len) pairs with on_device=True.  Returns ReplayResult; tuples is a numpy
+        TUPLE_DTYPE array unless out_ptr (device memory) is given."""
+        n = len(segments)
+        keep = []
+        segs = (Segment * max(n, 1))()
+        total = 0
+        for i, s in enumerate(segments):
+            sid = seg_ids[i] if seg_ids is not None else i
+            if on_device:
+                ptr, ln = s
+            else:
+                a = np.frombuffer(s, dtype=np.uint8) if isinstance(s, (bytes, bytearray)) else np.ascontiguousarray(s)
+                keep.append(a)
+                ptr, ln = (a.ctypes.data if a.size else None), a.size
+            segs[i] = Segment(sid, ptr, ln)
+            total += ln
+        flags = (SEGS_ON_DEVICE if on_device else 0)
+        exp_ptr, n_exp = None, 0
+        if expected is not None:
+            if expected_on_device:
+                exp_ptr, n_exp = expected
+                flags |= EXPECTED_ON_DEVICE
+            else:
+                e = np.ascontiguousarray(expected, dtype=np.uint32)
+                keep.append(e)
+                exp_ptr, n_exp = (e.ctypes.data if e.size else None), e.size
+        if cap is None:
+            cap = max(1024, total // 24 + n)
+        out_arr = None
+        if out_ptr is not None:
+            flags |= OUT_ON_DEVICE
+            outp = out_ptr
+        else:
+            out_arr = np.zeros(cap, dtype=TUPLE_DTYPE)
+            outp = out_arr.ctypes.data
+        n_out = C.c_size_t()
+        err = Error()
+        rc = self._rep.kvr_replay(self.h, segs, n, flags, exp_ptr, n_exp, outp, cap, C.byref(n_out), C.byref(err))
+        if rc == CAPACITY and out_ptr is None:
+            return self.replay(segments, seg_ids, expected, cap=n_out.value + 16, on_device=on_device,
+                               expected_on_device=expected_on_device)
+        if rc < 0:
+            raise NativeError(f"kvr_replay: {self._rep.kvr_strerror(rc).decode()} ({rc})")
+        tuples = out_arr[: n_out.value] if out_arr is not None and rc == OK else None
+        return ReplayResult(rc, tuples, n_out.value, err if rc == CORRUPTED else None, self.last_stats())
+
+    def gen_segment_device(self, spec: GenSpec, seg_no: int, d_buf: int, cap: int, d_expected=None,
+                           exp_cap=0):
+        p = spec.c()
+        ln, nr = C.c_uint64(), C.c_uint64()
+        rc = self._rep.kvr_gen_segment_device(self.h, C.byref(p), seg_no, d_buf, cap, C.byref(ln), d_expected,
+                                              exp_cap, C.byref(nr))
+        if rc != OK:
+            raise NativeError(f"kvr_gen_segment_device: {rc} (len {ln.value}, records {nr.value})")
+        return ln.value, nr.value
+
+
+def gen_segment_size(spec: GenSpec, seg_no: int):
+    _, host = _load()
+    p = spec.c()
+    ln, nr = C.c_uint64(), C.c_uint64()
+    host.kvh_gen_segment(C.byref(p), seg_no, None, 0, C.byref(ln), None, 0, C.byref(nr))
+    return ln.value, nr.value
+
+
+# ---- KVStore mirror ----------------------------------------------------------------------------
+class KVStore:
+    """The reference's KVStore::open / get / stats path with replay on the GPU."""
+
+    def __init__(self, handle, ctx):
+        self._h = handle
+        self._ctx = ctx
+        _, self._host = _load()
+
+    @classmethod
+    def open(cls, dirpath: str, ctx: Context | None = None):
+        _, host = _load()
+        ctx = ctx or Context(0)
+        h = C.c_void_p()
+        err = Error()
+        msg = C.create_string_buffer(8192)
+        rc = host.kvs_open(str(dirpath).encode(), ctx.h, C.byref(h), C.byref(err), msg, len(msg))
+        if rc == CORRUPTED:
+            raise CorruptedData(err.kind, err.seg_idx, err.rec_off, err.aux, msg.value.decode())
+        if rc != OK:
+            raise NativeError(f"kvs_open: {rc}")
+        return cls(h, ctx)
+
+    def get(self, key):
+        kb = key.encode() if isinstance(key, str) else bytes(key)
+        a = np.frombuffer(kb, dtype=np.uint8)
+        vp, vl = C.c_void_p(), C.c_size_t()
+        found = self._host.kvs_get(self._h, a.ctypes.data if a.size else None, a.size, C.byref(vp), C.byref(vl))
+        if not found:
+            return None
+        return C.string_at(vp.value, vl.value) if vl.value else b""
+
+    def locate(self, key):
+        kb = key.encode() if isinstance(key, str) else bytes(key)
+        a = np.frombuffer(kb, dtype=np.uint8)
+        sid, off, ln = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        if not self._host.kvs_locate(self._h, a.ctypes.data if a.size else None, a.size, C.byref(sid),
+                                     C.byref(off), C.byref(ln)):
+            return None
+        return int(sid.value), int(off.value), int(ln.value)
+
+    def stats(self):
+        s = StoreStats()
+        self._host.kvs_stats_get(self._h, C.byref(s))
+        return s
+
+    def close(self):
+        if self._h:
+            self._host.kvs_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

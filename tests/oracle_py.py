@@ -1,0 +1,105 @@
+"""ctypes access to the CPU oracle (oracle/replay_ref.c -> oracle/liboracle.so).
+
+TEST INFRASTRUCTURE: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use
+this module, and only as the checker.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+
+import sys  # noqa: E402
+
+sys.path.insert(0, os.path.join(ROOT, "mini-kvstore-v2_amd"))
+from kvreplay import TUPLE_DTYPE, Error  # noqa: E402
+
+_lib = None
+
+
+class OSeg(C.Structure):
+    _fields_ = [("seg_id", C.c_uint64), ("bytes", C.c_void_p), ("len", C.c_uint64)]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            raise RuntimeError("oracle/liboracle.so not built (run __graft_entry__.build())")
+        L = C.CDLL(ORACLE_SO)
+        L.oracle_crc32.argtypes = [C.c_uint32, C.c_void_p, C.c_size_t]
+        L.oracle_crc32.restype = C.c_uint32
+        L.oracle_utf8_check.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+        L.oracle_replay.argtypes = [C.POINTER(OSeg), C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                    C.POINTER(C.c_size_t), C.POINTER(Error)]
+        L.oracle_fold_live.argtypes = [C.POINTER(OSeg), C.c_void_p, C.c_size_t, C.c_void_p, C.POINTER(C.c_uint64)]
+        L.oracle_fold_live.restype = C.c_size_t
+        L.oracle_replay_faithful.argtypes = [C.POINTER(OSeg), C.c_size_t, C.POINTER(C.c_uint64),
+                                             C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                             C.POINTER(Error)]
+        _lib = L
+    return _lib
+
+
+def _as_u8(s):
+    if isinstance(s, (bytes, bytearray)):
+        return np.frombuffer(bytes(s), dtype=np.uint8)
+    return np.ascontiguousarray(s, dtype=np.uint8)
+
+
+def _segs(segments, seg_ids=None):
+    arrs = [_as_u8(s) for s in segments]
+    segs = (OSeg * max(len(arrs), 1))()
+    for i, a in enumerate(arrs):
+        segs[i] = OSeg(seg_ids[i] if seg_ids else i, a.ctypes.data if a.size else None, a.size)
+    return arrs, segs
+
+
+def crc32(data, crc=0):
+    a = _as_u8(data)
+    return int(lib().oracle_crc32(crc, a.ctypes.data if a.size else None, a.size))
+
+
+def utf8_check(data):
+    """(ok, valid_up_to, error_len) with error_len 0 meaning 'incomplete' (Rust None)."""
+    a = _as_u8(data)
+    vu, el = C.c_uint64(), C.c_uint32()
+    ok = lib().oracle_utf8_check(a.ctypes.data if a.size else None, a.size, C.byref(vu), C.byref(el))
+    return bool(ok), int(vu.value), int(el.value)
+
+
+def replay(segments, expected=None, seg_ids=None):
+    """-> (status, tuples ndarray, Error).  Tuples are those walked before the first error."""
+    arrs, segs = _segs(segments, seg_ids)
+    total = sum(a.size for a in arrs)
+    cap = total // 5 + 16
+    out = np.zeros(cap, dtype=TUPLE_DTYPE)
+    n = C.c_size_t()
+    err = Error()
+    e = None
+    if expected is not None:
+        e = np.ascontiguousarray(expected, dtype=np.uint32)
+    rc = lib().oracle_replay(segs, len(arrs), e.ctypes.data if e is not None and e.size else None,
+                             0 if e is None else e.size, out.ctypes.data, cap, C.byref(n), C.byref(err))
+    return rc, out[: min(n.value, cap)], err
+
+
+def fold_live(segments, tuples):
+    arrs, segs = _segs(segments)
+    t = np.ascontiguousarray(tuples, dtype=TUPLE_DTYPE)
+    live = np.zeros(max(len(t), 1), dtype=np.uint8)
+    tb = C.c_uint64()
+    nk = lib().oracle_fold_live(segs, t.ctypes.data if len(t) else None, len(t), live.ctypes.data, C.byref(tb))
+    return live[: len(t)].astype(bool), int(nk), int(tb.value)
+
+
+def replay_faithful(segments):
+    """The reference's cost model (CPU baseline). -> (rc, num_keys, total_bytes, n_records, digest, Error)"""
+    arrs, segs = _segs(segments)
+    nk, tb, nr, dg = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+    err = Error()
+    rc = lib().oracle_replay_faithful(segs, len(arrs), C.byref(nk), C.byref(tb), C.byref(nr), C.byref(dg),
+                                      C.byref(err))
+    return rc, nk.value, tb.value, nr.value, dg.value, err

@@ -1,0 +1,190 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle, bit-exact.
+
+Every tuple field (rec_off, seg_idx, key_len, val_len, crc32, key_tag, op, flags) and every
+error (kind, segment, offset, aux) must equal the oracle's on the same bytes.
+"""
+import os
+import random
+import shutil
+import zlib
+
+import numpy as np
+import pytest
+
+import kvreplay as K
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+KIND = {"NONE": 0, "OPEN": 1, "KEY_LEN": 2, "KEY": 3, "UTF8": 4, "VAL_LEN": 5, "VAL": 6, "OPCODE": 7}
+
+
+def rec_set(k, v):
+    return b"\x00" + len(k).to_bytes(4, "little") + k + len(v).to_bytes(4, "little") + v
+
+
+def rec_del(k):
+    return b"\x01" + len(k).to_bytes(4, "little") + k
+
+
+def read_dir(name):
+    d = os.path.join(GOLD, name)
+    names = sorted((n for n in os.listdir(d) if n.startswith("segment-")), key=lambda n: int(n[8:-4]))
+    return [int(n[8:-4]) for n in names], [open(os.path.join(d, n), "rb").read() for n in names]
+
+
+def check_parity(ctx, segs, expected=None, seg_ids=None):
+    ro = O.replay(segs, expected=expected, seg_ids=seg_ids)
+    rg = ctx.replay(segs, seg_ids=seg_ids, expected=expected)
+    assert rg.status == ro[0], (rg.status, ro[0], ro[2].kind, ro[2].rec_off)
+    if ro[0] == 0:
+        assert rg.n == len(ro[1])
+        a, b = rg.tuples, ro[1]
+        if not np.array_equal(a, b):
+            bad = np.nonzero(a != b)[0][:5]
+            raise AssertionError(f"tuple mismatch at {bad}: gpu={a[bad]} oracle={b[bad]}")
+    else:
+        eo, eg = ro[2], rg.error
+        assert (eg.kind, eg.seg_idx, eg.rec_off, eg.aux) == (eo.kind, eo.seg_idx, eo.rec_off, eo.aux)
+    return rg
+
+
+@pytest.mark.parametrize("name", ["persistence", "store_integration", "compaction_example", "large_dataset"])
+def test_golden_dirs(gctx, name):
+    ids, segs = read_dir(name)
+    check_parity(gctx, segs, seg_ids=ids)
+    if name == "persistence":   # config 1: replay of segment-1 alone
+        check_parity(gctx, segs[:1], seg_ids=ids[:1])
+
+
+def test_negative_cases(gctx, golden):
+    for c in golden["negative"]:
+        data = bytes.fromhex(c["hex"])
+        rg = check_parity(gctx, [data])
+        if c["kind"] != "NONE":
+            assert rg.error.kind == KIND[c["kind"]], c["name"]
+        # the same failure behind a good segment, and with the bad one first
+        check_parity(gctx, [read_dir("store_integration")[1][0], data])
+        check_parity(gctx, [data, read_dir("compaction_example")[1][0]])
+
+
+SPECS = {
+    "cfg2_1k": K.GenSpec(seed=21, seg_bytes=700_000, val_min=1024, val_max=1024),
+    "cfg3_64k": K.GenSpec(seed=31, seg_bytes=1_500_000, val_min=65536, val_max=65536),
+    "cfg4_del": K.GenSpec(seed=41, seg_bytes=600_000, val_min=1024, val_max=1024, del_permille=500),
+    "cfg5_zipf": K.GenSpec(seed=51, seg_bytes=3_000_000, key_dist=1, key_space_log2=24, val_min=16,
+                           val_max=1 << 20, del_permille=100),
+    "tiny": K.GenSpec(seed=61, seg_bytes=200_000, val_min=0, val_max=40, del_permille=300),
+    "flips": K.GenSpec(seed=71, seg_bytes=400_000, val_min=16, val_max=9000, flip_per_million=50_000),
+}
+
+
+@pytest.mark.parametrize("name", list(SPECS))
+def test_generated_parity(gctx, name):
+    spec = SPECS[name]
+    segs, exps = zip(*[K.gen_segment_cpu(spec, s) for s in range(3)])
+    exp = np.concatenate(exps)
+    rg = check_parity(gctx, list(segs), expected=exp)
+    if name == "flips":
+        assert rg.stats.n_crc_fail > 0
+        assert rg.stats.n_crc_fail == int(np.sum((rg.tuples["flags"] & K.TF_CRC_FAIL) != 0))
+    else:
+        assert rg.stats.n_crc_fail == 0
+
+
+def test_adversarial_speculation(gctx):
+    """Values that look like records defeat the speculative entry; results must stay exact."""
+    inner = b"".join(rec_set(b"k%d" % i, b"v" * (i % 50)) for i in range(4000))       # a segment in a value
+    zeros = bytes(200_000)                                                              # 9-byte empty SETs
+    rng = random.Random(5)
+    parts = []
+    for i in range(60):
+        kind = i % 3
+        v = inner if kind == 0 else zeros if kind == 1 else bytes(rng.getrandbits(8) for _ in range(3000))
+        parts.append(rec_set(b"key%d" % i, v[: rng.randint(1, len(v))]))
+        if i % 7 == 0:
+            parts.append(rec_del(b"key%d" % (i // 2)))
+    seg = b"".join(parts)
+    check_parity(gctx, [seg, seg[: len(seg) // 2 + 13], inner, zeros])
+
+
+def test_random_truncations_and_corruptions(gctx):
+    spec = K.GenSpec(seed=81, seg_bytes=400_000, val_min=1, val_max=3000, del_permille=200)
+    base, _ = K.gen_segment_cpu(spec, 0)
+    base = base.tobytes()
+    rc, t, _ = O.replay([base])
+    offs = t["rec_off"].astype(np.int64)
+    rng = random.Random(9)
+    for trial in range(24):
+        b = bytearray(base)
+        mode = trial % 4
+        j = rng.randrange(len(offs))
+        o = int(offs[j])
+        if mode == 0:
+            b = b[: o + rng.randint(1, 40)]                  # torn tail inside a record
+        elif mode == 1:
+            b[o] = rng.choice([2, 3, 0x7F, 0xFF])            # bad opcode
+        elif mode == 2:
+            b[o + 5 + rng.randrange(16)] = 0xFF              # invalid UTF-8 in a key
+        else:
+            b[o + 1: o + 5] = (len(b)).to_bytes(4, "little")  # key length past the end
+        good, _ = K.gen_segment_cpu(spec, 1)
+        check_parity(gctx, [good.tobytes(), bytes(b), good.tobytes()])
+
+
+def test_device_segments_at_odd_alignment(gctx):
+    torch = pytest.importorskip("torch")
+    spec = SPECS["cfg5_zipf"]
+    segs = [K.gen_segment_cpu(spec, s)[0] for s in range(3)]
+    rc, ref, _ = O.replay(segs)
+    buf = torch.zeros(sum(len(s) for s in segs) + 4096, dtype=torch.uint8, device="cuda")
+    ptrs, off = [], 3
+    for s in segs:
+        buf[off: off + len(s)] = torch.from_numpy(s).cuda()
+        ptrs.append((buf.data_ptr() + off, len(s)))
+        off += len(s) + 7
+    torch.cuda.synchronize()
+    rg = gctx.replay(ptrs, on_device=True)
+    assert rg.status == 0 and np.array_equal(rg.tuples, ref)
+
+
+def test_device_generator_matches_cpu(gctx):
+    torch = pytest.importorskip("torch")
+    for spec in (SPECS["cfg5_zipf"], SPECS["flips"], SPECS["cfg4_del"]):
+        for seg_no in (0, 3):
+            b, e = K.gen_segment_cpu(spec, seg_no)
+            d = torch.zeros(len(b) + 64, dtype=torch.uint8, device="cuda")
+            de = torch.zeros(len(e) + 4, dtype=torch.int32, device="cuda")
+            ln, nr = gctx.gen_segment_device(spec, seg_no, d.data_ptr(), d.numel(), de.data_ptr(), de.numel())
+            torch.cuda.synchronize()
+            assert (ln, nr) == (len(b), len(e))
+            assert np.array_equal(d[:ln].cpu().numpy(), b)
+            assert np.array_equal(de[:nr].cpu().numpy().view(np.uint32), e)
+
+
+def test_kvstore_open_golden(gctx, tmp_path):
+    d = tmp_path / "persisted_store"
+    shutil.copytree(os.path.join(GOLD, "persistence"), d)
+    s = K.KVStore.open(str(d), gctx)
+    assert s.get("session") == b"first" and s.get("counter") == b"43" and s.get("name") is None
+    assert s.locate("counter") == (2, 16, 2)
+    st = s.stats()
+    assert (st.num_keys, st.total_bytes, st.active_segment_id) == (2, 7, 4)
+    assert st.num_segments == 4                       # segment-1..3 + the new active segment-4
+    s.close()
+    d2 = tmp_path / "large"
+    shutil.copytree(os.path.join(GOLD, "large_dataset"), d2)
+    s = K.KVStore.open(str(d2), gctx)
+    assert s.get("user:05000:data") == b"User data for ID 5000" and s.stats().num_keys == 10000
+    s.close()
+
+
+def test_kvstore_open_reports_reference_message(gctx, tmp_path):
+    d = tmp_path / "db"
+    d.mkdir()
+    (d / "segment-1.dat").write_bytes(rec_set(b"a", b"1"))
+    (d / "segment-2.dat").write_bytes(rec_set(b"b", b"2") + b"\x00\x05\x00")
+    with pytest.raises(K.CorruptedData) as ei:
+        K.KVStore.open(str(d), gctx)
+    assert str(ei.value) == f"Corrupted data: Failed to read key length in {d}/segment-2.dat: failed to fill whole buffer"
