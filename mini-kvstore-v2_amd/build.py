@@ -40,7 +40,7 @@ def _deps(*names):
 def build(force=False, verbose=False):
     os.makedirs(LIB, exist_ok=True)
     rep = os.path.join(LIB, "libkvreplay.so")
-    deps = _deps("kvr_api.hip", "kvr_kernels.hip", "kvr_device.h", "kvr_gen_common.h")
+    deps = _deps(*[f for f in os.listdir(CSRC) if f.endswith((".hip", ".h"))])
     if force or _newer(rep, deps):
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
               "-Wall", "-Wno-unused-result", "-o", rep, os.path.join(CSRC, "kvr_api.hip")])

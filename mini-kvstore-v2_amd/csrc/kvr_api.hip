@@ -16,6 +16,7 @@
 #include <cstring>
 #include <vector>
 
+#include "kvr_replay_kernel.hip"
 #include "kvr_kernels.hip"
 
 using namespace kvr;
@@ -59,13 +60,14 @@ struct kvr_ctx {
     DevBuf<Counters> ctr;
     DevBuf<uint32_t> seg_bad, seg_err, expected;
     DevBuf<uint64_t> bsum;
-    DevBuf<uint32_t> crc, pw16, pw1;
+    DevBuf<uint32_t> crc, pw16, pw1, nib, xw;
     DevBuf<GenRecDev> gen;
     LinkResult *h_link = nullptr;
     Counters *h_ctr = nullptr;
     std::vector<SegDesc> h_segs;
     std::vector<StripeDesc> h_stripes;
     uint64_t pool_hint = 0;
+    uint32_t tps_override = 0;
     kvr_stats stats{};
 };
 
@@ -77,7 +79,8 @@ struct kvr_ctx {
 // ---------------------------------------------------------------------------------------
 // tables: slice-by-16 CRC tables and the shift operators X(n) = x^(8n) mod P
 // ---------------------------------------------------------------------------------------
-static void build_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &pw16, std::vector<uint32_t> &pw1) {
+static void build_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &pw16, std::vector<uint32_t> &pw1,
+                         std::vector<uint32_t> &nib, std::vector<uint32_t> &xw) {
     crc.assign(16 * 256, 0);
     for (uint32_t i = 0; i < 256; ++i) {
         uint32_t c = i;
@@ -96,6 +99,21 @@ static void build_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &pw16
     pw16.assign(TILE / 16 + 4, 0);
     pw16[0] = 0x80000000u;
     for (size_t k = 1; k < pw16.size(); ++k) pw16[k] = gf_mul(pw16[k - 1], x16);
+    // nibble tables: nib[(d * 2 + h) * 16 + n] = T_d[n << 4h]
+    nib.assign(16 * 32, 0);
+    for (int d = 0; d < 16; ++d)
+        for (int n = 0; n < 16; ++n) {
+            nib[(d * 2 + 0) * 16 + n] = crc[d * 256 + n];
+            nib[(d * 2 + 1) * 16 + n] = crc[d * 256 + (n << 4)];
+        }
+    // exponentiation windows: xw[i * 16 + j] = X(j * 16^i)
+    xw.assign(8 * 16, 0);
+    uint32_t base = pw1[1];   // X(1)
+    for (int i = 0; i < 8; ++i) {
+        xw[i * 16 + 0] = GF_ONE;
+        for (int j = 1; j < 16; ++j) xw[i * 16 + j] = gf_mul(xw[i * 16 + j - 1], base);
+        base = gf_mul(xw[i * 16 + 15], base);   // X(16^(i+1))
+    }
 }
 
 extern "C" {
@@ -171,13 +189,18 @@ int kvr_ctx_create(int device, kvr_ctx **out) {
     for (auto &e : c->ev) if (hipEventCreate(&e) != hipSuccess) { delete c; return KVR_EHIP; }
     if (hipHostMalloc(reinterpret_cast<void **>(&c->h_link), sizeof(LinkResult)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void **>(&c->h_ctr), sizeof(Counters)) != hipSuccess) { delete c; return KVR_ENOMEM; }
-    std::vector<uint32_t> crc, pw16, pw1;
-    build_tables(crc, pw16, pw1);
+    std::vector<uint32_t> crc, pw16, pw1, nib, xw;
+    build_tables(crc, pw16, pw1, nib, xw);
     if (c->crc.ensure(crc.size()) || c->pw16.ensure(pw16.size()) || c->pw1.ensure(pw1.size()) ||
-        c->link.ensure(1) || c->ctr.ensure(1)) { kvr_ctx_destroy(c); return KVR_ENOMEM; }
+        c->nib.ensure(nib.size()) || c->xw.ensure(xw.size()) || c->link.ensure(1) || c->ctr.ensure(1)) {
+        kvr_ctx_destroy(c);
+        return KVR_ENOMEM;
+    }
     if (hipMemcpy(c->crc.p, crc.data(), crc.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->pw16.p, pw16.data(), pw16.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(c->pw1.p, pw1.data(), pw1.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(c->pw1.p, pw1.data(), pw1.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->nib.p, nib.data(), nib.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->xw.p, xw.data(), xw.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
         kvr_ctx_destroy(c);
         return KVR_EHIP;
     }
@@ -192,7 +215,7 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->arena.release(); c->segs.release(); c->stripes.release(); c->sres.release(); c->tres.release();
     c->pool.release(); c->dense.release(); c->redo.release(); c->link.release(); c->ctr.release();
     c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->bsum.release();
-    c->crc.release(); c->pw16.release(); c->pw1.release(); c->gen.release();
+    c->crc.release(); c->pw16.release(); c->pw1.release(); c->nib.release(); c->xw.release(); c->gen.release();
     if (c->h_link) (void)hipHostFree(c->h_link);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
@@ -207,6 +230,12 @@ int kvr_ctx_set_stream(kvr_ctx *c, void *s) {
 }
 
 int kvr_ctx_device(const kvr_ctx *c) { return c ? c->device : -1; }
+
+int kvr_ctx_set_tiles_per_stripe(kvr_ctx *c, uint32_t tiles) {
+    if (!c) return KVR_EINVAL;
+    c->tps_override = tiles;
+    return KVR_OK;
+}
 
 int kvr_last_stats(const kvr_ctx *c, kvr_stats *out) {
     if (!c || !out) return KVR_EINVAL;
@@ -267,7 +296,7 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
     }
     if (total_tiles >= 0xFFFFFFFFull) return KVR_EINVAL;
     const uint64_t target = (uint64_t)c->n_cu * 8;
-    const uint64_t tps = std::max<uint64_t>(1, (total_tiles + target - 1) / target);
+    const uint64_t tps = c->tps_override ? c->tps_override : std::max<uint64_t>(1, (total_tiles + target - 1) / target);
     c->h_stripes.clear();
     for (size_t i = 0; i < n; ++i) {
         SegDesc &g = c->h_segs[i];
@@ -306,8 +335,13 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         }
     }
 
-    for (int attempt = 0; attempt < 4; ++attempt) {
-        const uint64_t pool_cap = std::max<uint64_t>(c->pool_hint, std::max<uint64_t>(65536, total_bytes / 192 + n));
+    const Tables tb{c->crc.p, c->nib.p, c->pw16.p, c->pw1.p, c->xw.p};
+    for (int attempt = 0; attempt < 10; ++attempt) {
+        // each workgroup claims pool space in chunks of >= pool_chunk tuples: budget one partly
+        // used chunk per stripe on top of the expected record count
+        const uint32_t pool_chunk = (uint32_t)std::min<uint64_t>(POOL_CHUNK, std::max<uint64_t>(256, tps * (TILE / 64)));
+        const uint64_t pool_cap = std::max<uint64_t>(
+            c->pool_hint, std::max<uint64_t>(65536, total_bytes / 192 + n + (uint64_t)n_stripes * pool_chunk));
         if (c->pool.ensure(pool_cap)) return KVR_ENOMEM;
         kvr_tuple *d_out;
         uint64_t out_cap;
@@ -323,15 +357,14 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         HIPCHK(hipMemsetAsync(c->link.p, 0, sizeof(LinkResult), st));
         HIPCHK(hipEventRecord(c->ev[0], st));
         hipLaunchKernelGGL(k_replay, dim3(n_stripes), dim3(NT), 0, st, c->segs.p, c->stripes.p, c->sres.p, c->tres.p,
-                           c->pool.p, pool_cap, c->ctr.p, c->crc.p, c->pw16.p, c->pw1.p, c->redo.p, c->link.p, 0);
+                           c->pool.p, pool_cap, c->ctr.p, tb, c->redo.p, c->link.p, 0, pool_chunk);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[1], st));
         hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
                            c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_replay, dim3(std::min(n_stripes, REDO_GRID)), dim3(NT), 0, st, c->segs.p, c->stripes.p,
-                           c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, c->crc.p, c->pw16.p, c->pw1.p,
-                           c->redo.p, c->link.p, 1);
+                           c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, c->redo.p, c->link.p, 1, pool_chunk);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
                            c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p);
@@ -354,19 +387,54 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         // rare: more re-walk rounds (a speculated entry was wrong twice in a row)
         uint32_t guard = 0;
         bool recompact = false;
+        const bool dbg = getenv("KVR_DEBUG") != nullptr;
+        if (dbg)
+            fprintf(stderr, "kvr: pass1 status=%d n_redo=%u first_problem=%u passes=%u overflow=%u\n",
+                    c->h_link->status, c->h_link->n_redo, c->h_link->first_problem_seg, c->h_link->passes,
+                    c->h_ctr->overflow);
+        if (c->h_ctr->overflow & 1u) {   // pool too small: grow to what this pass needed and run again
+            c->pool_hint = std::max<uint64_t>(c->h_ctr->pool_cursor, pool_cap) * 2;
+            continue;
+        }
         while (c->h_link->status == 3 && guard++ < n_stripes + 4) {
             hipLaunchKernelGGL(k_replay, dim3(std::min(n_stripes, REDO_GRID)), dim3(NT), 0, st, c->segs.p, c->stripes.p,
-                               c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, c->crc.p, c->pw16.p, c->pw1.p,
-                               c->redo.p, c->link.p, 1);
+                               c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, c->redo.p, c->link.p, 1, pool_chunk);
             hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes,
                                c->sres.p, c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p);
             HIPCHK(hipGetLastError());
             HIPCHK(hipMemcpyAsync(c->h_link, c->link.p, sizeof(LinkResult), hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
             recompact = true;
+            if (c->h_ctr->overflow) break;
+            if (dbg) {
+                fprintf(stderr, "kvr: round %u status=%d n_redo=%u first_problem=%u\n", guard, c->h_link->status,
+                        c->h_link->n_redo, c->h_link->first_problem_seg);
+                if (guard < 6 || guard % 50 == 0) {
+                    std::vector<RedoEnt> rl(c->h_link->n_redo);
+                    std::vector<StripeRes> sr(n_stripes);
+                    (void)hipMemcpy(rl.data(), c->redo.p, rl.size() * sizeof(RedoEnt), hipMemcpyDeviceToHost);
+                    (void)hipMemcpy(sr.data(), c->sres.p, sr.size() * sizeof(StripeRes), hipMemcpyDeviceToHost);
+                    for (auto &r : rl) {
+                        const StripeDesc &d = c->h_stripes[r.stripe];
+                        fprintf(stderr, "   redo stripe %u seg %u tiles [%u,%u) forced %llu | now entry %lld exit %lld err %u@%lld\n",
+                                r.stripe, d.seg, d.t_begin, d.t_end, (unsigned long long)r.entry,
+                                (long long)sr[r.stripe].entry, (long long)sr[r.stripe].exit, sr[r.stripe].err_kind,
+                                (long long)sr[r.stripe].err_pos);
+                    }
+                }
+            }
         }
-        if (c->h_link->status == 3) return KVR_EHIP;   // cannot happen: each round fixes one stripe
-        if (recompact && c->h_link->status == 0) {
+        c->stats.n_redo = guard;
+        if (c->h_ctr->overflow & 4u) {   // bug trap: an imposed entry before its stripe
+            fprintf(stderr, "kvr: stripe re-walk got an entry before the stripe\n");
+            return KVR_EHIP;
+        }
+        if (c->h_link->status == 3 && !(c->h_ctr->overflow & 1u)) {   // cannot happen: each round fixes one stripe (bug trap)
+            fprintf(stderr, "kvr: stripe linking did not converge after %u rounds\n", guard);
+            return KVR_EHIP;
+        }
+        if (recompact && c->h_link->status == 0 && !c->h_ctr->overflow) {
             hipLaunchKernelGGL(k_tsum, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->link.p);
             hipLaunchKernelGGL(k_tscan, dim3(1), dim3(1024), 0, st, c->bsum.p, nb, c->ctr.p, c->link.p);
             hipLaunchKernelGGL(k_compact, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->pool.p, pool_cap,
@@ -376,9 +444,12 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
             HIPCHK(hipStreamSynchronize(st));
         }
         c->stats.n_link_passes = c->h_link->passes;
-        if (c->h_ctr->overflow & 2u) return KVR_EHIP;   // stitch did not converge (bug trap)
+        if (c->h_ctr->overflow & 2u) {   // stitch did not converge (bug trap)
+            fprintf(stderr, "kvr: tile stitch did not converge\n");
+            return KVR_EHIP;
+        }
         if (c->h_ctr->overflow & 1u) {   // pool too small: grow to what this pass needed and run again
-            c->pool_hint = c->h_ctr->pool_cursor + c->h_ctr->pool_cursor / 8 + 4096;
+            c->pool_hint = std::max<uint64_t>(c->h_ctr->pool_cursor, pool_cap) * 2;
             continue;
         }
         if (c->h_link->status == 1) {
@@ -404,6 +475,21 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         return total > cap ? KVR_CAPACITY : KVR_OK;
     }
     return KVR_ENOMEM;
+}
+
+// diagnostic build only (-DKVR_PROF): per-phase cycle sums of k_replay's tile loop
+int kvr_prof_read(unsigned long long *out, int reset) {
+#ifdef KVR_PROF
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), 16 * 8) != hipSuccess) return KVR_EHIP;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return KVR_EHIP;
+    }
+    return KVR_OK;
+#else
+    (void)out; (void)reset;
+    return KVR_EINVAL;
+#endif
 }
 
 int kvr_gen_segment_device(kvr_ctx *c, const kvr_gen_params *p, uint64_t seg_no, uint8_t *d_buf, uint64_t cap,

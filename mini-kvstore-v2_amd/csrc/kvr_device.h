@@ -3,16 +3,16 @@
  *
  * Geometry:
  *   - A workgroup (NT = 256 threads = 4 waves) owns one STRIPE: a run of consecutive TILEs of
- *     one segment.  It walks them in order, so the record chain is exact inside a stripe;
- *     only the stripe's first entry is speculated (and verified by k_link).
- *   - A TILE (32 KiB) is staged HBM -> LDS with coalesced 16-B loads.  Its framing is walked
- *     in parallel: each thread speculates a chain through its 128-B SUB-CHUNK, wave 0 stitches
- *     the 256 sub-chains with a composition scan and repairs mismatches serially.
- *   - CRC-32 (reflected 0xEDB88320, crc32fast semantics, storage.rs:27) uses LDS-resident
- *     slice-by-16 tables.  Values of at most SMALL bytes that lie inside the tile are CRC'd by
- *     the thread that walked them; longer values become PIECES whose bytes are split into
- *     128-B UNITs (one per thread); unit CRCs are shifted into place with one GF(2)
- *     multiplication by a tabulated x^(128k) and XOR-combined in LDS.
+ *     one segment, walked in order, so the record chain is exact inside a stripe and only the
+ *     stripe's first entry is speculated (verified by k_link).
+ *   - A TILE (16 KiB) is streamed HBM -> LDS by LDS-DMA, one tile ahead of the one being
+ *     processed.  Its framing is walked in parallel: each thread speculates a chain through its
+ *     64-B SUB-CHUNK; wave 0 stitches the 256 sub-chains by pointer jumping.
+ *   - CRC-32 (reflected 0xEDB88320, crc32fast semantics, src/volume/storage.rs:27) runs on
+ *     conflict-free nibble tables (32 x 16 entries: every ds_read_b32 of a wave hits one
+ *     16-entry table = 16 distinct banks).  Each sub-chunk is also a CRC UNIT: its share of a
+ *     long value is CRC'd independently and shifted into place with one GF(2) multiply;
+ *     shares are XOR-combined (order-free), so tiles need no ordered hand-over of CRC state.
  */
 #ifndef KVR_DEVICE_H
 #define KVR_DEVICE_H
@@ -24,14 +24,13 @@
 namespace kvr {
 
 constexpr int      NT    = 256;            // threads per workgroup
-constexpr int      TILE  = 32768;          // bytes staged per tile
-constexpr int      SC    = TILE / NT;      // 128: framing sub-chunk per thread
-constexpr int      UNIT  = TILE / NT;      // 128: CRC unit per thread
-constexpr int      SMALL = 256;            // inline-CRC threshold (bytes)
-constexpr int      MAXP  = TILE / SMALL + 8;
+constexpr int      TILE  = 16384;          // bytes staged per tile
+constexpr int      SC    = TILE / NT;      // 64: framing sub-chunk = CRC unit per thread
+constexpr int      SMALL = 64;             // values <= SMALL inside the tile: CRC'd by their walker
 constexpr uint64_t NONE  = ~0ull;          // "no position"
 constexpr uint64_t ERRP  = ~0ull - 1;      // chain ended in a framing error
 constexpr uint32_t POLY  = 0xEDB88320u;
+constexpr uint32_t GF_ONE = 0x80000000u;   // x^0 in the reflected representation
 
 struct SegDesc {          // one caller segment
     const uint8_t *base;  // device pointer to byte 0
@@ -82,6 +81,14 @@ struct Counters {         // device scratch, reset per call
     uint32_t pad;
 };
 
+struct Tables {           // read-only tables in global memory (L1/L2 resident)
+    const uint32_t *crc8;   // [16][256] byte tables (generator manifest)
+    const uint32_t *nib;    // [16 distances][2 nibbles][16] nibble tables
+    const uint32_t *pw16;   // X(16 k), k = 0 .. TILE/16
+    const uint32_t *pw1;    // X(i), i = 0 .. 16
+    const uint32_t *xw;     // [8][16]: X(j * 16^i), square-free exponentiation windows
+};
+
 // ---------------------------------------------------------------------------------------
 // GF(2)[x] / P arithmetic in the reflected representation (bit 31 = x^0), as zlib's
 // multmodp.  X(n) = x^(8n) mod P is "append n zero bytes" to a raw CRC register.
@@ -97,21 +104,42 @@ __host__ __device__ inline uint32_t gf_mul(uint32_t a, uint32_t b) {
     return p;
 }
 
-// one slice-by-16 step: register c, 16 message bytes d (little-endian dwords)
-__device__ __forceinline__ uint32_t slice16(uint32_t c, uint4 d, const uint32_t *__restrict__ T) {
-    const uint32_t w0 = d.x ^ c;
-    return T[15 * 256 + (w0 & 0xFF)] ^ T[14 * 256 + ((w0 >> 8) & 0xFF)] ^
-           T[13 * 256 + ((w0 >> 16) & 0xFF)] ^ T[12 * 256 + (w0 >> 24)] ^
-           T[11 * 256 + (d.y & 0xFF)] ^ T[10 * 256 + ((d.y >> 8) & 0xFF)] ^
-           T[9 * 256 + ((d.y >> 16) & 0xFF)] ^ T[8 * 256 + (d.y >> 24)] ^
-           T[7 * 256 + (d.z & 0xFF)] ^ T[6 * 256 + ((d.z >> 8) & 0xFF)] ^
-           T[5 * 256 + ((d.z >> 16) & 0xFF)] ^ T[4 * 256 + (d.z >> 24)] ^
-           T[3 * 256 + (d.w & 0xFF)] ^ T[2 * 256 + ((d.w >> 8) & 0xFF)] ^
-           T[1 * 256 + ((d.w >> 16) & 0xFF)] ^ T[0 * 256 + (d.w >> 24)];
+// X(d) for any d < 2^32 bytes from the nibble windows X(j * 16^i)
+__device__ inline uint32_t gf_xpow(uint64_t d, const uint32_t *__restrict__ xw) {
+    uint32_t r = GF_ONE;
+    for (int i = 0; i < 8 && d; ++i, d >>= 4) {
+        const uint32_t n = (uint32_t)(d & 15u);
+        if (n) r = (r == GF_ONE) ? xw[i * 16 + n] : gf_mul(r, xw[i * 16 + n]);
+    }
+    return r;
 }
 
-__device__ __forceinline__ uint32_t crc_byte(uint32_t c, uint32_t b, const uint32_t *__restrict__ T) {
-    return (c >> 8) ^ T[(c ^ b) & 0xFF];
+// ---------------------------------------------------------------------------------------
+// Nibble-table CRC.  nt[(d * 2 + h) * 16 + n] = T_d[n << 4h]: the contribution of a byte whose
+// nibble h is n, at distance d bytes from the end of a 16-byte block.
+// ---------------------------------------------------------------------------------------
+template <int D>
+__device__ __forceinline__ uint32_t nib_word(uint32_t w, const uint32_t *__restrict__ nt) {
+    const uint32_t lo4 = (w << 2) & 0x3C3C3C3Cu, hi4 = (w >> 2) & 0x3C3C3C3Cu;   // nibble * 4
+    const char *b = reinterpret_cast<const char *>(nt);
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t al = (lo4 >> (8 * j)) & 0xFFu, ah = (hi4 >> (8 * j)) & 0xFFu;
+        r ^= *reinterpret_cast<const uint32_t *>(b + ((D - j) * 2 + 0) * 64 + al) ^
+             *reinterpret_cast<const uint32_t *>(b + ((D - j) * 2 + 1) * 64 + ah);
+    }
+    return r;
+}
+
+// one slice-by-16 step: register c, 16 message bytes d (little-endian dwords)
+__device__ __forceinline__ uint32_t nslice16(uint32_t c, uint4 d, const uint32_t *__restrict__ nt) {
+    return nib_word<15>(d.x ^ c, nt) ^ nib_word<11>(d.y, nt) ^ nib_word<7>(d.z, nt) ^ nib_word<3>(d.w, nt);
+}
+
+__device__ __forceinline__ uint32_t nbyte(uint32_t c, uint32_t b, const uint32_t *__restrict__ nt) {
+    const uint32_t x = (c ^ b) & 0xFFu;
+    return (c >> 8) ^ nt[x & 15u] ^ nt[16 + (x >> 4)];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -150,9 +178,9 @@ struct TileView {
     }
 };
 
-// End of the record at p (engine.rs framing), or ERRP if the framing is broken there:
-// opcode outside {0,1} or a field running past the segment end.  Requires p < len.
-__device__ __forceinline__ uint64_t next_rec(const TileView &tv, uint64_t p) {
+// End of the record at p (engine.rs framing, exact, HBM fallback), or ERRP if the framing is
+// broken there: opcode outside {0,1} or a field running past the segment end.  Needs p < len.
+__device__ inline uint64_t next_rec(const TileView &tv, uint64_t p) {
     const uint64_t n = tv.len;
     const uint32_t op = tv.rd8(p);
     if (op > 1u || n - p < 5) return ERRP;
@@ -162,54 +190,6 @@ __device__ __forceinline__ uint64_t next_rec(const TileView &tv, uint64_t p) {
     if (n - e < 4) return ERRP;
     const uint64_t e2 = e + 4 + (uint64_t)tv.rd32(e);
     return e2 > n ? ERRP : e2;
-}
-
-// Speculation filter: p parses as a record and so does the head of the next one.
-__device__ __forceinline__ bool plausible(const TileView &tv, uint64_t p) {
-    const uint64_t nx = next_rec(tv, p);
-    if (nx == ERRP) return false;
-    const uint64_t n = tv.len;
-    if (nx == n) return true;
-    if (tv.rd8(nx) > 1u || n - nx < 5) return false;
-    return nx + 5 + (uint64_t)tv.rd32(nx + 1) <= n;
-}
-
-// First plausible record start in [p0, p1) (both inside the LDS tile and < len), or NONE.
-// Prefilter: only bytes 0x00/0x01 can be opcodes; four bytes are tested per dword.
-__device__ inline uint64_t find_cand(const TileView &tv, uint64_t p0, uint64_t p1) {
-    if (p0 >= p1) return NONE;
-    const int o0 = (int)((int64_t)p0 - tv.lo), o1 = (int)((int64_t)p1 - tv.lo);
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(tv.lds);
-    for (int q = o0 >> 2; q <= (o1 - 1) >> 2; ++q) {
-        const uint32_t y = w[q] & 0xFEFEFEFEu;
-        uint32_t z = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
-        const int bq = q * 4;
-        if (bq < o0) z &= ~0u << (8 * (o0 - bq));
-        if (bq + 4 > o1) z &= (1u << (8 * (o1 - bq))) - 1u;
-        while (z) {
-            const int b = __builtin_ctz(z) >> 3;
-            const uint64_t p = (uint64_t)(tv.lo + bq + b);
-            if (plausible(tv, p)) return p;
-            z &= z - 1u;
-        }
-    }
-    return NONE;
-}
-
-// Walk the chain from p while p < pe.  Returns the records walked; *exit = first start >= pe,
-// or ERRP with *errpos = the record whose framing is broken.
-__device__ inline uint32_t walk_chain(const TileView &tv, uint64_t p, uint64_t pe, uint64_t *exit,
-                                      uint64_t *errpos) {
-    uint32_t cnt = 0;
-    while (p < pe) {
-        const uint64_t nx = next_rec(tv, p);
-        if (nx == ERRP) { *exit = ERRP; *errpos = p; return cnt; }
-        ++cnt;
-        p = nx;
-    }
-    *exit = p;
-    *errpos = NONE;
-    return cnt;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -252,9 +232,9 @@ __device__ inline bool utf8_check(const TileView &tv, uint64_t p, uint64_t n, ui
     return true;
 }
 
-// Raw CRC register update over [p, p+n): LDS slice-by-16 when resident, bytes otherwise.
+// CRC register update over [p, p+n): LDS nibble slice-by-16 when resident, bytes otherwise.
 __device__ inline uint32_t crc_range(const TileView &tv, uint32_t c, uint64_t p, uint64_t n,
-                                     const uint32_t *__restrict__ T) {
+                                     const uint32_t *__restrict__ nt) {
     if (tv.in_lds(p, n)) {
         int64_t off = (int64_t)p - tv.lo;
         const uint32_t *w = reinterpret_cast<const uint32_t *>(tv.lds);
@@ -268,14 +248,14 @@ __device__ inline uint32_t crc_range(const TileView &tv, uint32_t c, uint64_t p,
                 d = make_uint4(__builtin_amdgcn_alignbyte(a1, a0, sh), __builtin_amdgcn_alignbyte(a2, a1, sh),
                                __builtin_amdgcn_alignbyte(a3, a2, sh), __builtin_amdgcn_alignbyte(a4, a3, sh));
             }
-            c = slice16(c, d, T);
+            c = nslice16(c, d, nt);
             off += 16;
             n -= 16;
         }
-        while (n > 0) { c = crc_byte(c, tv.lds[off], T); ++off; --n; }
+        while (n > 0) { c = nbyte(c, tv.lds[off], nt); ++off; --n; }
         return c;
     }
-    for (uint64_t i = 0; i < n; ++i) c = crc_byte(c, tv.rd8(p + i), T);
+    for (uint64_t i = 0; i < n; ++i) c = nbyte(c, tv.rd8(p + i), nt);
     return c;
 }
 

@@ -85,6 +85,7 @@ def _load():
     rep.kvr_ctx_destroy.restype = None
     rep.kvr_ctx_set_stream.argtypes = [P, P]
     rep.kvr_ctx_device.argtypes = [P]
+    rep.kvr_ctx_set_tiles_per_stripe.argtypes = [P, U32]
     rep.kvr_replay.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
     rep.kvr_last_stats.argtypes = [P, C.POINTER(Stats)]
     rep.kvr_strerror.argtypes = [I]
@@ -246,6 +247,9 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def set_tiles_per_stripe(self, tiles: int):
+        self._rep.kvr_ctx_set_tiles_per_stripe(self.h, tiles)
 
     def set_stream(self, stream_ptr: int | None):
         self._rep.kvr_ctx_set_stream(self.h, stream_ptr)

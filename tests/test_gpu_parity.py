@@ -93,6 +93,59 @@ def test_generated_parity(gctx, name):
         assert rg.stats.n_crc_fail == 0
 
 
+@pytest.mark.parametrize("tps", [2, 5, 64, 100000])
+@pytest.mark.parametrize("name", ["cfg2_1k", "cfg3_64k", "cfg4_del", "cfg5_zipf", "tiny", "flips"])
+def test_multi_tile_stripes(gctx, name, tps):
+    """Stripes of several tiles: exact chains across tiles, carried values, stripe speculation."""
+    spec = SPECS[name]
+    segs, exps = zip(*[K.gen_segment_cpu(spec, s) for s in range(3)])
+    gctx.set_tiles_per_stripe(tps)
+    try:
+        check_parity(gctx, list(segs), expected=np.concatenate(exps))
+    finally:
+        gctx.set_tiles_per_stripe(0)
+
+
+def boundary_segment(tile=16384):
+    """Records whose start sits at every offset r in [-44, 8] around a tile boundary, for several
+    key and value lengths: headers, key bytes, length fields and the first value bytes straddle
+    the boundary in every possible way (fillers align each probe record)."""
+    out = bytearray()
+    for klen in (0, 3, 16):
+        for vlen in (0, 5, 64, 65, 200, 20000):
+            for r in range(-44, 9):
+                b = (len(out) // tile + 2) * tile
+                fill = b + r - len(out) - 10                  # filler: 9 + 1 (key "f") + fill bytes
+                out += rec_set(b"f", bytes((len(out) + j) & 255 for j in range(fill)))
+                assert len(out) == b + r
+                out += rec_set(bytes(97 + j % 26 for j in range(klen)), bytes((r * 7 + j) & 255 for j in range(vlen)))
+    out += rec_del(b"end")
+    return bytes(out)
+
+
+def test_tile_boundary_sweep(gctx):
+    seg = boundary_segment()
+    rc, ref, _ = O.replay([seg])
+    assert rc == 0
+    for tps in (0, 1, 4):
+        gctx.set_tiles_per_stripe(tps)
+        try:
+            check_parity(gctx, [seg, seg[:-3]])
+        finally:
+            gctx.set_tiles_per_stripe(0)
+    torch = pytest.importorskip("torch")
+    buf = torch.zeros(len(seg) + 64, dtype=torch.uint8, device="cuda")
+    for shift in (1, 5, 13):                           # device placement moves the tile grid
+        buf.zero_()
+        buf[shift: shift + len(seg)] = torch.frombuffer(bytearray(seg), dtype=torch.uint8).cuda()
+        torch.cuda.synchronize()
+        for tps in (0, 3):
+            gctx.set_tiles_per_stripe(tps)
+            rg = gctx.replay([(buf.data_ptr() + shift, len(seg))], on_device=True)
+            gctx.set_tiles_per_stripe(0)
+            assert rg.status == 0 and np.array_equal(rg.tuples, ref), (shift, tps)
+
+
 def test_adversarial_speculation(gctx):
     """Values that look like records defeat the speculative entry; results must stay exact."""
     inner = b"".join(rec_set(b"k%d" % i, b"v" * (i % 50)) for i in range(4000))       # a segment in a value

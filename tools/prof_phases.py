@@ -1,0 +1,66 @@
+"""Diagnostic: per-phase cycle breakdown of k_replay's tile loop (build with -DKVR_PROF into
+lib/libkvreplay_prof.so).  Usage: python tools/prof_phases.py [cfg2|cfg3|...] [n_segments]"""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mini-kvstore-v2_amd"))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import kvreplay as K  # noqa: E402
+from bench import CONFIGS  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg2"
+nseg_override = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+lib = C.CDLL(os.path.join(ROOT, "mini-kvstore-v2_amd", "lib", "libkvreplay_prof.so"))
+P, U64, U32, SZ = C.c_void_p, C.c_uint64, C.c_uint32, C.c_size_t
+lib.kvr_ctx_create.argtypes = [C.c_int, C.POINTER(P)]
+lib.kvr_replay.argtypes = [P, C.POINTER(K.Segment), SZ, U32, P, SZ, P, SZ, C.POINTER(SZ), C.POINTER(K.Error)]
+lib.kvr_gen_segment_device.argtypes = [P, C.POINTER(K.GenParams), U64, P, U64, C.POINTER(U64), P, U64, C.POINTER(U64)]
+lib.kvr_last_stats.argtypes = [P, C.POINTER(K.Stats)]
+lib.kvr_prof_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+
+nseg, seg_bytes, kw, desc = CONFIGS[cfg]
+if nseg_override:
+    nseg = nseg_override
+spec = K.GenSpec(seed=0x6B767265706C6179 + int(cfg[3:]), seg_bytes=seg_bytes, **kw).c()
+ctx = P()
+assert lib.kvr_ctx_create(0, C.byref(ctx)) == 0
+sizes = []
+for s in range(nseg):
+    ln, nr = U64(), U64()
+    lib.kvr_gen_segment_device(ctx, C.byref(spec), s, None, 0, C.byref(ln), None, 0, C.byref(nr))
+    sizes.append((ln.value, nr.value))
+offs, tot = [], 0
+for ln, _ in sizes:
+    offs.append(tot)
+    tot += (ln + 255) & ~255
+nrec = sum(n for _, n in sizes)
+data = torch.empty(tot + 256, dtype=torch.uint8, device="cuda")
+for s, (ln, nr), o in zip(range(nseg), sizes, offs):
+    ln2, nr2 = U64(), U64()
+    assert lib.kvr_gen_segment_device(ctx, C.byref(spec), s, data.data_ptr() + o, ln, C.byref(ln2), None, 0,
+                                      C.byref(nr2)) == 0
+torch.cuda.synchronize()
+segs = (K.Segment * nseg)(*[K.Segment(s, data.data_ptr() + o, ln) for s, ((ln, _), o) in enumerate(zip(sizes, offs))])
+out = torch.empty((nrec + 1024) * 32, dtype=torch.uint8, device="cuda")
+prof = (C.c_ulonglong * 16)()
+for it in range(3):
+    lib.kvr_prof_read(prof, 1)
+    n = SZ()
+    e = K.Error()
+    rc = lib.kvr_replay(ctx, segs, nseg, K.SEGS_ON_DEVICE | K.OUT_ON_DEVICE, None, 0, out.data_ptr(), nrec + 1024,
+                        C.byref(n), C.byref(e))
+    st = K.Stats()
+    lib.kvr_last_stats(ctx, C.byref(st))
+    lib.kvr_prof_read(prof, 0)
+names = ["load+open", "spec-walk", "stitch", "records", "unit-map", "unit-crc", "finalize", "bookkeep"]
+tiles = st.n_tiles
+tot_c = sum(prof[i] for i in range(8))
+print(f"{cfg}: rc={rc} n={n.value}/{nrec} bytes={tot} tiles={tiles} stripes={st.n_stripes} ms_replay={st.ms_replay:.3f}"
+      f" GB/s={tot / st.ms_replay / 1e6:.1f}")
+for i, nm in enumerate(names):
+    print(f"  {nm:10s} {prof[i] / tiles:10.0f} cycles/tile  {100 * prof[i] / max(tot_c, 1):5.1f}%")
+print(f"  total      {tot_c / tiles:10.0f} cycles/tile (wave-0 lane-0 view)")
