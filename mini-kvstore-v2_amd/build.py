@@ -63,5 +63,18 @@ def build(force=False, verbose=False):
     return rep, host, orc
 
 
+def build_prof():
+    """Diagnostic variant with per-phase cycle stamps (tools/prof_phases.py); not shipped."""
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, "libkvreplay_prof.so")
+    deps = _deps(*[f for f in os.listdir(CSRC) if f.endswith((".hip", ".h"))])
+    if _newer(out, deps):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DKVR_PROF",
+              "-Wno-unused-result", "-o", out, os.path.join(CSRC, "kvr_api.hip")])
+    return out
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
+    if "--prof" in sys.argv:
+        print("built", build_prof())

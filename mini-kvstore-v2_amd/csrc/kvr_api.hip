@@ -60,7 +60,7 @@ struct kvr_ctx {
     DevBuf<Counters> ctr;
     DevBuf<uint32_t> seg_bad, seg_err, expected;
     DevBuf<uint64_t> bsum;
-    DevBuf<uint32_t> crc, pw16, pw1, nib, xw;
+    DevBuf<uint32_t> crc, kmul, initx;
     DevBuf<GenRecDev> gen;
     LinkResult *h_link = nullptr;
     Counters *h_ctr = nullptr;
@@ -79,8 +79,7 @@ struct kvr_ctx {
 // ---------------------------------------------------------------------------------------
 // tables: slice-by-16 CRC tables and the shift operators X(n) = x^(8n) mod P
 // ---------------------------------------------------------------------------------------
-static void build_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &pw16, std::vector<uint32_t> &pw1,
-                         std::vector<uint32_t> &nib, std::vector<uint32_t> &xw) {
+static void build_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &kmul, std::vector<uint32_t> &initx) {
     crc.assign(16 * 256, 0);
     for (uint32_t i = 0; i < 256; ++i) {
         uint32_t c = i;
@@ -92,27 +91,19 @@ static void build_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &pw16
             const uint32_t prev = crc[(t - 1) * 256 + i];
             crc[t * 256 + i] = (prev >> 8) ^ crc[prev & 0xFF];
         }
-    pw1.assign(20, 0);
-    pw1[0] = 0x80000000u;                              // x^0
-    for (int i = 1; i < 20; ++i) pw1[i] = gf_mul(pw1[i - 1], 0x00800000u);   // * x^8
-    const uint32_t x16 = pw1[16];
-    pw16.assign(TILE / 16 + 4, 0);
-    pw16[0] = 0x80000000u;
-    for (size_t k = 1; k < pw16.size(); ++k) pw16[k] = gf_mul(pw16[k - 1], x16);
-    // nibble tables: nib[(d * 2 + h) * 16 + n] = T_d[n << 4h]
-    nib.assign(16 * 32, 0);
-    for (int d = 0; d < 16; ++d)
-        for (int n = 0; n < 16; ++n) {
-            nib[(d * 2 + 0) * 16 + n] = crc[d * 256 + n];
-            nib[(d * 2 + 1) * 16 + n] = crc[d * 256 + (n << 4)];
-        }
-    // exponentiation windows: xw[i * 16 + j] = X(j * 16^i)
-    xw.assign(8 * 16, 0);
-    uint32_t base = pw1[1];   // X(1)
-    for (int i = 0; i < 8; ++i) {
-        xw[i * 16 + 0] = GF_ONE;
-        for (int j = 1; j < 16; ++j) xw[i * 16 + j] = gf_mul(xw[i * 16 + j - 1], base);
-        base = gf_mul(xw[i * 16 + 15], base);   // X(16^(i+1))
+    // X(n) = x^(8n) mod P (reflected): "push the register through n zero bytes"
+    std::vector<uint32_t> X(65);
+    X[0] = GF_ONE;
+    for (int i = 1; i <= 64; ++i) X[i] = gf_mul(X[i - 1], 0x00800000u);   // * x^8
+    initx.assign(68, 0);
+    for (int j = 0; j <= 64; ++j) initx[j] = gf_mul(0xFFFFFFFFu, X[j]);
+    // kmul[j][i][n] = (n << 4i) * X(64 * 2^j)
+    kmul.assign(8 * 8 * 16, 0);
+    uint32_t K = X[64];
+    for (int j = 0; j < 8; ++j) {
+        for (int i = 0; i < 8; ++i)
+            for (uint32_t n = 0; n < 16; ++n) kmul[(j * 8 + i) * 16 + n] = gf_mul(n << (4 * i), K);
+        K = gf_mul(K, K);
     }
 }
 
@@ -189,18 +180,16 @@ int kvr_ctx_create(int device, kvr_ctx **out) {
     for (auto &e : c->ev) if (hipEventCreate(&e) != hipSuccess) { delete c; return KVR_EHIP; }
     if (hipHostMalloc(reinterpret_cast<void **>(&c->h_link), sizeof(LinkResult)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void **>(&c->h_ctr), sizeof(Counters)) != hipSuccess) { delete c; return KVR_ENOMEM; }
-    std::vector<uint32_t> crc, pw16, pw1, nib, xw;
-    build_tables(crc, pw16, pw1, nib, xw);
-    if (c->crc.ensure(crc.size()) || c->pw16.ensure(pw16.size()) || c->pw1.ensure(pw1.size()) ||
-        c->nib.ensure(nib.size()) || c->xw.ensure(xw.size()) || c->link.ensure(1) || c->ctr.ensure(1)) {
+    std::vector<uint32_t> crc, kmul, initx;
+    build_tables(crc, kmul, initx);
+    if (c->crc.ensure(crc.size()) || c->kmul.ensure(kmul.size()) || c->initx.ensure(initx.size()) ||
+        c->link.ensure(1) || c->ctr.ensure(1)) {
         kvr_ctx_destroy(c);
         return KVR_ENOMEM;
     }
     if (hipMemcpy(c->crc.p, crc.data(), crc.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(c->pw16.p, pw16.data(), pw16.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(c->pw1.p, pw1.data(), pw1.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(c->nib.p, nib.data(), nib.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(c->xw.p, xw.data(), xw.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(c->kmul.p, kmul.data(), kmul.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->initx.p, initx.data(), initx.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
         kvr_ctx_destroy(c);
         return KVR_EHIP;
     }
@@ -215,7 +204,7 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->arena.release(); c->segs.release(); c->stripes.release(); c->sres.release(); c->tres.release();
     c->pool.release(); c->dense.release(); c->redo.release(); c->link.release(); c->ctr.release();
     c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->bsum.release();
-    c->crc.release(); c->pw16.release(); c->pw1.release(); c->nib.release(); c->xw.release(); c->gen.release();
+    c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
     if (c->h_link) (void)hipHostFree(c->h_link);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
@@ -335,13 +324,14 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         }
     }
 
-    const Tables tb{c->crc.p, c->nib.p, c->pw16.p, c->pw1.p, c->xw.p};
+    const Tables tb{c->crc.p, c->kmul.p, c->initx.p};
     for (int attempt = 0; attempt < 10; ++attempt) {
         // each workgroup claims pool space in chunks of >= pool_chunk tuples: budget one partly
         // used chunk per stripe on top of the expected record count
         const uint32_t pool_chunk = (uint32_t)std::min<uint64_t>(POOL_CHUNK, std::max<uint64_t>(256, tps * (TILE / 64)));
         const uint64_t pool_cap = std::max<uint64_t>(
             c->pool_hint, std::max<uint64_t>(65536, total_bytes / 192 + n + (uint64_t)n_stripes * pool_chunk));
+        if (pool_cap > 0xFFFFFF00ull) return KVR_ENOMEM;   // k_replay keeps 32-bit pool slots in LDS
         if (c->pool.ensure(pool_cap)) return KVR_ENOMEM;
         kvr_tuple *d_out;
         uint64_t out_cap;

@@ -3,16 +3,15 @@
  *
  * Geometry:
  *   - A workgroup (NT = 256 threads = 4 waves) owns one STRIPE: a run of consecutive TILEs of
- *     one segment, walked in order, so the record chain is exact inside a stripe and only the
- *     stripe's first entry is speculated (verified by k_link).
- *   - A TILE (16 KiB) is streamed HBM -> LDS by LDS-DMA, one tile ahead of the one being
- *     processed.  Its framing is walked in parallel: each thread speculates a chain through its
- *     64-B SUB-CHUNK; wave 0 stitches the 256 sub-chains by pointer jumping.
+ *     one segment, walked in order, so the record chain and the CRC register of a value that
+ *     spans tiles are handed from tile to tile; only the stripe's first entry is speculated
+ *     (verified by k_link).
+ *   - A TILE (16 KiB, plus a HALO of the next 256 B for headers and short fields that straddle
+ *     the tile end) is streamed HBM -> LDS by LDS-DMA, one tile ahead of the one processed.
+ *   - Each thread owns one 64-B UNIT of the tile for framing speculation and value CRCs.
  *   - CRC-32 (reflected 0xEDB88320, crc32fast semantics, src/volume/storage.rs:27) runs on
- *     conflict-free nibble tables (32 x 16 entries: every ds_read_b32 of a wave hits one
- *     16-entry table = 16 distinct banks).  Each sub-chunk is also a CRC UNIT: its share of a
- *     long value is CRC'd independently and shifted into place with one GF(2) multiply;
- *     shares are XOR-combined (order-free), so tiles need no ordered hand-over of CRC state.
+ *     slice-by-4 byte tables in LDS; register states move across units with the constants
+ *     x^(8*64*2^j) (nibble tables), never with a variable GF(2) multiply.
  */
 #ifndef KVR_DEVICE_H
 #define KVR_DEVICE_H
@@ -26,7 +25,8 @@ namespace kvr {
 constexpr int      NT    = 256;            // threads per workgroup
 constexpr int      TILE  = 16384;          // bytes staged per tile
 constexpr int      SC    = TILE / NT;      // 64: framing sub-chunk = CRC unit per thread
-constexpr int      SMALL = 64;             // values <= SMALL inside the tile: CRC'd by their walker
+constexpr int      SMALL = 64;             // values <= SMALL: CRC'd whole by their record's thread
+constexpr int      HALO  = 256;            // bytes of the next tile staged behind each tile
 constexpr uint64_t NONE  = ~0ull;          // "no position"
 constexpr uint64_t ERRP  = ~0ull - 1;      // chain ended in a framing error
 constexpr uint32_t POLY  = 0xEDB88320u;
@@ -81,12 +81,10 @@ struct Counters {         // device scratch, reset per call
     uint32_t pad;
 };
 
-struct Tables {           // read-only tables in global memory (L1/L2 resident)
-    const uint32_t *crc8;   // [16][256] byte tables (generator manifest)
-    const uint32_t *nib;    // [16 distances][2 nibbles][16] nibble tables
-    const uint32_t *pw16;   // X(16 k), k = 0 .. TILE/16
-    const uint32_t *pw1;    // X(i), i = 0 .. 16
-    const uint32_t *xw;     // [8][16]: X(j * 16^i), square-free exponentiation windows
+struct Tables {           // read-only tables in global memory (copied to LDS per workgroup)
+    const uint32_t *crc8;   // [16][256] slice-by-16 byte tables (first 4 used by k_replay)
+    const uint32_t *kmul;   // [8][8][16]: (n << 4i) * x^(8 * 64 * 2^j)
+    const uint32_t *initx;  // [65]: 0xFFFFFFFF * x^(8 j)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -104,48 +102,10 @@ __host__ __device__ inline uint32_t gf_mul(uint32_t a, uint32_t b) {
     return p;
 }
 
-// X(d) for any d < 2^32 bytes from the nibble windows X(j * 16^i)
-__device__ inline uint32_t gf_xpow(uint64_t d, const uint32_t *__restrict__ xw) {
-    uint32_t r = GF_ONE;
-    for (int i = 0; i < 8 && d; ++i, d >>= 4) {
-        const uint32_t n = (uint32_t)(d & 15u);
-        if (n) r = (r == GF_ONE) ? xw[i * 16 + n] : gf_mul(r, xw[i * 16 + n]);
-    }
-    return r;
-}
-
 // ---------------------------------------------------------------------------------------
-// Nibble-table CRC.  nt[(d * 2 + h) * 16 + n] = T_d[n << 4h]: the contribution of a byte whose
-// nibble h is n, at distance d bytes from the end of a 16-byte block.
-// ---------------------------------------------------------------------------------------
-template <int D>
-__device__ __forceinline__ uint32_t nib_word(uint32_t w, const uint32_t *__restrict__ nt) {
-    const uint32_t lo4 = (w << 2) & 0x3C3C3C3Cu, hi4 = (w >> 2) & 0x3C3C3C3Cu;   // nibble * 4
-    const char *b = reinterpret_cast<const char *>(nt);
-    uint32_t r = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t al = (lo4 >> (8 * j)) & 0xFFu, ah = (hi4 >> (8 * j)) & 0xFFu;
-        r ^= *reinterpret_cast<const uint32_t *>(b + ((D - j) * 2 + 0) * 64 + al) ^
-             *reinterpret_cast<const uint32_t *>(b + ((D - j) * 2 + 1) * 64 + ah);
-    }
-    return r;
-}
-
-// one slice-by-16 step: register c, 16 message bytes d (little-endian dwords)
-__device__ __forceinline__ uint32_t nslice16(uint32_t c, uint4 d, const uint32_t *__restrict__ nt) {
-    return nib_word<15>(d.x ^ c, nt) ^ nib_word<11>(d.y, nt) ^ nib_word<7>(d.z, nt) ^ nib_word<3>(d.w, nt);
-}
-
-__device__ __forceinline__ uint32_t nbyte(uint32_t c, uint32_t b, const uint32_t *__restrict__ nt) {
-    const uint32_t x = (c ^ b) & 0xFFu;
-    return (c >> 8) ^ nt[x & 15u] ^ nt[16 + (x >> 4)];
-}
-
-// ---------------------------------------------------------------------------------------
-// A view of one segment with one tile resident in LDS.  Positions are segment offsets;
-// LDS offset 0 holds segment position `lo` (lo may be negative for the first tile).
-// rd8(p) needs p < len; rd32(p) needs p + 4 <= len.  Bytes outside the tile come from HBM.
+// A view of one segment with one tile (+ halo) resident in LDS.  Positions are segment
+// offsets; LDS offset 0 holds segment position `lo` (lo may be negative for the first tile).
+// rd8(p) needs p < len; rd32(p) needs p + 4 <= len.  Bytes outside tile + halo come from HBM.
 // ---------------------------------------------------------------------------------------
 struct TileView {
     const uint8_t *seg;
@@ -163,18 +123,18 @@ struct TileView {
     }
     __device__ __forceinline__ uint32_t rd8(uint64_t p) const {
         const int64_t off = (int64_t)p - lo;
-        if (off >= 0 && off < TILE) return lds[off];
+        if (off >= 0 && off < TILE + HALO) return lds[off];
         return seg[p];
     }
     __device__ __forceinline__ uint32_t rd32(uint64_t p) const {
         const int64_t off = (int64_t)p - lo;
-        if (off >= 0 && off <= TILE - 4) return lds_u32(off);
+        if (off >= 0 && off <= TILE + HALO - 4) return lds_u32(off);
         return (uint32_t)seg[p] | ((uint32_t)seg[p + 1] << 8) | ((uint32_t)seg[p + 2] << 16) |
                ((uint32_t)seg[p + 3] << 24);
     }
     __device__ __forceinline__ bool in_lds(uint64_t p, uint64_t n) const {
         const int64_t off = (int64_t)p - lo;
-        return off >= 0 && off + (int64_t)n <= TILE;
+        return off >= 0 && off + (int64_t)n <= TILE + HALO;
     }
 };
 
@@ -230,33 +190,6 @@ __device__ inline bool utf8_check(const TileView &tv, uint64_t p, uint64_t n, ui
         ++i;
     }
     return true;
-}
-
-// CRC register update over [p, p+n): LDS nibble slice-by-16 when resident, bytes otherwise.
-__device__ inline uint32_t crc_range(const TileView &tv, uint32_t c, uint64_t p, uint64_t n,
-                                     const uint32_t *__restrict__ nt) {
-    if (tv.in_lds(p, n)) {
-        int64_t off = (int64_t)p - tv.lo;
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(tv.lds);
-        while (n >= 16) {
-            const uint32_t q = (uint32_t)off >> 2, sh = (uint32_t)off & 3u;
-            uint4 d;
-            if (sh == 0) {
-                d = make_uint4(w[q], w[q + 1], w[q + 2], w[q + 3]);
-            } else {
-                const uint32_t a0 = w[q], a1 = w[q + 1], a2 = w[q + 2], a3 = w[q + 3], a4 = w[q + 4];
-                d = make_uint4(__builtin_amdgcn_alignbyte(a1, a0, sh), __builtin_amdgcn_alignbyte(a2, a1, sh),
-                               __builtin_amdgcn_alignbyte(a3, a2, sh), __builtin_amdgcn_alignbyte(a4, a3, sh));
-            }
-            c = nslice16(c, d, nt);
-            off += 16;
-            n -= 16;
-        }
-        while (n > 0) { c = nbyte(c, tv.lds[off], nt); ++off; --n; }
-        return c;
-    }
-    for (uint64_t i = 0; i < n; ++i) c = nbyte(c, tv.rd8(p + i), nt);
-    return c;
 }
 
 }  // namespace kvr

@@ -73,28 +73,34 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
         if (r.entry != NONE) run = (int32_t)s;
     }
     __syncthreads();
+    // A segment whose first inconsistent stripe precedes its first error stripe is unresolved;
+    // one whose error comes first has its true first error.  Segments are independent chains.
     for (uint32_t g = tid; g < n_segs; g += LT) {
         const uint32_t bb = __hip_atomic_load(&seg_bad[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t ee = __hip_atomic_load(&seg_err[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (bb != ~0u || ee != ~0u) atomicMin(&first_problem, g);
+        if (ee != ~0u && ee < bb) atomicMin(&first_problem, g);     // first segment with a resolved error
     }
     __syncthreads();
-    const uint32_t fp = first_problem;
-    bool unresolved = false;
-    uint32_t fbad = ~0u, ferr = ~0u;
-    if (fp != ~0u) {
-        fbad = __hip_atomic_load(&seg_bad[fp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ferr = __hip_atomic_load(&seg_err[fp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unresolved = fbad < ferr;
+    const uint32_t fe = first_problem;       // segments after it are never reached (engine.rs:56 `?`)
+    __syncthreads();
+    if (tid == 0) first_problem = ~0u;
+    __syncthreads();
+    for (uint32_t g = tid; g < n_segs && g < fe; g += LT) {
+        const uint32_t bb = __hip_atomic_load(&seg_bad[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (bb != ~0u) atomicMin(&first_problem, g);                // first unresolved segment
     }
-    // pass 2: re-walk list (stripes whose entry disagrees with the true chain so far)
+    __syncthreads();
+    const uint32_t fu = first_problem;
+    const bool unresolved = fu != ~0u;
+    // pass 2: re-walk list (stripes whose entry disagrees with the true chain so far), in every
+    // segment before the first resolved error
     if (unresolved) {
         run = run0;
         for (uint32_t s = b; s < e; ++s) {
             const StripeRes r = sres[s];
             const StripeDesc d = stripes[s];
             const SegDesc g = segs[d.seg];
-            if (d.seg <= fp && s != g.stripe0) {
+            if (d.seg < fe && s != g.stripe0) {
                 const uint64_t xp = run >= 0 ? sres[run].exit : NONE;
                 bool bad = false;
                 if (xp != ERRP) {
@@ -115,19 +121,19 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
     __syncthreads();
     if (tid == 0) {
         LinkResult L;
-        L.first_problem_seg = fp;
+        L.first_problem_seg = unresolved ? fu : fe;
         L.n_redo = nredo < redo_cap ? nredo : redo_cap;
         L.passes = res->passes + 1;
         L.err_kind = 0; L.err_seg = 0; L.err_pos = 0; L.err_aux = 0;
-        if (fp == ~0u) {
-            L.status = 0;
-        } else if (unresolved) {
+        if (unresolved) {
             L.status = 3;
+        } else if (fe == ~0u) {
+            L.status = 0;
         } else {
-            const StripeRes r = sres[ferr];
+            const StripeRes r = sres[__hip_atomic_load(&seg_err[fe], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)];
             L.status = 1;
             L.err_kind = r.err_kind;
-            L.err_seg = fp;
+            L.err_seg = fe;
             L.err_pos = r.err_pos;
             L.err_aux = r.err_aux;
         }
