@@ -47,6 +47,7 @@ constexpr uint32_t REDO_GRID = 1024;
 struct kvr_ctx {
     int device = 0;
     int n_cu = 256;
+    int wg_per_cu = 3;
     hipStream_t own = nullptr, stream = nullptr;
     hipEvent_t ev[6] = {};
     DevBuf<uint8_t> arena;
@@ -175,6 +176,8 @@ int kvr_ctx_create(int device, kvr_ctx **out) {
     c->device = device;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->n_cu = prop.multiProcessorCount;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_replay, NT, 0) == hipSuccess && occ > 0) c->wg_per_cu = occ;
     if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return KVR_EHIP; }
     c->stream = c->own;
     for (auto &e : c->ev) if (hipEventCreate(&e) != hipSuccess) { delete c; return KVR_EHIP; }
@@ -284,6 +287,8 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         total_tiles += g.n_tiles;
     }
     if (total_tiles >= 0xFFFFFFFFull) return KVR_EINVAL;
+    // about 8 stripes per CU (measured better than one round of resident workgroups: a stripe
+    // that must be re-walked costs 1/8 of a CU's share instead of all of it)
     const uint64_t target = (uint64_t)c->n_cu * 8;
     const uint64_t tps = c->tps_override ? c->tps_override : std::max<uint64_t>(1, (total_tiles + target - 1) / target);
     c->h_stripes.clear();

@@ -691,10 +691,9 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
                 if (Vend >= 0 && G.lvb[Vend] >= us) { a = G.lvb[Vend] - us; starts = true; }
                 uint32_t c = 0;
 #pragma unroll
-                for (int kk = 0; kk < 16; ++kk) {
-                    const int sh = a - 4 * kk;   // bytes of this word before the value
-                    const uint32_t x = sh >= 4 ? 0u : (sh <= 0 ? w[kk] : (w[kk] & (~0u << (8 * sh))));
-                    c = crc4(c, x, S.T);
+                for (int kk = 0; kk < 16; ++kk) {   // bytes before the value are zeroed (branch-free)
+                    const int sh = min(max(8 * (a - 4 * kk), 0), 32);
+                    c = crc4(c, w[kk] & (uint32_t)(~0ull << sh), S.T);
                 }
                 if (starts) v = c ^ S.IX[SC - a];
                 else if (tid == 0) v = c ^ kmul(S.c_state, S.KT);   // carried state across unit 0
@@ -724,8 +723,10 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
                     const int m = (int)(ve_rel - us);   // 1 .. 64
                     uint32_t c = tid == 0 ? S.c_state : S.r.sc.sx[tid - 1];
 #pragma unroll
-                    for (int kk = 0; kk < 16; ++kk)
-                        if (4 * kk + 4 <= m) c = crc4(c, w[kk], S.T);
+                    for (int kk = 0; kk < 16; ++kk) {
+                        const uint32_t cn = crc4(c, w[kk], S.T);
+                        c = 4 * kk + 4 <= m ? cn : c;
+                    }
                     for (int b = m & ~3; b < m; ++b) c = crc1(c, tile[us + b], S.T);
                     const uint64_t idx = Vst == VCARRY ? S.c_idx : (uint64_t)G.lidx[Vst];
                     if (idx < pool_cap) pool[idx].crc32 = ~c;
