@@ -68,7 +68,9 @@ def main():
     ctx = K.Context(local)
 
     # ---- generate this rank's shard directly into HBM -------------------------------------
-    seg_nos = [rank * nseg + i for i in range(nseg)]
+    # round-robin sharding of the store's segment list (segment i -> GPU i mod N):
+    # rank r owns global segments r, r + N, r + 2N, ...
+    seg_nos = [rank + world * i for i in range(nseg)]
     sizes = [K.gen_segment_size(spec, s) for s in seg_nos]
     offs, tot = [], 0
     for ln, _ in sizes:
@@ -112,9 +114,8 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        from kvreplay.shard import max_over_ranks
+        dt = max_over_ranks(dt)
 
     ms_replay = float(np.mean([a for a, _ in k_ms]))
     ms_pipe = float(np.mean([b for _, b in k_ms]))

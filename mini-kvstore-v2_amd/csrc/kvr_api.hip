@@ -358,13 +358,9 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
                            c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p);
         HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_replay, dim3(std::min(n_stripes, REDO_GRID)), dim3(NT), 0, st, c->segs.p, c->stripes.p,
-                           c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, c->redo.p, c->link.p, 1, pool_chunk);
-        HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
-                           c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p);
-        HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[2], st));
+        // compaction is launched right away: it does nothing unless linking succeeded (status 0),
+        // which is the common case; otherwise the host re-walks and compacts again below
         hipLaunchKernelGGL(k_tsum, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->link.p);
         hipLaunchKernelGGL(k_tscan, dim3(1), dim3(1024), 0, st, c->bsum.p, nb, c->ctr.p, c->link.p);
         hipLaunchKernelGGL(k_compact, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->pool.p, pool_cap,
@@ -383,16 +379,29 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         uint32_t guard = 0;
         bool recompact = false;
         const bool dbg = getenv("KVR_DEBUG") != nullptr;
-        if (dbg)
+        if (dbg) {
             fprintf(stderr, "kvr: pass1 status=%d n_redo=%u first_problem=%u passes=%u overflow=%u\n",
                     c->h_link->status, c->h_link->n_redo, c->h_link->first_problem_seg, c->h_link->passes,
                     c->h_ctr->overflow);
+            std::vector<RedoEnt> rl(c->h_link->n_redo);
+            std::vector<StripeRes> sr(n_stripes);
+            (void)hipMemcpy(rl.data(), c->redo.p, rl.size() * sizeof(RedoEnt), hipMemcpyDeviceToHost);
+            (void)hipMemcpy(sr.data(), c->sres.p, sr.size() * sizeof(StripeRes), hipMemcpyDeviceToHost);
+            for (size_t q = 0; q < rl.size() && q < 40; ++q) {
+                const uint32_t s = rl[q].stripe;
+                const StripeDesc &d = c->h_stripes[s];
+                fprintf(stderr, "   p1 redo stripe %u seg %u tiles [%u,%u) true-entry %llu | spec entry %lld exit %lld err %u@%lld"
+                        " | pred entry %lld exit %lld\n", s, d.seg, d.t_begin, d.t_end, (unsigned long long)rl[q].entry,
+                        (long long)sr[s].entry, (long long)sr[s].exit, sr[s].err_kind, (long long)sr[s].err_pos,
+                        s ? (long long)sr[s - 1].entry : -9, s ? (long long)sr[s - 1].exit : -9);
+            }
+        }
         if (c->h_ctr->overflow & 1u) {   // pool too small: grow to what this pass needed and run again
             c->pool_hint = std::max<uint64_t>(c->h_ctr->pool_cursor, pool_cap) * 2;
             continue;
         }
         while (c->h_link->status == 3 && guard++ < n_stripes + 4) {
-            hipLaunchKernelGGL(k_replay, dim3(std::min(n_stripes, REDO_GRID)), dim3(NT), 0, st, c->segs.p, c->stripes.p,
+            hipLaunchKernelGGL(k_replay, dim3(std::max(1u, std::min(c->h_link->n_redo, (uint32_t)c->redo.n))), dim3(NT), 0, st, c->segs.p, c->stripes.p,
                                c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, c->redo.p, c->link.p, 1, pool_chunk);
             hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes,
                                c->sres.p, c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p);

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
 // Scan of per-tile counts and the ordered gather pool -> out.
 // ---------------------------------------------------------------------------------------
 constexpr int CT = 256;           // threads per compaction block
-constexpr int CPT = 4;            // tiles per thread
+constexpr int CPT = 1;            // tiles per thread
 constexpr int CB = CT * CPT;      // tiles per compaction block
 
 __global__ __launch_bounds__(CT) void k_tsum(const TileRes *__restrict__ tres, uint32_t n_tiles,
@@ -216,24 +216,28 @@ __global__ __launch_bounds__(CT) void k_compact(const TileRes *__restrict__ tres
     const uint64_t base = bsum[blockIdx.x] + part[threadIdx.x] - s;
     for (int i = 0; i < CPT; ++i) off[threadIdx.x * CPT + i] = base + loc[i];
     __syncthreads();
-    // one wave per tile: lanes move whole 32-B tuples
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // every thread moves whole 32-B tuples: tuple k of the block lives in the tile whose
+    // local offset range holds k (binary search over the block's CB tile offsets in LDS)
+    const int lane = threadIdx.x & 63;
+    const uint64_t b0 = off[0];
+    const uint32_t nt = min((uint32_t)CB, n_tiles - tb);
+    const uint64_t btotal = (tb + nt - 1 < n_tiles ? off[nt - 1] + tres[tb + nt - 1].count : b0) - b0;
     uint32_t fails = 0;
-    for (int i = wave; i < CB; i += CT / 64) {
-        const uint32_t t = tb + i;
-        if (t >= n_tiles) break;
-        const uint32_t cnt = tres[t].count;
-        const uint64_t src = tres[t].pool_off, dst = off[i];
-        for (uint32_t j = lane; j < cnt; j += 64) {
-            if (src + j >= pool_cap) continue;
-            kvr_tuple tp = pool[src + j];
-            const uint64_t o = dst + j;
-            if (expected && o < n_expected && tp.op == 0) {
-                tp.flags |= KVR_TF_VERIFIED;
-                if (expected[o] != tp.crc32) { tp.flags |= KVR_TF_CRC_FAIL; ++fails; }
-            }
-            if (o < out_cap) out[o] = tp;
+    for (uint64_t k = threadIdx.x; k < btotal; k += CT) {
+        uint32_t lo_i = 0, hi_i = nt - 1;       // last tile i with off[i] - b0 <= k
+        while (lo_i < hi_i) {
+            const uint32_t mid = (lo_i + hi_i + 1) >> 1;
+            if (off[mid] - b0 <= k) lo_i = mid; else hi_i = mid - 1;
         }
+        const uint64_t o = b0 + k;
+        const uint64_t src = tres[tb + lo_i].pool_off + (o - off[lo_i]);
+        if (src >= pool_cap) continue;
+        kvr_tuple tp = pool[src];
+        if (expected && o < n_expected && tp.op == 0) {
+            tp.flags |= KVR_TF_VERIFIED;
+            if (expected[o] != tp.crc32) { tp.flags |= KVR_TF_CRC_FAIL; ++fails; }
+        }
+        if (o < out_cap) out[o] = tp;
     }
     for (int d = 32; d >= 1; d >>= 1) fails += __shfl_xor(fails, d, 64);
     if (lane == 0 && fails) atomicAdd(&ctr->crc_fail, (unsigned long long)fails);

@@ -153,9 +153,12 @@ __device__ __forceinline__ uint64_t next_spec(const TileView &tv, uint64_t p) {
     return e2 > n ? ERRP : e2;
 }
 
-// Could the first min(klen, 16) key bytes (those inside the tile) begin a valid UTF-8 string?
-// Keys are String (engine.rs:114); a candidate whose "key" is random value bytes fails here.
-// Heuristic only: a true record rejected here is found again by the stripe link check.
+// Could the first min(klen, 16) key bytes (those inside the tile) begin a valid UTF-8 string
+// without NUL?  Keys are String (engine.rs:114): a candidate whose "key" is random value bytes
+// fails the UTF-8 test, and one that starts a few bytes before a true header ([0][len LE]
+// makes an in-range length whose "key" is the zero bytes of the true length) fails the NUL test.
+// Heuristic only: a true record rejected here (a key holding NUL) is found again by the exact
+// chain walk or by the stripe link check, so results never depend on it.
 __device__ __forceinline__ bool key_prefix_ok(const TileView &tv, int off_k, uint32_t klen) {
     int m = TILE - off_k;
     m = m > 16 ? 16 : m;
@@ -163,6 +166,7 @@ __device__ __forceinline__ bool key_prefix_ok(const TileView &tv, int off_k, uin
     int i = 0;
     while (i < m) {
         const uint32_t b = tv.lds[off_k + i];
+        if (b == 0u) return false;
         if (b < 0x80u) { ++i; continue; }
         int w;
         uint32_t c_lo = 0x80u, c_hi = 0xBFu;

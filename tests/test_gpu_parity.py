@@ -241,3 +241,28 @@ def test_kvstore_open_reports_reference_message(gctx, tmp_path):
     with pytest.raises(K.CorruptedData) as ei:
         K.KVStore.open(str(d), gctx)
     assert str(ei.value) == f"Corrupted data: Failed to read key length in {d}/segment-2.dat: failed to fill whole buffer"
+
+
+def test_sharded_replay_matches_single(gctx):
+    """N-way round-robin sharding (two contexts on one device stand in for two GPUs) merges back
+    into exactly the single-context answer, including the store's first error."""
+    from kvreplay import shard as SH
+    spec = SPECS["cfg4_del"]
+    parts = [K.gen_segment_cpu(spec, s) for s in range(5)]
+    segs = [p[0] for p in parts]
+    ctx2 = K.Context(0)
+    try:
+        sr = SH.ShardedReplay(contexts=[gctx, ctx2])
+        st, t, err = sr.replay(segs)
+        rc, ref, _ = O.replay(segs)
+        assert st == rc == 0 and np.array_equal(t, ref)
+        exp = (np.concatenate([p[1] for p in parts]), [len(p[1]) for p in parts])
+        st, t, _ = sr.replay(segs, expected=exp)
+        assert st == 0 and not np.any(t["flags"] & K.TF_CRC_FAIL) and np.all(t["flags"][t["op"] == 0] & 1)
+        bad = [s.tobytes() for s in segs]
+        bad[2], bad[3] = bad[2][:-5], bad[3][:-2]
+        st, _, err = sr.replay(bad)
+        rc, _, e = O.replay(bad)
+        assert st == rc == 1 and err == (e.kind, e.seg_idx, e.rec_off, e.aux) and err[1] == 2
+    finally:
+        ctx2.close()

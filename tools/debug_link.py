@@ -16,8 +16,8 @@ for tps in (1,):
     except Exception as e:
         print("boundary tps", tps, "EXC", e, flush=True)
 spec = K.GenSpec(seed=0x6B767265706C6179 + 2, seg_bytes=64 << 20, val_min=1024, val_max=1024, key_space_log2=20)
-segs = [K.gen_segment_cpu(spec, s)[0] for s in range(4)]
-for tps in ():
+segs = [K.gen_segment_cpu(spec, s)[0] for s in range(8)]
+for tps in (0,):
     ctx.set_tiles_per_stripe(tps)
     t0 = time.time()
     r = ctx.replay(segs)
