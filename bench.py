@@ -125,7 +125,7 @@ def main():
     alg_bytes = seg_total + 32 * n_rec          # segment bytes read once + 32-B tuple writes
     achieved = alg_bytes / (ms_replay / 1e3) / 1e9
 
-    cpu = None
+    cpu = e2e = None
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle_py as O   # the checker / CPU baseline only
         cs = min(args.cpu_segs, nseg)
@@ -135,11 +135,31 @@ def main():
         rc, nk, tb, nr, dg, err = O.replay_faithful(host_segs)
         ct = time.perf_counter() - t1
         assert rc == 0 and nr == sum(nr_ for _, nr_ in sizes[:cs])
+        # end-to-end from host memory (the path's real start and end): the same sample
+        # replayed from pageable host buffers, H2D of segment bytes + kernels + D2H of the tuples
+        ctx.replay(host_segs, seg_ids=seg_nos[:cs])
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        rh = ctx.replay(host_segs, seg_ids=seg_nos[:cs])
+        et = time.perf_counter() - t2
+        assert rh.status == 0 and rh.n == nr
+        e2e = {"value": round(sb / et / 2 ** 30, 3), "unit": "GiB/s", "sample": f"{cs} segments ({sb / 2**30:.2f} GiB) "
+               "from pageable host memory: H2D of segment bytes + replay + D2H of the tuples, one call"}
         cpu = {"value": round(sb / ct / 2 ** 30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
                "records_per_s": round(nr / ct, 1),
                "sample": f"{cs} of the {nseg} segments ({sb / 2**30:.2f} GiB), oracle_replay_faithful: "
                          f"8 KiB buffered reads, per-record allocations, owning key->value map, CRC-32 per value "
                          f"(engine.rs:79-154 cost model), 1 thread, warm memory"}
+
+    traffic = None   # HBM bytes per k_replay launch from PMC (tools/pmc_traffic.py), if measured on this build
+    tj = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tj):
+        import hashlib
+        pm = json.load(open(tj))
+        lib = os.path.join(ROOT, "mini-kvstore-v2_amd", "lib", "libkvreplay.so")
+        if (pm.get("lib_sha256_16") == hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
+                and args.config == "cfg2" and nseg == CONFIGS["cfg2"][0]):
+            traffic = round(pm["hbm_bytes"])
 
     res = {
         "metric": METRIC, "value": round(gib_s, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
@@ -152,9 +172,10 @@ def main():
         "crc_verified_records_per_s": round(total_recs / dt, 1),
         "ms_kernel_replay": round(ms_replay, 4), "ms_device_pipeline": round(ms_pipe, 4),
         "roofline": {"bound": "hbm", "kernel": "k_replay", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
-                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                      "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": cpu,
+        "e2e_host": e2e,
     }
     if rank == 0:
         print(json.dumps(res))
