@@ -47,7 +47,7 @@ constexpr uint32_t REDO_GRID = 1024;
 struct kvr_ctx {
     int device = 0;
     int n_cu = 256;
-    int wg_per_cu = 3;
+    int wg_per_cu = 5;
     hipStream_t own = nullptr, stream = nullptr;
     hipEvent_t ev[6] = {};
     DevBuf<uint8_t> arena;
@@ -287,9 +287,8 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         total_tiles += g.n_tiles;
     }
     if (total_tiles >= 0xFFFFFFFFull) return KVR_EINVAL;
-    // about 8 stripes per CU (measured better than one round of resident workgroups: a stripe
-    // that must be re-walked costs 1/8 of a CU's share instead of all of it)
-    const uint64_t target = (uint64_t)c->n_cu * 8;
+    // one stripe per wave, two rounds of resident waves (k_replay: 4 stripes per workgroup)
+    const uint64_t target = (uint64_t)c->n_cu * (uint64_t)c->wg_per_cu * 4 * 2;
     const uint64_t tps = c->tps_override ? c->tps_override : std::max<uint64_t>(1, (total_tiles + target - 1) / target);
     c->h_stripes.clear();
     for (size_t i = 0; i < n; ++i) {
@@ -351,8 +350,8 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         HIPCHK(hipMemsetAsync(c->ctr.p, 0, sizeof(Counters), st));
         HIPCHK(hipMemsetAsync(c->link.p, 0, sizeof(LinkResult), st));
         HIPCHK(hipEventRecord(c->ev[0], st));
-        hipLaunchKernelGGL(k_replay, dim3(n_stripes), dim3(NT), 0, st, c->segs.p, c->stripes.p, c->sres.p, c->tres.p,
-                           c->pool.p, pool_cap, c->ctr.p, tb, c->redo.p, c->link.p, 0, pool_chunk);
+        hipLaunchKernelGGL(k_replay, dim3((n_stripes + 3) / 4), dim3(NT), 0, st, c->segs.p, c->stripes.p, n_stripes,
+                           c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, c->redo.p, c->link.p, 0, pool_chunk);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[1], st));
         hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
@@ -401,8 +400,9 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
             continue;
         }
         while (c->h_link->status == 3 && guard++ < n_stripes + 4) {
-            hipLaunchKernelGGL(k_replay, dim3(std::max(1u, std::min(c->h_link->n_redo, (uint32_t)c->redo.n))), dim3(NT), 0, st, c->segs.p, c->stripes.p,
-                               c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, c->redo.p, c->link.p, 1, pool_chunk);
+            hipLaunchKernelGGL(k_replay, dim3((std::max(1u, std::min(c->h_link->n_redo, (uint32_t)c->redo.n)) + 3) / 4), dim3(NT),
+                               0, st, c->segs.p, c->stripes.p, n_stripes, c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p,
+                               tb, c->redo.p, c->link.p, 1, pool_chunk);
             hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes,
                                c->sres.p, c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p);
             HIPCHK(hipGetLastError());

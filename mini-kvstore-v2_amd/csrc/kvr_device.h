@@ -23,8 +23,8 @@
 namespace kvr {
 
 constexpr int      NT    = 256;            // threads per workgroup
-constexpr int      TILE  = 16384;          // bytes staged per tile
-constexpr int      SC    = TILE / NT;      // 64: framing sub-chunk = CRC unit per thread
+constexpr int      TILE  = 4096;           // bytes per tile (one wave: 64 lanes x 64-B units)
+constexpr int      SC    = 64;             // unit: framing sub-chunk = CRC unit per lane
 constexpr int      SMALL = 64;             // values <= SMALL: CRC'd whole by their record's thread
 constexpr int      HALO  = 256;            // bytes of the next tile staged behind each tile
 constexpr uint64_t NONE  = ~0ull;          // "no position"
@@ -158,6 +158,7 @@ __device__ inline uint64_t next_rec(const TileView &tv, uint64_t p) {
 // ---------------------------------------------------------------------------------------
 __device__ inline bool utf8_check(const TileView &tv, uint64_t p, uint64_t n, uint64_t *vu, uint32_t *el) {
     uint64_t i = 0;
+#pragma unroll 1
     while (i < n) {
         if (n - i >= 4 && tv.in_lds(p + i, 4)) {          // ASCII fast path, 4 bytes at a time
             const uint32_t w4 = tv.lds_u32((int64_t)(p + i) - tv.lo);

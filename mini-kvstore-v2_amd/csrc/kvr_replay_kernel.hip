@@ -1,104 +1,80 @@
 /*
  * kvr_replay_kernel.hip — k_replay, the hot path (gfx950).
  *
- * One workgroup replays one stripe (consecutive tiles of one segment) exactly as
+ * One WAVE replays one stripe (consecutive 4-KiB tiles of one segment) exactly as
  * src/store/engine.rs:79-154 walks a segment file, and emits one 32-B kvr_tuple per record with
  * the CRC-32 of its key and value (crc32fast::hash semantics, src/volume/storage.rs:27).
+ * A workgroup holds 4 independent stripes; after the CRC tables are staged in LDS there is no
+ * workgroup barrier at all, so a wave waiting on a header hop or on HBM never holds up another.
  *
- * Per 16-KiB tile (geometry in kvr_device.h), with the next tile's LDS-DMA in flight:
- *   F  framing: the record starts of the tile, exactly, from the tile entry (the previous
- *      tile's exit).  Sparse tiles: lane 0 hops header to header (a few LDS round trips per
- *      record).  Dense tiles (or after HOP_BUDGET hops): every thread speculates a record chain
- *      through its 64-B sub-chunk and wave 0 stitches the sub-chains by pointer jumping.
- *      The stripe's first tile has no known entry: its first plausible record start is taken
- *      and k_link verifies it against the previous stripe's exit.
- *   R  records, one thread per record: engine.rs checks in engine.rs order (key length, key,
- *      UTF-8, opcode, value length, value), key CRC, CRC of values <= SMALL bytes, the tuple.
- *      Longer values register the first 64-B unit boundary they cross.
- *   C  CRC of long values, one thread per 64-B unit: every thread CRCs its unit's piece of the
- *      value crossing the unit's end; a segmented scan over the 256 units (multipliers are the
- *      constants x^(8*64*2^j), nibble tables) turns pieces into register states at every unit
- *      boundary; the thread whose unit holds a value's last byte finishes that CRC from the
- *      state at its unit start.  A value running past the tile hands its register state to the
- *      next tile (the stripe walks its tiles in order), so no variable GF(2) multiply is needed.
- * Barriers are raw s_barrier + lgkmcnt waits so the next tile's LDS-DMA stays in flight.
+ * Per tile, lane l owns the 64-B unit [64 l, 64 l + 64):
+ *   load  the unit arrives in registers (prefetched one tile ahead with 16-B global loads) and is
+ *         written to the wave's LDS tile for random access; the next 256 B (halo) come by LDS-DMA
+ *   F     framing: the record starts, exactly, from the tile entry (the previous tile's exit).
+ *         Sparse tiles: all lanes hop header to header together (LDS broadcast reads), lane j
+ *         keeps record j.  Dense tiles (or past 64 records): every lane speculates a chain through
+ *         its unit and the wave stitches the sub-chains by pointer jumping.  The stripe's first
+ *         tile takes its first plausible record start; k_link verifies it.
+ *   R     records: engine.rs checks in engine.rs order, key CRC, CRC of values <= 64 B, tuple.
+ *         Longer values register the first unit boundary they cross.
+ *   C     long values: each lane CRCs, from its registers, its unit's piece of the value crossing
+ *         the unit's end; a 6-step segmented scan across the wave (multipliers are the constants
+ *         x^(8*64*2^j)) gives the CRC register at every unit boundary; the lane holding a value's
+ *         last byte finishes that CRC.  A value running past the tile hands its register to the
+ *         next tile of the stripe (walked in order), so no variable GF(2) multiply is needed.
  */
 #include "kvr_device.h"
 
 namespace kvr {
 
-constexpr uint16_t N16 = 0xFFFFu;        // no offset
+constexpr int WPB = NT / 64;              // stripes (waves) per workgroup
+constexpr int UNITS = TILE / SC;          // 64 units per tile = one per lane
+static_assert(UNITS == 64, "one 64-B unit per lane");
+constexpr uint16_t N16 = 0xFFFFu;
 constexpr uint32_t N32 = 0xFFFFFFFFu;
 constexpr uint32_t X_BEYOND = 0xFFFFFFFEu, X_ERR = 0xFFFFFFFFu;
-constexpr uint64_t BEYOND = ~0ull - 2;   // record end not readable from the tile (>= tile end)
-constexpr int16_t T_END = NT, T_ERR = NT + 1, T_MM = NT + 2;
+constexpr uint64_t BEYOND = ~0ull - 2;    // record end not readable from the tile (>= tile end)
+constexpr int T_END = 64, T_ERR = 65, T_MM = 66;
 constexpr uint32_t POOL_CHUNK = 2048;
-constexpr int MAXREC = TILE / 5 + 2;     // record starts in one tile (a record is >= 5 B)
-constexpr int MAXLONG = NT + 2;          // long values touching a tile: one per first-crossed boundary (+ pending)
-constexpr uint32_t HOP_BUDGET = 40;      // exact hops by one lane before switching to speculation
-constexpr uint32_t DENSE = 48;           // records in the previous tile above which we speculate at once
+constexpr uint32_t HOP_MAX = 64;          // records found by hopping (one per lane)
+constexpr uint32_t DENSE = 48;            // previous tile's records above which we speculate at once
+constexpr int MAXLONG = UNITS + 2;        // long values touching a tile (one per first-crossed boundary + pending)
 constexpr int32_t VNONE = -1, VCARRY = -2;
-constexpr int32_t FAR = 1 << 30;         // "ends beyond the tile" (tile-relative clamp)
+constexpr int32_t FAR = 1 << 30;          // "ends beyond the tile" (tile-relative clamp)
 
-struct SpecLds {                 // framing speculation (dense tiles)
-    uint32_t sc_exit[NT];        // exit offset from lo (X_BEYOND / X_ERR)
-    uint32_t sc_base[NT];        // index of the sub-chunk's first record among the speculated ones
-    uint16_t sc_cand[NT], sc_last[NT], sc_cnt[NT], sc_entry[NT];
-    int16_t  nxt[NT], nxt0[NT];
-    uint8_t  reach[NT];
+struct WaveLds {                          // one stripe's scratch
+    uint8_t  tile[TILE + HALO];
+    uint32_t sc_exit[UNITS];
+    uint16_t sc_cand[UNITS], sc_cnt[UNITS], sc_last[UNITS];
+    uint8_t  reach[UNITS];
+    int32_t  lvb[MAXLONG], lve[MAXLONG];
+    uint32_t lidx[MAXLONG];
+    uint32_t bkey[UNITS + 1];
+    uint32_t nlong, pad[3];
 };
 
-struct LongLds {                 // long values of the tile (after framing)
-    int32_t  lvb[MAXLONG];       // value start, tile-relative
-    int32_t  lve[MAXLONG];       // value end, tile-relative, clamped to FAR
-    uint32_t lidx[MAXLONG];      // pool slot of the record's tuple
-    uint32_t bkey[NT + 1];       // boundary b: key of the long value whose first crossed boundary is b
-    int32_t  vc[NT + 1];         // value crossing boundary b: L, VCARRY or VNONE
+struct __align__(16) Smem {
+    uint32_t T[4 * 256];                  // slice-by-4 byte tables
+    uint32_t KT[6 * 8 * 16];              // [j][nibble i][n]: (n << 4i) * x^(8*64*2^j)
+    uint32_t IX[68];                      // 0xFFFFFFFF * x^(8j): initial register pushed through j bytes
+    WaveLds w[WPB];
 };
 
-struct ScanLds {
-    uint64_t x[2][NT];           // ping-pong (state | segment flag << 32)
-    uint32_t sx[NT];             // inclusive states: register at the end of every unit
-};
+__device__ __forceinline__ void wsync() {   // LDS writes of this wave visible to its other lanes
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
 
-struct __align__(16) RSmem {
-    uint8_t  buf[2][TILE + HALO];
-    uint32_t T[4 * 256];         // slice-by-4 CRC tables
-    uint32_t KT[8 * 8 * 16];     // [j][nibble i][n]: (n << 4i) * x^(8*64*2^j)
-    uint32_t IX[68];             // 0xFFFFFFFF * x^(8j): initial register pushed through j bytes
-    union { uint16_t rec[MAXREC]; ScanLds sc; } r;
-    union { SpecLds sp; LongLds lg; } u;
-    uint32_t wt[4];
-    uint64_t entry, tile_exit, err_pos, err_aux, stripe_entry, pool_base, chunk_base, chunk_left;
-    uint64_t c_vb, c_ve, c_idx;           // carried long value: 1 = crosses the tile start (c_state
-    uint64_t n_vb, n_ve, n_idx;           //   valid), 2 = pending (starts in a later tile); n_* = next tile's
-    uint32_t carry, c_state, n_carry, n_state;
-    uint32_t err_kind, nrec, nlong, total, search, stop, prev_n, cand_min, need_spec, spec_total, err_rec;
-};
-
-#define KVR_BARRIER()                                          \
-    do {                                                       \
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     \
-        __builtin_amdgcn_s_barrier();                          \
-        asm volatile("" ::: "memory");                         \
-    } while (0)
-
-#ifdef KVR_PROF
-__device__ unsigned long long g_prof[16];
-#define KVR_STAMP(i)                                                        \
-    do {                                                                    \
-        if (threadIdx.x == 0) {                                             \
-            const unsigned long long t_ = __builtin_amdgcn_s_memtime();     \
-            atomicAdd(&g_prof[i], t_ - t_last);                             \
-            t_last = t_;                                                    \
-        }                                                                   \
-    } while (0)
-#else
-#define KVR_STAMP(i) do { } while (0)
-#endif
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {   // wave-uniform value into SGPRs
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // ---------------------------------------------------------------------------------------
-// CRC primitives on the LDS byte tables
+// CRC primitives on the LDS tables
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t crc4(uint32_t c, uint32_t w, const uint32_t *T) {
     c ^= w;
@@ -122,12 +98,16 @@ __device__ inline uint32_t crc_range(const TileView &tv, uint32_t c, uint64_t p,
     if (tv.in_lds(p, n)) {
         int off = (int)((int64_t)p - tv.lo);
         const int end = off + (int)n;
+        #pragma unroll 1
         while (off < end && (off & 3)) { c = crc1(c, tv.lds[off], T); ++off; }
         const uint32_t *w = reinterpret_cast<const uint32_t *>(tv.lds);
+        #pragma unroll 1
         while (off + 4 <= end) { c = crc4(c, w[off >> 2], T); off += 4; }
+        #pragma unroll 1
         while (off < end) { c = crc1(c, tv.lds[off], T); ++off; }
         return c;
     }
+    #pragma unroll 1
     for (uint64_t i = 0; i < n; ++i) c = crc1(c, tv.rd8(p + i), T);
     return c;
 }
@@ -164,6 +144,7 @@ __device__ __forceinline__ bool key_prefix_ok(const TileView &tv, int off_k, uin
     m = m > 16 ? 16 : m;
     m = (uint32_t)m > klen ? (int)klen : m;
     int i = 0;
+    #pragma unroll 1
     while (i < m) {
         const uint32_t b = tv.lds[off_k + i];
         if (b == 0u) return false;
@@ -202,16 +183,18 @@ __device__ __forceinline__ bool plausible(const TileView &tv, uint64_t p) {
 }
 
 // first plausible record start in [p0, p1) (inside the tile), or NONE
-__device__ inline uint64_t find_cand(const TileView &tv, uint64_t p0, uint64_t p1) {
+__device__ __noinline__ uint64_t find_cand(const TileView tv, uint64_t p0, uint64_t p1) {
     if (p0 >= p1) return NONE;
     const int o0 = (int)((int64_t)p0 - tv.lo), o1 = (int)((int64_t)p1 - tv.lo);
     const uint32_t *w = reinterpret_cast<const uint32_t *>(tv.lds);
+    #pragma unroll 1
     for (int q = o0 >> 2; q <= (o1 - 1) >> 2; ++q) {
         const uint32_t y = w[q] & 0xFEFEFEFEu;                 // bytes 0x00 / 0x01 become 0
         uint32_t z = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
         const int bq = q * 4;
         if (bq < o0) z &= ~0u << (8 * (o0 - bq));
         if (bq + 4 > o1) z &= (1u << (8 * (o1 - bq))) - 1u;
+        #pragma unroll 1
         while (z) {
             const int b = __builtin_ctz(z) >> 3;
             const uint64_t p = (uint64_t)(tv.lo + bq + b);
@@ -222,7 +205,8 @@ __device__ inline uint64_t find_cand(const TileView &tv, uint64_t p0, uint64_t p
     return NONE;
 }
 
-// Walk from p while p < pe: records walked, last record start, exit offset (X_BEYOND/X_ERR)
+// Walk from p while p < pe: records walked (a record whose framing fails counts: its parse
+// reports the error), last record start, exit offset (X_BEYOND / X_ERR)
 __device__ inline uint32_t walk_spec(const TileView &tv, uint64_t p, uint64_t pe, uint32_t *exit_off,
                                      uint16_t *last_off) {
     uint32_t cnt = 0;
@@ -235,8 +219,8 @@ __device__ inline uint32_t walk_spec(const TileView &tv, uint64_t p, uint64_t pe
             break;
         }
         const uint64_t nx = next_spec(tv, p);
-        ++cnt;                                     // a record whose framing fails is still one:
-        last = (uint16_t)((int64_t)p - tv.lo);     // its parse reports the error
+        ++cnt;
+        last = (uint16_t)((int64_t)p - tv.lo);
         if (nx == ERRP) { x = X_ERR; break; }
         if (nx == BEYOND) { x = X_BEYOND; break; }
         p = nx;
@@ -246,291 +230,298 @@ __device__ inline uint32_t walk_spec(const TileView &tv, uint64_t p, uint64_t pe
     return cnt;
 }
 
-// ---------------------------------------------------------------------------------------
-// stitching of the speculated sub-chains (wave 0)
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ void wave_sync_lds() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-}
-
-__device__ __forceinline__ int wave_max_i32(int v) {
-    for (int d = 32; d >= 1; d >>= 1) {
-        const int o = __shfl_xor(v, d, 64);
-        v = o > v ? o : v;
-    }
-    return v;
-}
-
-// lane 0: the true chain enters the sub-chunk holding y at y; re-walk it and the following
-// sub-chunks whose speculation disagrees with the true chain (bounded per call)
-__device__ void repair(SpecLds &P, const TileView &tv, uint64_t y, uint64_t vhi) {
+// lane 0: the true chain enters the unit holding y at y; re-walk it and the following units
+// whose speculation disagrees with the true chain (bounded per call)
+__device__ void repair(WaveLds &W, const TileView &tv, uint64_t y, uint64_t vhi) {
     const int64_t lo = tv.lo;
-    for (int k = 0; k < 64; ++k) {
+    for (int k = 0; k < UNITS; ++k) {
         const int t = (int)(((int64_t)y - lo) / SC);
         const int64_t ce = lo + (int64_t)(t + 1) * SC;
         const uint64_t pe = (uint64_t)ce > vhi ? vhi : (uint64_t)ce;
         uint32_t x;
         uint16_t last;
         const uint32_t cnt = walk_spec(tv, y, pe, &x, &last);
-        P.sc_cand[t] = (uint16_t)((int64_t)y - lo);
-        P.sc_exit[t] = x;
-        P.sc_cnt[t] = (uint16_t)cnt;
-        P.sc_last[t] = last;
+        W.sc_cand[t] = (uint16_t)((int64_t)y - lo);
+        W.sc_exit[t] = x;
+        W.sc_cnt[t] = (uint16_t)cnt;
+        W.sc_last[t] = last;
         if (x >= X_BEYOND || lo + (int64_t)x >= (int64_t)vhi) return;
-        if (P.sc_cand[x / SC] == x) return;        // back in step with the speculation
+        if (W.sc_cand[x / SC] == x) return;        // back in step with the speculation
         y = (uint64_t)(lo + (int64_t)x);
     }
 }
 
-// Stitch from the exact position e (vlo <= e < vhi): publishes sc_entry / sc_base of the
-// sub-chunks on the true chain, S.spec_total and S.tile_exit.
-__device__ void stitch(RSmem &S, const TileView &tv, uint64_t e, uint64_t vhi, Counters *ctr) {
-    SpecLds &P = S.u.sp;
-    const int lane = threadIdx.x;
+struct Stitched { uint16_t ent; uint32_t cnt, base, total; uint64_t exit; };
+
+// Stitch the per-unit chains from the exact position e (vlo <= e < vhi) by pointer jumping:
+// per lane its unit's entry on the true chain (or N16) and record count/base; the tile exit.
+__device__ __noinline__ Stitched stitch(WaveLds &W, const TileView tv, uint64_t e, uint64_t vhi, Counters *ctr) {
+    const int lane = threadIdx.x & 63;
     const int64_t lo = tv.lo;
     const int s0 = (int)(((int64_t)e - lo) / SC);
     const uint16_t e_off = (uint16_t)((int64_t)e - lo);
     const uint32_t vhi_off = (uint32_t)((int64_t)vhi - lo);
-    for (int guard = 0; guard < 2 * NT + 8; ++guard) {
-        if (P.sc_cand[s0] != e_off) {
-            if (lane == 0) repair(P, tv, e, vhi);
-            wave_sync_lds();
+    Stitched R;
+    for (int guard = 0; guard < 2 * UNITS + 8; ++guard) {
+        if (W.sc_cand[s0] != e_off) {
+            if (lane == 0) repair(W, tv, e, vhi);
+            wsync();
             continue;
         }
-        bool any = false;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int s = 4 * lane + j;
-            const uint16_t c = P.sc_cand[s];
-            const uint32_t x = P.sc_exit[s];
-            int16_t T;
-            if (c == N16) T = T_END;
-            else if (x == X_ERR) T = T_ERR;
-            else if (x >= vhi_off) T = T_END;          // includes X_BEYOND
-            else { const int t = (int)(x / SC); T = (P.sc_cand[t] == x) ? (int16_t)t : T_MM; any = true; }
-            P.nxt0[s] = T;
-            P.nxt[s] = T;
-            P.reach[s] = (s == s0) ? 1 : 0;
+        const uint16_t c = W.sc_cand[lane];
+        const uint32_t x = W.sc_exit[lane];
+        int T;
+        if (c == N16) T = T_END;
+        else if (x == X_ERR) T = T_ERR;
+        else if (x >= vhi_off) T = T_END;              // includes X_BEYOND
+        else { const int t = (int)(x / SC); T = (W.sc_cand[t] == x) ? t : T_MM; }
+        W.reach[lane] = lane == s0 ? 1 : 0;
+        wsync();
+        int J = T;
+        bool reach = lane == s0;
+        for (int r = 0; r < 7 && __any(J < UNITS); ++r) {   // J <- J o J, reach <- reach U J(reach)
+            if (J < UNITS && reach) W.reach[J] = 1;
+            const int jn = J < UNITS ? __shfl(J, J, 64) : J;
+            wsync();
+            reach = W.reach[lane] != 0;
+            J = jn;
         }
-        wave_sync_lds();
-        for (int r = 0; r < 8 && __any(any); ++r) {   // J <- J o J, reach <- reach U J(reach)
-            int16_t jn[4];
-            any = false;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int s = 4 * lane + j;
-                const int16_t J = P.nxt[s];
-                jn[j] = J < NT ? P.nxt[J] : J;
-                any |= jn[j] < NT;
-                if (J < NT && P.reach[s]) P.reach[J] = 1;
-            }
-            wave_sync_lds();
-#pragma unroll
-            for (int j = 0; j < 4; ++j) P.nxt[4 * lane + j] = jn[j];
-            wave_sync_lds();
-        }
-        int smax = -1;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) if (P.reach[4 * lane + j]) smax = 4 * lane + j;
-        smax = wave_max_i32(smax);
-        const int16_t Tl = P.nxt0[smax];
+        const unsigned long long rm = __ballot(reach);
+        const int smax = 63 - __builtin_clzll(rm);
+        const int Tl = __shfl(T, smax, 64);
+        const uint32_t xs = __shfl(x, smax, 64);
         if (Tl == T_MM) {
-            if (lane == 0) repair(P, tv, (uint64_t)(lo + (int64_t)P.sc_exit[smax]), vhi);
-            wave_sync_lds();
+            if (lane == 0) repair(W, tv, (uint64_t)(lo + (int64_t)xs), vhi);
+            wsync();
             continue;
         }
-        // accepted path: entries and record index bases
-        uint16_t ent[4];
-        uint32_t c4[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int s = 4 * lane + j;
-            const bool on = P.reach[s] != 0;
-            ent[j] = on ? P.sc_cand[s] : N16;
-            c4[j] = on ? P.sc_cnt[s] : 0u;
-        }
-        const uint32_t tot = c4[0] + c4[1] + c4[2] + c4[3];
-        uint32_t inc = tot;
+        R.ent = reach ? c : N16;
+        R.cnt = reach ? W.sc_cnt[lane] : 0u;
+        uint32_t inc = R.cnt;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const uint32_t o = __shfl_up(inc, d, 64);
             if (lane >= d) inc += o;
         }
-        uint32_t base = inc - tot;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int s = 4 * lane + j;
-            P.sc_entry[s] = ent[j];
-            P.sc_base[s] = base;
-            base += c4[j];
-        }
-        const uint32_t total = __shfl(inc, 63, 64);
-        if (lane == 0) {
-            S.spec_total = total;
-            uint64_t x;
-            if (Tl == T_ERR) x = ERRP;
-            else if (P.sc_exit[smax] != X_BEYOND) x = (uint64_t)(lo + (int64_t)P.sc_exit[smax]);
-            else x = next_rec(tv, (uint64_t)(lo + (int64_t)P.sc_last[smax]));   // exact, halo / HBM
-            S.tile_exit = x;
-        }
-        return;
+        R.base = inc - R.cnt;
+        R.total = uni32(__shfl(inc, 63, 64));
+        uint64_t xe;
+        if (Tl == T_ERR) xe = ERRP;
+        else if (xs != X_BEYOND) xe = (uint64_t)(lo + (int64_t)xs);
+        else xe = next_rec(tv, (uint64_t)(lo + (int64_t)W.sc_last[smax]));   // exact, halo / HBM
+        R.exit = uni64(xe);
+        return R;
     }
-    if (lane == 0) {   // unreachable: every round repairs one more sub-chunk for good (bug trap)
-        S.spec_total = 0;
-        S.tile_exit = ERRP;
-        atomicOr(&ctr->overflow, 2u);
-    }
-}
-
-// async HBM -> LDS copy of tile k and its halo (16-B LDS-DMA per lane; wave w of instruction i
-// lands at byte (i * NT + w * 64) * 16; the halo, the next HALO bytes, lands at TILE)
-__device__ __forceinline__ void issue_tile(const SegDesc &sg, uint32_t k, uint8_t *dst) {
-    const int tid = threadIdx.x, wave = tid >> 6;
-    const int64_t lo = (int64_t)k * TILE - (int64_t)sg.d0;
-    const uint8_t *abase = sg.base - sg.d0 + (int64_t)k * TILE;
-#pragma unroll
-    for (int i = 0; i < TILE / 16 / NT; ++i) {
-        const int w = i * NT + tid;
-        const int64_t pos = lo + 16 * (int64_t)w;
-        if (pos + 16 > 0 && pos < (int64_t)sg.len) {
-            __builtin_amdgcn_global_load_lds(
-                reinterpret_cast<const void *>(abase + 16 * w),
-                reinterpret_cast<__attribute__((address_space(3))) void *>(
-                    (__attribute__((address_space(3))) uint8_t *)(dst + (i * NT + wave * 64) * 16)),
-                16, 0, 0);
-        }
-    }
-    if (tid < HALO / 16) {
-        const int64_t pos = lo + TILE + 16 * (int64_t)tid;
-        if (pos < (int64_t)sg.len) {
-            __builtin_amdgcn_global_load_lds(
-                reinterpret_cast<const void *>(abase + TILE + 16 * tid),
-                reinterpret_cast<__attribute__((address_space(3))) void *>(
-                    (__attribute__((address_space(3))) uint8_t *)(dst + TILE)),
-                16, 0, 0);
-        }
-    }
+    if (lane == 0) atomicOr(&ctr->overflow, 2u);   // unreachable: every round repairs one more unit (bug trap)
+    R.ent = N16; R.cnt = 0; R.base = 0; R.total = 0; R.exit = ERRP;
+    return R;
 }
 
 // ---------------------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------------------
+struct RecRes {          // one record's outcome
+    uint32_t err, kind;  // record index of an error (N32: none) and its KVR_E_* kind
+    uint64_t aux;
+    uint32_t hand;       // 1: its long value crosses the tile end, 2: its value starts in a later tile
+    uint64_t vb, ve, slot;
+};
+
+// parse + emit the record at p (engine.rs order of checks); long values register with the tile
+__device__ __forceinline__ RecRes do_record(const TileView &tv, WaveLds &W, const uint32_t *T, uint64_t p, uint32_t j,
+                                         uint64_t slot, uint32_t seg, kvr_tuple *pool, uint64_t pool_cap) {
+    RecRes ro;
+    ro.err = N32; ro.kind = 0; ro.aux = 0; ro.hand = 0; ro.vb = 0; ro.ve = 0; ro.slot = slot;
+    const uint64_t len = tv.len;
+    const int64_t lo = tv.lo;
+    const uint32_t op = tv.rd8(p);
+    if (len - p < 5) { ro.err = j; ro.kind = KVR_E_KEY_LEN; return ro; }                 // engine.rs:96
+    const uint64_t klen = tv.rd32(p + 1);
+    const uint64_t kb = p + 5;
+    if (len - kb < klen) { ro.err = j; ro.kind = KVR_E_KEY; return ro; }                  // engine.rs:107
+    uint64_t vu = 0;
+    uint32_t el = 0;
+    if (!utf8_check(tv, kb, klen, &vu, &el)) {                                          // engine.rs:114
+        ro.err = j; ro.kind = KVR_E_UTF8; ro.aux = vu | ((uint64_t)el << 32); return ro;
+    }
+    if (op > 1u) { ro.err = j; ro.kind = KVR_E_OPCODE; ro.aux = op; return ro; }          // engine.rs:143
+    kvr_tuple t;
+    t.rec_off = p;
+    t.seg_idx = seg;
+    t.key_len = (uint32_t)klen;
+    t.key_tag = ~crc_range(tv, ~0u, kb, klen, T);
+    t.op = (uint8_t)op;
+    t.flags = 0;
+    t.reserved = 0;
+    t.crc32 = 0;
+    t.val_len = 0;
+    if (op == 0u) {
+        const uint64_t q = kb + klen;
+        if (len - q < 4) { ro.err = j; ro.kind = KVR_E_VAL_LEN; return ro; }              // engine.rs:121
+        const uint64_t vlen = tv.rd32(q);
+        const uint64_t vb = q + 4, ve = vb + vlen;
+        if (len - vb < vlen) { ro.err = j; ro.kind = KVR_E_VAL; return ro; }              // engine.rs:130
+        t.val_len = (uint32_t)vlen;
+        if (vlen <= (uint64_t)SMALL) {
+            t.crc32 = ~crc_range(tv, ~0u, vb, vlen, T);
+        } else {
+            const int64_t vbr = (int64_t)vb - lo, ver = (int64_t)ve - lo;
+            if (vbr < TILE) {
+                const uint32_t L = atomicAdd(&W.nlong, 1u);
+                W.lvb[L] = (int32_t)vbr;
+                W.lve[L] = ver > FAR ? FAR : (int32_t)ver;
+                W.lidx[L] = (uint32_t)slot;
+                W.bkey[vbr / SC + 1] = ((uint32_t)(vbr + 1) << 7) | L;
+                if (ver > TILE) { ro.hand = 1; ro.vb = vb; ro.ve = ve; }   // runs past the tile
+            } else {                       // the value starts in a later tile
+                ro.hand = 2; ro.vb = vb; ro.ve = ve;
+            }
+        }
+    }
+    if (slot < pool_cap) pool[slot] = t;
+    return ro;
+}
+
+// this lane's 64-B unit of tile k (16-B loads; bytes outside the segment read as 0)
+__device__ __forceinline__ void load_unit(const uint8_t *abase, int64_t d0, uint64_t len, uint32_t k, int lane,
+                                          uint4 &r0, uint4 &r1, uint4 &r2, uint4 &r3) {
+    const int64_t pos = (int64_t)k * TILE - d0 + lane * SC;
+    const uint4 *u = reinterpret_cast<const uint4 *>(abase + (int64_t)k * TILE + lane * SC);
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    r0 = (pos + 16 > 0 && pos < (int64_t)len) ? u[0] : z;
+    r1 = (pos + 32 > 0 && pos + 16 < (int64_t)len) ? u[1] : z;
+    r2 = (pos + 48 > 0 && pos + 32 < (int64_t)len) ? u[2] : z;
+    r3 = (pos + 64 > 0 && pos + 48 < (int64_t)len) ? u[3] : z;
+}
+
+// halo of tile k: the next HALO bytes after it, LDS-DMA into tile + TILE (lanes 0 .. HALO/16-1)
+__device__ __forceinline__ void load_halo(const uint8_t *abase, int64_t d0, uint64_t len, uint32_t k, int lane,
+                                          uint8_t *tile) {
+    if (lane < HALO / 16) {
+        const int64_t pos = (int64_t)k * TILE - d0 + TILE + 16 * lane;
+        if (pos < (int64_t)len)
+            __builtin_amdgcn_global_load_lds(
+                reinterpret_cast<const void *>(abase + (int64_t)k * TILE + TILE + 16 * lane),
+                reinterpret_cast<__attribute__((address_space(3))) void *>(
+                    (__attribute__((address_space(3))) uint8_t *)(tile + TILE)),
+                16, 0, 0);
+    }
+}
+
 __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ segs,
-                                                  const StripeDesc *__restrict__ stripes,
-                                                  StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
-                                                  kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
-                                                  Tables tb, const RedoEnt *__restrict__ redo,
-                                                  const LinkResult *__restrict__ link, int redo_mode,
-                                                  uint32_t pool_chunk) {
-    __shared__ RSmem S;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+                                               const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
+                                               StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
+                                               kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
+                                               Tables tb, const RedoEnt *__restrict__ redo,
+                                               const LinkResult *__restrict__ link, int redo_mode,
+                                               uint32_t pool_chunk) {
+    __shared__ Smem S;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int i = tid; i < 4 * 256; i += NT) S.T[i] = tb.crc8[i];
+    for (int i = tid; i < 6 * 8 * 16; i += NT) S.KT[i] = tb.kmul[i];
+    if (tid < 65) S.IX[tid] = tb.initx[tid];
+    __syncthreads();   // the only workgroup barrier: from here on every wave is on its own
+
+    const uint32_t gw = blockIdx.x * WPB + wv;
     uint32_t si;
     uint64_t forced = NONE;
     if (redo_mode) {
-        if (blockIdx.x >= link->n_redo || link->status != 3) return;
-        si = redo[blockIdx.x].stripe;
-        forced = redo[blockIdx.x].entry;
+        if (gw >= link->n_redo || link->status != 3) return;
+        si = redo[gw].stripe;
+        forced = redo[gw].entry;
     } else {
-        si = blockIdx.x;
+        if (gw >= n_stripes) return;
+        si = gw;
     }
+    WaveLds &W = S.w[wv];
     const StripeDesc sd = stripes[si];
     const SegDesc sg = segs[sd.seg];
     const uint64_t len = sg.len;
     const int64_t d0 = sg.d0;
     const int64_t shi_i = (int64_t)sd.t_end * TILE - d0;
     const uint64_t s_hi = (uint64_t)shi_i > len ? len : (uint64_t)shi_i;
+    const uint8_t *abase = sg.base - d0;   // 16-B aligned: tile k starts at abase + k * TILE
 
-    for (int i = tid; i < 4 * 256; i += NT) S.T[i] = tb.crc8[i];
-    for (int i = tid; i < 8 * 8 * 16; i += NT) S.KT[i] = tb.kmul[i];
-    if (tid < 65) S.IX[tid] = tb.initx[tid];
-    if (tid == 0) {
-        S.carry = 0; S.n_carry = 0;
-        S.err_kind = 0; S.err_pos = NONE; S.err_aux = 0; S.err_rec = N32;
-        S.total = 0; S.stop = 0; S.prev_n = 0;
-        S.chunk_left = 0; S.chunk_base = 0;
-        S.nrec = 0; S.need_spec = 0; S.cand_min = N32; S.nlong = 0;
-        const uint64_t e = redo_mode ? forced : ((sd.t_begin == 0) ? 0ull : NONE);
-        S.search = (e == NONE);
-        S.entry = e;
-        S.stripe_entry = (e != NONE && e >= s_hi) ? NONE : e;
-        if (e != NONE && e >= s_hi) S.stop = 2;   // imposed entry beyond the stripe: nothing starts here
-        const int64_t slo_i = (int64_t)sd.t_begin * TILE - d0;
-        if (e != NONE && (int64_t)e < slo_i) {     // k_link never imposes an entry before the stripe (bug trap)
-            S.stop = 2;
-            S.stripe_entry = NONE;
-            atomicOr(&ctr->overflow, 4u);
-        }
-        S.tile_exit = S.entry;
+    // stripe state (wave-uniform)
+    uint64_t entry = redo_mode ? forced : ((sd.t_begin == 0) ? 0ull : NONE);
+    bool search = entry == NONE;
+    uint64_t stripe_entry = (entry != NONE && entry >= s_hi) ? NONE : entry;
+    int stop = (entry != NONE && entry >= s_hi) ? 2 : 0;   // imposed entry beyond the stripe: nothing starts here
+    if (entry != NONE && (int64_t)entry < (int64_t)sd.t_begin * TILE - d0) {   // bug trap: k_link never does this
+        stop = 2;
+        stripe_entry = NONE;
+        if (lane == 0) atomicOr(&ctr->overflow, 4u);
     }
-    issue_tile(sg, sd.t_begin, S.buf[0]);
-#ifdef KVR_PROF
-    unsigned long long t_last = __builtin_amdgcn_s_memtime();
-#endif
+    uint64_t err_pos = NONE, err_aux = 0;
+    uint32_t err_kind = 0, total = 0, prev_n = 0;
+    uint64_t chunk_base = 0, chunk_left = 0;
+    uint32_t carry = 0, c_state = 0;      // 1: a long value crosses the tile start (c_state valid);
+    uint64_t c_vb = 0, c_ve = 0, c_idx = 0;   // 2: pending (its value starts in a later tile)
+
+    uint4 nx0, nx1, nx2, nx3;   // this lane's unit of the next tile (prefetch)
+    load_unit(abase, d0, len, sd.t_begin, lane, nx0, nx1, nx2, nx3);
+    load_halo(abase, d0, len, sd.t_begin, lane, W.tile);
+    bool loaded = true;
     uint32_t k = sd.t_begin;
-    int cur = 0;
-    bool loaded = true;   // tile k has been issued into buf[cur]
-    for (;; ++k, cur ^= 1) {
+    for (;; ++k) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        KVR_BARRIER();
         const bool in_stripe = k < sd.t_end;
-        if (S.stop || (!in_stripe && !S.carry) || k >= sg.n_tiles) break;
-        if (!loaded) {   // not prefetched (stripe end): load now
-            issue_tile(sg, k, S.buf[cur]);
+        if (stop || (!in_stripe && !carry) || k >= sg.n_tiles) break;
+        if (!loaded) {
+            load_unit(abase, d0, len, k, lane, nx0, nx1, nx2, nx3);
+            load_halo(abase, d0, len, k, lane, W.tile);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            KVR_BARRIER();
         }
-        // prefetch the next tile while this one is processed
-        loaded = (k + 1 < sg.n_tiles) && (k + 1 < sd.t_end || S.carry);
-        if (loaded) issue_tile(sg, k + 1, S.buf[cur ^ 1]);
-        KVR_STAMP(0);
+        {
+            uint4 *tp = reinterpret_cast<uint4 *>(W.tile + lane * SC);
+            tp[0] = nx0; tp[1] = nx1; tp[2] = nx2; tp[3] = nx3;
+        }
+        loaded = (k + 1 < sg.n_tiles) && (k + 1 < sd.t_end || carry);
+        if (loaded) load_unit(abase, d0, len, k + 1, lane, nx0, nx1, nx2, nx3);
+        if (lane == 0) W.nlong = 0;
+        W.bkey[lane + 1] = 0u;
+        wsync();
 
         const int64_t lo = (int64_t)k * TILE - d0;
         const uint64_t vlo = lo < 0 ? 0ull : (uint64_t)lo;
         const uint64_t vhi = (uint64_t)(lo + TILE) > len ? len : (uint64_t)(lo + TILE);
-        uint8_t *tile = S.buf[cur];
-        const TileView tv{sg.base, tile, len, lo};
-        const int64_t cs_i = lo + (int64_t)tid * SC;
+        const TileView tv{sg.base, W.tile, len, lo};
+        const int64_t cs_i = lo + (int64_t)lane * SC;
         const uint64_t cs = cs_i < (int64_t)vlo ? vlo : (uint64_t)cs_i;
         const uint64_t ce = (uint64_t)(cs_i + SC) > vhi ? vhi : (uint64_t)(cs_i + SC);
 
-        // ---- F. framing --------------------------------------------------------------------
-        if (in_stripe && S.search) {   // the stripe's entry: the first plausible record start
-            if (cs < ce) {
-                const uint64_t cand = find_cand(tv, cs, ce);
-                if (cand != NONE) atomicMin(&S.cand_min, (uint32_t)((int64_t)cand - lo));
+        // ---- F. framing ------------------------------------------------------------------------
+        if (in_stripe && search) {   // the stripe's entry: the first plausible record start
+            const uint64_t cand = cs < ce ? find_cand(tv, cs, ce) : NONE;
+            uint64_t m = cand;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+                const uint64_t o = __shfl_xor(m, d, 64);
+                m = o < m ? o : m;
             }
-            KVR_BARRIER();
-            if (tid == 0 && S.cand_min != N32) {
-                S.entry = (uint64_t)(lo + (int64_t)S.cand_min);
-                S.search = 0;
-                S.stripe_entry = S.entry;
-                S.tile_exit = S.entry;
-            }
-            KVR_BARRIER();
+            m = uni64(m);
+            if (m != NONE) { entry = m; search = false; stripe_entry = m; }
         }
-        const bool walk = in_stripe && !S.search && S.entry < vhi;
+        const bool walk = in_stripe && !search && entry < vhi;
+        uint64_t tile_exit = entry;
+        uint32_t n_hop = 0, myrec = N32;
+        Stitched st;
+        st.ent = N16; st.cnt = 0; st.base = 0; st.total = 0;
         if (walk) {
-            if (tid == 0) {   // exact hops while the tile looks sparse
-                uint64_t p = S.entry;
-                uint32_t n = 0;
-                if (S.prev_n <= DENSE) {
-                    while (p < vhi && n < HOP_BUDGET) {
-                        S.r.rec[n++] = (uint16_t)((int64_t)p - lo);
-                        p = next_rec(tv, p);
-                        if (p == ERRP) break;
-                    }
+            uint64_t p = entry;
+            if (prev_n <= DENSE) {   // exact hops, all lanes together (LDS broadcast reads)
+                while (p < vhi && n_hop < HOP_MAX) {
+                    if (lane == (int)n_hop) myrec = (uint32_t)((int64_t)p - lo);
+                    ++n_hop;
+                    p = uni64(next_rec(tv, p));
+                    if (p == ERRP) break;
                 }
-                S.nrec = n;
-                S.tile_exit = p;
-                S.need_spec = (p != ERRP && p < vhi) ? 1u : 0u;
             }
-            KVR_BARRIER();
-            if (S.need_spec) {   // dense: speculate per sub-chunk from the exact position e
-                const uint64_t e = S.tile_exit;
+            tile_exit = p;
+            if (p != ERRP && p < vhi) {   // dense: speculate per unit from the exact position p
                 uint16_t cand16 = N16, last16 = N16;
                 uint32_t x = X_BEYOND, cnt = 0;
-                const uint64_t p0 = cs > e ? cs : e;
+                const uint64_t p0 = cs > p ? cs : p;
                 if (p0 < ce) {
                     const uint64_t cand = find_cand(tv, p0, ce);
                     if (cand != NONE) {
@@ -538,161 +529,141 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
                         cnt = walk_spec(tv, cand, ce, &x, &last16);
                     }
                 }
-                S.u.sp.sc_cand[tid] = cand16;
-                S.u.sp.sc_exit[tid] = x;
-                S.u.sp.sc_cnt[tid] = (uint16_t)cnt;
-                S.u.sp.sc_last[tid] = last16;
-                KVR_BARRIER();
-                if (tid < 64) stitch(S, tv, e, vhi, ctr);
-                KVR_BARRIER();
-                const uint16_t ent = S.u.sp.sc_entry[tid];
-                if (ent != N16) {   // materialize the record starts of this sub-chunk
-                    uint32_t o = S.nrec + S.u.sp.sc_base[tid];
-                    uint64_t p = (uint64_t)(lo + (int64_t)ent);
-                    const uint32_t c = S.u.sp.sc_cnt[tid];
-                    for (uint32_t i = 0; i < c; ++i) {
-                        S.r.rec[o + i] = (uint16_t)((int64_t)p - lo);
-                        if (i + 1 < c) p = next_spec(tv, p);
-                    }
-                }
-                KVR_BARRIER();
-                if (tid == 0) S.nrec += S.spec_total;
+                W.sc_cand[lane] = cand16;
+                W.sc_exit[lane] = x;
+                W.sc_cnt[lane] = (uint16_t)cnt;
+                W.sc_last[lane] = last16;
+                wsync();
+                st = stitch(W, tv, p, vhi, ctr);
+                tile_exit = st.exit;
             }
         }
-        // tile setup: pool slots, long-value registry (zeroed after the speculation arrays die)
+        const uint32_t nrec = n_hop + st.total;
+        // pool slots for this tile's records (bulk chunks)
+        if (nrec > chunk_left) {
+            const uint64_t m = nrec > pool_chunk ? nrec : pool_chunk;
+            unsigned long long b = 0;
+            if (lane == 0) {
+                b = atomicAdd(&ctr->pool_cursor, (unsigned long long)m);
+                if (b + m > pool_cap) atomicOr(&ctr->overflow, 1u);
+            }
+            chunk_base = uni64(b);
+            chunk_left = m;
+        }
+        const uint64_t pool_base = chunk_base;
+        chunk_base += nrec;
+        chunk_left -= nrec;
+        // a value whose record started in an earlier tile begins in this one: register it
+        uint32_t n_carry = 0;
+        uint64_t n_vb = 0, n_ve = 0, n_idx = 0;
+        if (carry == 2u) {
+            if ((int64_t)c_vb - lo < TILE) {
+                if (lane == 0) {
+                    const int32_t pvb = (int32_t)((int64_t)c_vb - lo);
+                    const int64_t ve = (int64_t)c_ve - lo;
+                    W.lvb[0] = pvb;
+                    W.lve[0] = ve > FAR ? FAR : (int32_t)ve;
+                    W.lidx[0] = (uint32_t)c_idx;
+                    W.bkey[pvb / SC + 1] = (uint32_t)(pvb + 1) << 7;
+                    W.nlong = 1;
+                }
+                carry = 0;
+                n_vb = c_vb; n_ve = c_ve; n_idx = c_idx;   // in case it also runs past this tile
+            } else {                        // still further on: hand it over untouched
+                n_carry = 2; n_vb = c_vb; n_ve = c_ve; n_idx = c_idx;
+            }
+        }
+        wsync();
+
+        // ---- R. records ----------------------------------------------------------------------
+        RecRes ro;
+        ro.err = N32; ro.kind = 0; ro.aux = 0; ro.hand = 0; ro.vb = 0; ro.ve = 0; ro.slot = 0;
+        uint32_t hand = 0;
+        uint64_t pvb = 0, pve = 0, pidx = 0;
+        {   // this lane's records: its hop record (record index = lane), then its unit's speculated ones
+            const uint32_t has_hop = myrec != N32 ? 1u : 0u;
+            const uint32_t nmine = has_hop + (st.ent != N16 ? st.cnt : 0u);
+            uint64_t ps = (uint64_t)(lo + (int64_t)st.ent);
+            for (uint32_t i = 0; i < nmine; ++i) {
+                const bool h = i < has_hop;
+                const uint64_t p = h ? (uint64_t)(lo + (int64_t)myrec) : ps;
+                const uint32_t j = h ? (uint32_t)lane : n_hop + st.base + (i - has_hop);
+                ro = do_record(tv, W, S.T, p, j, pool_base + j, sd.seg, pool, pool_cap);
+                if (ro.hand) { hand = ro.hand; pvb = ro.vb; pve = ro.ve; pidx = ro.slot; }
+                if (ro.err != N32) break;
+                if (!h && i + 1 < nmine) ps = next_spec(tv, ps);
+            }
+        }
+        // first error of the tile (lowest record index)
+        uint32_t err_rec = ro.err;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t o = __shfl_xor(err_rec, d, 64);
+            err_rec = o < err_rec ? o : err_rec;
+        }
+        err_rec = uni32(err_rec);
+        if (err_rec != N32) {
+            const int el = __builtin_ctzll(__ballot(ro.err == err_rec));
+            err_kind = uni32(__shfl(ro.kind, el, 64));
+            err_aux = uni64(__shfl(ro.aux, el, 64));
+            // the failing record's start: hop records live in myrec, speculated ones are re-found
+            uint64_t ep = NONE;
+            if (ro.err == err_rec) {
+                if (err_rec < n_hop) ep = (uint64_t)(lo + (int64_t)myrec);
+                else {
+                    uint64_t p = (uint64_t)(lo + (int64_t)st.ent);
+                    for (uint32_t i = n_hop + st.base; i < err_rec; ++i) p = next_spec(tv, p);
+                    ep = p;
+                }
+            }
+            err_pos = uni64(__shfl(ep, el, 64));
+        }
+        // a long value crossing the tile end / starting later (one at most): its lane hands it over
         {
-            const bool pend = S.carry == 2u && (int64_t)S.c_vb - lo < TILE;
-            const int32_t pvb = pend ? (int32_t)((int64_t)S.c_vb - lo) : 0;
-            const uint32_t pb1 = pend ? (uint32_t)(pvb / SC + 1) : 0u;
-            S.u.lg.bkey[tid + 1] = (pend && pb1 == (uint32_t)tid + 1) ? (((uint32_t)pvb + 1u) << 9) : 0u;
-            if (tid == 0) {
-                const uint32_t n = S.nrec;
-                if (n > S.chunk_left) {                   // bulk pool allocation
-                    const uint64_t m = n > pool_chunk ? n : pool_chunk;
-                    S.chunk_base = atomicAdd(&ctr->pool_cursor, (unsigned long long)m);
-                    S.chunk_left = m;
-                    if (S.chunk_base + m > pool_cap) atomicOr(&ctr->overflow, 1u);
-                }
-                S.pool_base = S.chunk_base;
-                S.chunk_base += n;
-                S.chunk_left -= n;
-                S.nlong = 0;
-                S.n_carry = 0;
-                if (pend) {   // a value whose record started in an earlier tile begins in this one
-                    const int64_t ve = (int64_t)S.c_ve - lo;
-                    S.u.lg.lvb[0] = pvb;
-                    S.u.lg.lve[0] = ve > FAR ? FAR : (int32_t)ve;
-                    S.u.lg.lidx[0] = (uint32_t)S.c_idx;
-                    S.nlong = 1;
-                    S.carry = 0;
-                } else if (S.carry == 2u) {               // still further on: hand it over untouched
-                    S.n_carry = 2; S.n_vb = S.c_vb; S.n_ve = S.c_ve; S.n_idx = S.c_idx;
-                }
+            const unsigned long long bp = __ballot(hand == 2u), bc = __ballot(hand == 1u);
+            if (bp | bc) {
+                const int ol = __builtin_ctzll(bp | bc);
+                n_vb = uni64(__shfl(pvb, ol, 64));
+                n_ve = uni64(__shfl(pve, ol, 64));
+                n_idx = uni64(__shfl(pidx, ol, 64));
+                if (bp) n_carry = 2;
             }
         }
-        KVR_BARRIER();
-        KVR_STAMP(1);
+        wsync();
+        if (loaded) load_halo(abase, d0, len, k + 1, lane, W.tile);   // this tile's halo reads are done
 
-        // ---- R. records: one thread per record ------------------------------------------------
-        const uint32_t nrec = S.nrec;
-        uint32_t my_err = N32, my_kind = 0;
-        uint64_t my_aux = 0;
-        for (uint32_t j = tid; j < nrec; j += NT) {
-            const uint64_t p = (uint64_t)(lo + (int64_t)S.r.rec[j]);
-            const uint64_t slot = S.pool_base + j;
-            const uint32_t op = tv.rd8(p);
-            if (len - p < 5) { my_err = j; my_kind = KVR_E_KEY_LEN; break; }            // engine.rs:96
-            const uint64_t klen = tv.rd32(p + 1);
-            const uint64_t kb = p + 5;
-            if (len - kb < klen) { my_err = j; my_kind = KVR_E_KEY; break; }             // engine.rs:107
-            uint64_t vu = 0;
-            uint32_t el = 0;
-            if (!utf8_check(tv, kb, klen, &vu, &el)) {                                   // engine.rs:114
-                my_err = j; my_kind = KVR_E_UTF8; my_aux = vu | ((uint64_t)el << 32); break;
-            }
-            if (op > 1u) { my_err = j; my_kind = KVR_E_OPCODE; my_aux = op; break; }     // engine.rs:143
-            kvr_tuple t;
-            t.rec_off = p;
-            t.seg_idx = sd.seg;
-            t.key_len = (uint32_t)klen;
-            t.key_tag = ~crc_range(tv, ~0u, kb, klen, S.T);
-            t.op = (uint8_t)op;
-            t.flags = 0;
-            t.reserved = 0;
-            t.crc32 = 0;
-            t.val_len = 0;
-            if (op == 0u) {
-                const uint64_t q = kb + klen;
-                if (len - q < 4) { my_err = j; my_kind = KVR_E_VAL_LEN; break; }         // engine.rs:121
-                const uint64_t vlen = tv.rd32(q);
-                const uint64_t vb = q + 4, ve = vb + vlen;
-                if (len - vb < vlen) { my_err = j; my_kind = KVR_E_VAL; break; }         // engine.rs:130
-                t.val_len = (uint32_t)vlen;
-                if (vlen <= (uint64_t)SMALL) {
-                    t.crc32 = ~crc_range(tv, ~0u, vb, vlen, S.T);
-                } else {
-                    const int64_t vbr = (int64_t)vb - lo, ver = (int64_t)ve - lo;
-                    if (vbr < TILE) {
-                        const uint32_t L = atomicAdd(&S.nlong, 1u);
-                        S.u.lg.lvb[L] = (int32_t)vbr;
-                        S.u.lg.lve[L] = ver > FAR ? FAR : (int32_t)ver;
-                        S.u.lg.lidx[L] = (uint32_t)slot;
-                        S.u.lg.bkey[vbr / SC + 1] = ((uint32_t)(vbr + 1) << 9) | L;
-                        if (ver > TILE) { S.n_vb = vb; S.n_ve = ve; S.n_idx = slot; }   // runs past the tile
-                    } else {            // the value starts in a later tile
-                        S.n_carry = 2; S.n_vb = vb; S.n_ve = ve; S.n_idx = slot;
-                    }
-                }
-            }
-            if (slot < pool_cap) pool[slot] = t;
-        }
-        if (my_err != N32) atomicMin(&S.err_rec, my_err);
-        KVR_BARRIER();
-        KVR_STAMP(2);
-        if (my_err != N32 && my_err == S.err_rec) {
-            S.err_pos = (uint64_t)(lo + (int64_t)S.r.rec[my_err]);
-            S.err_kind = my_kind;
-            S.err_aux = my_aux;
-        }
-
-        // ---- C. CRC of long values -----------------------------------------------------------
-        if (S.nlong != 0 || S.carry == 1u) {
-            LongLds &G = S.u.lg;
-            // which value crosses boundary tid + 1 (the end of unit tid): latest long value
-            // starting before it (prefix max of keys), if it reaches past it
-            uint32_t key = G.bkey[tid + 1];
+        // ---- C. CRC of long values --------------------------------------------------------
+        const uint32_t nlong = uni32(W.nlong);
+        if (nlong != 0u || carry == 1u) {
+            // which value crosses the end of this lane's unit: latest long value starting before
+            // it (prefix max of boundary keys), if it reaches past it
+            uint32_t key = W.bkey[lane + 1];
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
                 const uint32_t o = __shfl_up(key, d, 64);
                 if (lane >= d && o > key) key = o;
             }
-            if (lane == 63) S.wt[wave] = key;
-            KVR_BARRIER();
-            for (int w = 0; w < wave; ++w) key = S.wt[w] > key ? S.wt[w] : key;
-            const int32_t pb = SC * (tid + 1);
+            const int32_t pb = SC * (lane + 1);
             int32_t Vend = VNONE;
             if (key != 0u) {
-                const int32_t L = (int32_t)(key & 511u);
-                if (G.lve[L] > pb) Vend = L;
-            } else if (S.carry == 1u && (int64_t)S.c_ve - lo > (int64_t)pb) {
+                const int32_t L = (int32_t)(key & 127u);
+                if (W.lve[L] > pb) Vend = L;
+            } else if (carry == 1u && (int64_t)c_ve - lo > (int64_t)pb) {
                 Vend = VCARRY;
             }
-            G.vc[tid + 1] = Vend;
-            if (tid == 0) G.vc[0] = S.carry == 1u ? VCARRY : VNONE;
-            KVR_BARRIER();
-            const int32_t Vst = G.vc[tid];
-            const int32_t us = SC * tid;
-            const uint4 *up = reinterpret_cast<const uint4 *>(tile + us);
-            const uint4 q0 = up[0], q1 = up[1], q2 = up[2], q3 = up[3];
-            const uint32_t w[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                                    q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+            int32_t Vst = __shfl_up(Vend, 1, 64);
+            if (lane == 0) Vst = carry == 1u ? VCARRY : VNONE;
+            const int32_t us = SC * lane;
+            const uint4 *up = reinterpret_cast<const uint4 *>(W.tile + us);   // this lane's unit
+            const uint4 cu0 = up[0], cu1 = up[1], cu2 = up[2], cu3 = up[3];
+            const uint32_t w[16] = {cu0.x, cu0.y, cu0.z, cu0.w, cu1.x, cu1.y, cu1.z, cu1.w,
+                                    cu2.x, cu2.y, cu2.z, cu2.w, cu3.x, cu3.y, cu3.z, cu3.w};
             // piece of the value crossing the unit's end: register contribution at that boundary
-            uint32_t v = 0;
-            uint32_t f = 1;   // segment start (the scan does not look further left)
+            uint32_t v = 0, f = 1;
             if (Vend != VNONE) {
                 int32_t a = 0;
                 bool starts = false;
-                if (Vend >= 0 && G.lvb[Vend] >= us) { a = G.lvb[Vend] - us; starts = true; }
+                if (Vend >= 0 && W.lvb[Vend] >= us) { a = W.lvb[Vend] - us; starts = true; }
                 uint32_t c = 0;
 #pragma unroll
                 for (int kk = 0; kk < 16; ++kk) {   // bytes before the value are zeroed (branch-free)
@@ -700,90 +671,78 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
                     c = crc4(c, w[kk] & (uint32_t)(~0ull << sh), S.T);
                 }
                 if (starts) v = c ^ S.IX[SC - a];
-                else if (tid == 0) v = c ^ kmul(S.c_state, S.KT);   // carried state across unit 0
+                else if (lane == 0) v = c ^ kmul(c_state, S.KT);   // the carried register across unit 0
                 else { v = c; f = 0; }
             }
-            // segmented scan over the 256 units (Kogge-Stone through LDS; step j shifts by 2^j
-            // units = the constant x^(8*64*2^j)): state at boundary s+1 = f ? v : state(s)*X(64) ^ v
+            // segmented scan across the wave: state at boundary s+1 = f ? v : state(s) * X(64) ^ v
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < 6; ++j) {
                 const int d = 1 << j;
-                uint64_t *xb = S.r.sc.x[j & 1];
-                xb[tid] = (uint64_t)v | ((uint64_t)f << 32);
-                KVR_BARRIER();
-                if (tid >= d && !f) {
-                    const uint64_t o = xb[tid - d];
-                    v ^= kmul((uint32_t)o, S.KT + 128 * j);
-                    f = (uint32_t)(o >> 32);
-                }
+                const uint32_t ov = __shfl_up(v, d, 64);
+                const uint32_t of = __shfl_up(f, d, 64);
+                if (lane >= d && !f) { v ^= kmul(ov, S.KT + 128 * j); f = of; }
             }
-            S.r.sc.sx[tid] = v;
-            KVR_BARRIER();
-            KVR_STAMP(3);
+            uint32_t sin = __shfl_up(v, 1, 64);
+            if (lane == 0) sin = c_state;
             // the value crossing the unit's start ends in this unit: finish its CRC
             if (Vst != VNONE) {
-                const int64_t ve_rel = Vst == VCARRY ? (int64_t)S.c_ve - lo : (int64_t)G.lve[Vst];
+                const int64_t ve_rel = Vst == VCARRY ? (int64_t)c_ve - lo : (int64_t)W.lve[Vst];
                 if (ve_rel <= (int64_t)us + SC) {
                     const int m = (int)(ve_rel - us);   // 1 .. 64
-                    uint32_t c = tid == 0 ? S.c_state : S.r.sc.sx[tid - 1];
+                    uint32_t c = sin;
 #pragma unroll
                     for (int kk = 0; kk < 16; ++kk) {
                         const uint32_t cn = crc4(c, w[kk], S.T);
                         c = 4 * kk + 4 <= m ? cn : c;
                     }
-                    for (int b = m & ~3; b < m; ++b) c = crc1(c, tile[us + b], S.T);
-                    const uint64_t idx = Vst == VCARRY ? S.c_idx : (uint64_t)G.lidx[Vst];
+                    for (int b = m & ~3; b < m; ++b) c = crc1(c, W.tile[us + b], S.T);
+                    const uint64_t idx = Vst == VCARRY ? c_idx : (uint64_t)W.lidx[Vst];
                     if (idx < pool_cap) pool[idx].crc32 = ~c;
                 }
             }
-            if (tid == NT - 1) {   // a value running past the tile: hand over its register state
-                const int32_t Vo = G.vc[NT];
-                if (Vo != VNONE) {
-                    S.n_carry = 1;
-                    S.n_state = v;
-                    if (Vo == VCARRY) { S.n_vb = S.c_vb; S.n_ve = S.c_ve; S.n_idx = S.c_idx; }
-                }
+            // a value running past the tile: hand over its register state
+            const int32_t Vo = __shfl(Vend, 63, 64);
+            if (Vo != VNONE) {
+                n_carry = 1;
+                c_state = uni32(__shfl(v, 63, 64));
+                if (Vo == VCARRY) { n_vb = c_vb; n_ve = c_ve; n_idx = c_idx; }
             }
         }
-        KVR_STAMP(4);
-        // bookkeeping (thread 0): tile result, next entry, carried value
-        KVR_BARRIER();
-        if (tid == 0) {
-            const uint32_t n = S.nrec;
-            const uint32_t n_ok = S.err_rec < n ? S.err_rec : n;
-            if (in_stripe) {
-                tres[sg.tile0 + k].pool_off = n_ok ? S.pool_base : 0ull;
+
+        // ---- bookkeeping ------------------------------------------------------------------
+        if (in_stripe) {
+            const uint32_t n_ok = err_rec < nrec ? err_rec : nrec;
+            if (lane == 0) {
+                tres[sg.tile0 + k].pool_off = n_ok ? pool_base : 0ull;
                 tres[sg.tile0 + k].count = n_ok;
-                S.total += n_ok;
-                if (walk) S.entry = S.tile_exit;
-                S.prev_n = n;
             }
-            S.carry = S.n_carry;
-            S.c_vb = S.n_vb; S.c_ve = S.n_ve; S.c_idx = S.n_idx; S.c_state = S.n_state;
-            if (S.err_pos != NONE) S.stop = 1;
-            else if (walk && S.tile_exit == ERRP) {   // defensive: a broken chain must have reported
-                S.stop = 1; S.err_pos = S.entry; S.err_kind = KVR_E_VAL;
-            }
-            S.nrec = 0; S.need_spec = 0; S.cand_min = N32; S.err_rec = N32;
-            S.tile_exit = S.entry;
+            total += n_ok;
+            if (walk) entry = tile_exit;
+            prev_n = nrec;
         }
-        KVR_STAMP(5);
+        carry = n_carry;
+        c_vb = n_vb; c_ve = n_ve; c_idx = n_idx;
+        if (err_pos != NONE) stop = 1;
+        else if (walk && tile_exit == ERRP) {   // defensive: a broken chain must have reported
+            stop = 1; err_pos = entry; err_kind = KVR_E_VAL;
+        }
+        wsync();
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain an unused prefetch before exit
     // tiles of the stripe that were never reached (error stop / pass-through) hold no tuples
     const uint32_t kfirst = k < sd.t_end ? k : sd.t_end;
-    for (uint32_t kk = kfirst + tid; kk < sd.t_end; kk += NT) {
+    for (uint32_t kk = kfirst + lane; kk < sd.t_end; kk += 64) {
         tres[sg.tile0 + kk].pool_off = 0;
         tres[sg.tile0 + kk].count = 0;
     }
-    if (tid == 0) {
+    if (lane == 0) {
         StripeRes r;
-        r.entry = S.stripe_entry;
-        r.exit = (S.err_pos != NONE) ? ERRP : (S.stripe_entry == NONE ? NONE : S.entry);
-        r.err_pos = S.err_pos;
-        r.err_aux = S.err_aux;
-        r.err_kind = (S.err_pos != NONE) ? S.err_kind : 0u;
-        r.count = S.total;
+        r.entry = stripe_entry;
+        r.exit = (err_pos != NONE) ? ERRP : (stripe_entry == NONE ? NONE : entry);
+        r.err_pos = err_pos;
+        r.err_aux = err_aux;
+        r.err_kind = (err_pos != NONE) ? err_kind : 0u;
+        r.count = total;
         r.forced = redo_mode ? 1u : 0u;
         r.pad = 0;
         sres[si] = r;
