@@ -98,13 +98,16 @@ static void build_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &kmul
     for (int i = 1; i <= 64; ++i) X[i] = gf_mul(X[i - 1], 0x00800000u);   // * x^8
     initx.assign(68, 0);
     for (int j = 0; j <= 64; ++j) initx[j] = gf_mul(0xFFFFFFFFu, X[j]);
-    // kmul[j][i][n] = (n << 4i) * X(64 * 2^j)
-    kmul.assign(8 * 8 * 16, 0);
+    // nibble tables of "multiply by a constant": kmul[t][i][n] = (n << 4i) * K_t, with
+    //   K_t = X(64 * 2^t) for t = 0 .. 7   (segmented scan across units)
+    //   K_t = X(4 * (t - 8)) for t = 8 .. 24 (finishing a value: the register pushed through 4q bytes)
+    kmul.assign(KMUL_SETS * 8 * 16, 0);
     uint32_t K = X[64];
-    for (int j = 0; j < 8; ++j) {
+    for (int t = 0; t < KMUL_SETS; ++t) {
+        const uint32_t Kt = t < 8 ? K : X[4 * (t - 8)];
         for (int i = 0; i < 8; ++i)
-            for (uint32_t n = 0; n < 16; ++n) kmul[(j * 8 + i) * 16 + n] = gf_mul(n << (4 * i), K);
-        K = gf_mul(K, K);
+            for (uint32_t n = 0; n < 16; ++n) kmul[(t * 8 + i) * 16 + n] = gf_mul(n << (4 * i), Kt);
+        if (t < 8) K = gf_mul(K, K);
     }
 }
 

@@ -27,6 +27,7 @@ constexpr int      TILE  = 4096;           // bytes per tile (one wave: 64 lanes
 constexpr int      SC    = 64;             // unit: framing sub-chunk = CRC unit per lane
 constexpr int      SMALL = 64;             // values <= SMALL: CRC'd whole by their record's thread
 constexpr int      HALO  = 256;            // bytes of the next tile staged behind each tile
+constexpr int      KMUL_SETS = 8 + 17;     // X(64*2^j) j<8, then X(4q) q<=16
 constexpr uint64_t NONE  = ~0ull;          // "no position"
 constexpr uint64_t ERRP  = ~0ull - 1;      // chain ended in a framing error
 constexpr uint32_t POLY  = 0xEDB88320u;
@@ -83,7 +84,7 @@ struct Counters {         // device scratch, reset per call
 
 struct Tables {           // read-only tables in global memory (copied to LDS per workgroup)
     const uint32_t *crc8;   // [16][256] slice-by-16 byte tables (first 4 used by k_replay)
-    const uint32_t *kmul;   // [8][8][16]: (n << 4i) * x^(8 * 64 * 2^j)
+    const uint32_t *kmul;   // [KMUL_SETS][8][16]: (n << 4i) * K_t (kvr_api.hip build_tables)
     const uint32_t *initx;  // [65]: 0xFFFFFFFF * x^(8 j)
 };
 

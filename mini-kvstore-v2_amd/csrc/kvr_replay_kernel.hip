@@ -56,9 +56,22 @@ struct WaveLds {                          // one stripe's scratch
 struct __align__(16) Smem {
     uint32_t T[4 * 256];                  // slice-by-4 byte tables
     uint32_t KT[6 * 8 * 16];              // [j][nibble i][n]: (n << 4i) * x^(8*64*2^j)
+    uint32_t KQ[17 * 8 * 16];             // [q][nibble i][n]: (n << 4i) * x^(8*4q)
     uint32_t IX[68];                      // 0xFFFFFFFF * x^(8j): initial register pushed through j bytes
     WaveLds w[WPB];
 };
+
+#ifdef KVR_PROF
+__device__ unsigned long long g_prof[16];
+#define KVR_STAMP(i)                                                        \
+    do {                                                                    \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();         \
+        prof_acc[i] += t_ - t_last;                                         \
+        t_last = t_;                                                        \
+    } while (0)
+#else
+#define KVR_STAMP(i) do { } while (0)
+#endif
 
 __device__ __forceinline__ void wsync() {   // LDS writes of this wave visible to its other lanes
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -419,6 +432,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (int i = tid; i < 4 * 256; i += NT) S.T[i] = tb.crc8[i];
     for (int i = tid; i < 6 * 8 * 16; i += NT) S.KT[i] = tb.kmul[i];
+    for (int i = tid; i < 17 * 8 * 16; i += NT) S.KQ[i] = tb.kmul[8 * 8 * 16 + i];
     if (tid < 65) S.IX[tid] = tb.initx[tid];
     __syncthreads();   // the only workgroup barrier: from here on every wave is on its own
 
@@ -463,8 +477,13 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
     load_halo(abase, d0, len, sd.t_begin, lane, W.tile);
     bool loaded = true;
     uint32_t k = sd.t_begin;
+#ifdef KVR_PROF
+    unsigned long long t_last = __builtin_amdgcn_s_memtime();
+    unsigned long long prof_acc[6] = {0, 0, 0, 0, 0, 0};
+#endif
     for (;; ++k) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        KVR_STAMP(5);
         const bool in_stripe = k < sd.t_end;
         if (stop || (!in_stripe && !carry) || k >= sg.n_tiles) break;
         if (!loaded) {
@@ -490,6 +509,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
         const uint64_t cs = cs_i < (int64_t)vlo ? vlo : (uint64_t)cs_i;
         const uint64_t ce = (uint64_t)(cs_i + SC) > vhi ? vhi : (uint64_t)(cs_i + SC);
 
+        KVR_STAMP(0);
         // ---- F. framing ------------------------------------------------------------------------
         if (in_stripe && search) {   // the stripe's entry: the first plausible record start
             const uint64_t cand = cs < ce ? find_cand(tv, cs, ce) : NONE;
@@ -575,6 +595,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
         }
         wsync();
 
+        KVR_STAMP(1);
         // ---- R. records ----------------------------------------------------------------------
         RecRes ro;
         ro.err = N32; ro.kind = 0; ro.aux = 0; ro.hand = 0; ro.vb = 0; ro.ve = 0; ro.slot = 0;
@@ -632,6 +653,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
         wsync();
         if (loaded) load_halo(abase, d0, len, k + 1, lane, W.tile);   // this tile's halo reads are done
 
+        KVR_STAMP(2);
         // ---- C. CRC of long values --------------------------------------------------------
         const uint32_t nlong = uni32(W.nlong);
         if (nlong != 0u || carry == 1u) {
@@ -658,18 +680,32 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
             const uint4 cu0 = up[0], cu1 = up[1], cu2 = up[2], cu3 = up[3];
             const uint32_t w[16] = {cu0.x, cu0.y, cu0.z, cu0.w, cu1.x, cu1.y, cu1.z, cu1.w,
                                     cu2.x, cu2.y, cu2.z, cu2.w, cu3.x, cu3.y, cu3.z, cu3.w};
-            // piece of the value crossing the unit's end: register contribution at that boundary
+            // One pass over the unit's bytes gives both register pieces this lane owns:
+            //  - raw CRC of [0, m) (bytes of the value crossing the unit start, if it ends here at m),
+            //    snapshotted on the way, and
+            //  - raw CRC of [a, 64) (the value crossing the unit end; a > 0 if it starts here), by
+            //    restarting the register at a's word with the bytes before a zeroed.
+            int32_t m = 0;                               // 1 .. 64 if the start-crossing value ends here
+            if (Vst != VNONE) {
+                const int64_t ve_rel = Vst == VCARRY ? (int64_t)c_ve - lo : (int64_t)W.lve[Vst];
+                if (ve_rel <= (int64_t)us + SC) m = (int32_t)(ve_rel - us);
+            }
+            int32_t a = 0;
+            bool starts = false;
+            if (Vend >= 0 && W.lvb[Vend] >= us) { a = W.lvb[Vend] - us; starts = true; }
+            const int qm = m >> 2, qa = starts ? (a >> 2) : -1;
+            uint32_t c = 0, snap = 0, wm = 0;
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) {
+                snap = kk == qm ? c : snap;
+                wm = kk == qm ? w[kk] : wm;
+                c = kk == qa ? 0u : c;
+                const int sh = kk == qa ? 8 * (a & 3) : 0;   // bytes of a's word before a are zeroed
+                c = crc4(c, w[kk] & (~0u << sh), S.T);
+            }
+            snap = qm == 16 ? c : snap;
             uint32_t v = 0, f = 1;
             if (Vend != VNONE) {
-                int32_t a = 0;
-                bool starts = false;
-                if (Vend >= 0 && W.lvb[Vend] >= us) { a = W.lvb[Vend] - us; starts = true; }
-                uint32_t c = 0;
-#pragma unroll
-                for (int kk = 0; kk < 16; ++kk) {   // bytes before the value are zeroed (branch-free)
-                    const int sh = min(max(8 * (a - 4 * kk), 0), 32);
-                    c = crc4(c, w[kk] & (uint32_t)(~0ull << sh), S.T);
-                }
                 if (starts) v = c ^ S.IX[SC - a];
                 else if (lane == 0) v = c ^ kmul(c_state, S.KT);   // the carried register across unit 0
                 else { v = c; f = 0; }
@@ -684,21 +720,17 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
             }
             uint32_t sin = __shfl_up(v, 1, 64);
             if (lane == 0) sin = c_state;
-            // the value crossing the unit's start ends in this unit: finish its CRC
-            if (Vst != VNONE) {
-                const int64_t ve_rel = Vst == VCARRY ? (int64_t)c_ve - lo : (int64_t)W.lve[Vst];
-                if (ve_rel <= (int64_t)us + SC) {
-                    const int m = (int)(ve_rel - us);   // 1 .. 64
-                    uint32_t c = sin;
-#pragma unroll
-                    for (int kk = 0; kk < 16; ++kk) {
-                        const uint32_t cn = crc4(c, w[kk], S.T);
-                        c = 4 * kk + 4 <= m ? cn : c;
-                    }
-                    for (int b = m & ~3; b < m; ++b) c = crc1(c, W.tile[us + b], S.T);
-                    const uint64_t idx = Vst == VCARRY ? c_idx : (uint64_t)W.lidx[Vst];
-                    if (idx < pool_cap) pool[idx].crc32 = ~c;
+            // the value crossing the unit's start ends in this unit at m: its register is
+            // sin * x^(8m) ^ raw[0, m)  (the x^(8m) push: a constant table for 4q bytes + r zero bytes)
+            if (m != 0) {
+                const int r = m & 3;
+                uint32_t rp = snap, cf = kmul(sin, S.KQ + 128 * qm);
+                for (int b = 0; b < r; ++b) {
+                    rp = crc1(rp, (wm >> (8 * b)) & 255u, S.T);
+                    cf = crc1(cf, 0u, S.T);
                 }
+                const uint64_t idx = Vst == VCARRY ? c_idx : (uint64_t)W.lidx[Vst];
+                if (idx < pool_cap) pool[idx].crc32 = ~(cf ^ rp);
             }
             // a value running past the tile: hand over its register state
             const int32_t Vo = __shfl(Vend, 63, 64);
@@ -709,6 +741,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
             }
         }
 
+        KVR_STAMP(3);
         // ---- bookkeeping ------------------------------------------------------------------
         if (in_stripe) {
             const uint32_t n_ok = err_rec < nrec ? err_rec : nrec;
@@ -727,8 +760,13 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
             stop = 1; err_pos = entry; err_kind = KVR_E_VAL;
         }
         wsync();
+        KVR_STAMP(4);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain an unused prefetch before exit
+#ifdef KVR_PROF
+    if (lane == 0)
+        for (int i = 0; i < 6; ++i) atomicAdd(&g_prof[i], prof_acc[i]);
+#endif
     // tiles of the stripe that were never reached (error stop / pass-through) hold no tuples
     const uint32_t kfirst = k < sd.t_end ? k : sd.t_end;
     for (uint32_t kk = kfirst + lane; kk < sd.t_end; kk += 64) {

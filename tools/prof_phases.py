@@ -56,7 +56,7 @@ for it in range(3):
     st = K.Stats()
     lib.kvr_last_stats(ctx, C.byref(st))
     lib.kvr_prof_read(prof, 0)
-names = ["load+prefetch", "framing", "records", "cover+crc+scan", "finalize", "bookkeep", "-", "-"]
+names = ["setup(store+pref)", "framing", "records", "crc+scan+fin", "bookkeep", "wait(vmcnt)", "-", "-"]
 tiles = st.n_tiles
 tot_c = sum(prof[i] for i in range(8))
 print(f"{cfg}: rc={rc} n={n.value}/{nrec} bytes={tot} tiles={tiles} stripes={st.n_stripes} ms_replay={st.ms_replay:.3f}"
