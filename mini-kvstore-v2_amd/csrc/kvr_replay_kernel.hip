@@ -333,24 +333,155 @@ __device__ __noinline__ Stitched stitch(WaveLds &W, const TileView tv, uint64_t 
 // ---------------------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------------------
+
+// ---------------------------------------------------------------------------------------
+// 48 bytes of the tile + halo starting at any byte offset off (off + 52 <= TILE + HALO):
+// 13 aligned dword reads issued together, realigned in registers.
+// ---------------------------------------------------------------------------------------
+struct Win { uint32_t q[12]; };
+
+__device__ __forceinline__ Win lds_window(const uint8_t *lds, int off) {
+    const uint32_t *tw = reinterpret_cast<const uint32_t *>(lds) + (off >> 2);
+    const uint32_t sh = (uint32_t)off & 3u;
+    uint32_t r[13];
+#pragma unroll
+    for (int i = 0; i < 13; ++i) r[i] = tw[i];
+    Win w;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) w.q[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
+    return w;
+}
+
+// the u32 at window byte offset t (t <= 44), t per lane: a select chain over the 12 words
+__device__ __forceinline__ uint32_t win_u32(const Win &w, uint32_t t) {
+    const uint32_t j = t >> 2, s = t & 3u;
+    uint32_t lo = w.q[0], hi = w.q[1];
+#pragma unroll
+    for (int i = 1; i < 11; ++i) {
+        lo = j == (uint32_t)i ? w.q[i] : lo;
+        hi = j == (uint32_t)i ? w.q[i + 1] : hi;
+    }
+    return __builtin_amdgcn_alignbyte(hi, lo, s);
+}
+
+// Fast path for the common record shape: header, a key of at most 36 ASCII bytes and the value
+// length inside the tile + halo, no error.  Fills the tuple (crc32 of a value <= SMALL still to
+// do) and returns true; anything else returns false and takes the general path.
+__device__ __forceinline__ bool rec_fast(const TileView &tv, const uint32_t *T, uint64_t p, uint32_t kmax,
+                                         kvr_tuple &t, uint64_t &vb, uint64_t &vlen) {
+    const int64_t off = (int64_t)p - tv.lo;
+    const uint64_t len = tv.len;
+    if (off < 0 || off + 52 > TILE + HALO || len - p < 9) return false;
+    const Win w = lds_window(tv.lds, (int)off);
+    const uint32_t op = w.q[0] & 255u;
+    const uint32_t klen = __builtin_amdgcn_alignbyte(w.q[1], w.q[0], 1);
+    if (op > 1u || klen > kmax || len - p - 5 < klen) return false;
+    // key bytes start at window byte 5: key word i = bytes 5+4i .. 8+4i
+    uint32_t bad = 0, c = ~0u, tail = 0;
+    const uint32_t nw = (kmax + 3u) >> 2;                                 // wave-uniform trip count
+    for (uint32_t i = 0; i < nw; ++i) {
+        uint32_t kw = w.q[1];
+#pragma unroll
+        for (int s = 1; s < 10; ++s) kw = i == (uint32_t)(s - 1) ? __builtin_amdgcn_alignbyte(w.q[s + 1], w.q[s], 1) : kw;
+        const uint32_t n = klen > 4u * i ? klen - 4u * i : 0u;           // key bytes in this word
+        const uint32_t m = n >= 4u ? ~0u : ((1u << (8 * n)) - 1u);
+        bad |= kw & m & 0x80808080u;                                     // non-ASCII: the full check
+        const uint32_t cn = crc4(c, kw, T);
+        c = n >= 4u ? cn : c;
+        tail = (n > 0u && n < 4u) ? kw : tail;
+    }
+    if (bad) return false;
+    for (uint32_t b = 0; b < (klen & 3u); ++b) c = crc1(c, (tail >> (8 * b)) & 255u, T);
+    t.rec_off = p;
+    t.key_len = klen;
+    t.key_tag = ~c;
+    t.op = (uint8_t)op;
+    t.flags = 0;
+    t.reserved = 0;
+    t.crc32 = 0;
+    t.val_len = 0;
+    vb = p + 5 + klen;
+    vlen = 0;
+    if (op == 0u) {
+        if (len - vb < 4) return false;
+        vlen = win_u32(w, 5 + klen);
+        vb += 4;
+        if (len - vb < vlen) return false;
+        t.val_len = (uint32_t)vlen;
+    }
+    return true;
+}
+
+// next record start after the record at p (exact, = next_rec): one window read when the header
+// and a key of at most 36 bytes sit in the tile + halo; next_rec otherwise
+__device__ __forceinline__ uint64_t hop_next(const TileView &tv, uint64_t p) {
+    const int64_t off = (int64_t)p - tv.lo;
+    const uint64_t len = tv.len;
+    if (off >= 0 && off + 52 <= TILE + HALO && len - p >= 9) {
+        const Win w = lds_window(tv.lds, (int)off);
+        const uint32_t op = w.q[0] & 255u;
+        const uint32_t klen = __builtin_amdgcn_alignbyte(w.q[1], w.q[0], 1);
+        if (op <= 1u && klen <= 36u) {
+            const uint64_t e = p + 5 + klen;
+            if (e > len) return ERRP;
+            if (op == 1u) return e;
+            if (len - e < 4) return ERRP;
+            const uint64_t e2 = e + 4 + (uint64_t)win_u32(w, 5 + klen);
+            return e2 > len ? ERRP : e2;
+        }
+    }
+    return next_rec(tv, p);
+}
+
 struct RecRes {          // one record's outcome
     uint32_t err, kind;  // record index of an error (N32: none) and its KVR_E_* kind
     uint64_t aux;
     uint32_t hand;       // 1: its long value crosses the tile end, 2: its value starts in a later tile
     uint64_t vb, ve, slot;
+    uint32_t klen;       // key length (fast-path sizing for the next tile)
 };
 
 // parse + emit the record at p (engine.rs order of checks); long values register with the tile
 __device__ __forceinline__ RecRes do_record(const TileView &tv, WaveLds &W, const uint32_t *T, uint64_t p, uint32_t j,
-                                         uint64_t slot, uint32_t seg, kvr_tuple *pool, uint64_t pool_cap) {
+                                         uint64_t slot, uint32_t seg, kvr_tuple *pool, uint64_t pool_cap,
+                                         uint32_t kmax) {
     RecRes ro;
-    ro.err = N32; ro.kind = 0; ro.aux = 0; ro.hand = 0; ro.vb = 0; ro.ve = 0; ro.slot = slot;
+    ro.err = N32; ro.kind = 0; ro.aux = 0; ro.hand = 0; ro.vb = 0; ro.ve = 0; ro.slot = slot; ro.klen = 0;
+    {
+        kvr_tuple t;
+        uint64_t vb, vlen;
+        if (rec_fast(tv, T, p, kmax, t, vb, vlen)) {
+            t.seg_idx = seg;
+            ro.klen = t.key_len;
+            if (t.op == 0u) {
+                if (vlen <= (uint64_t)SMALL) {
+                    t.crc32 = ~crc_range(tv, ~0u, vb, vlen, T);
+                } else {
+                    const uint64_t ve = vb + vlen;
+                    const int64_t vbr = (int64_t)vb - tv.lo, ver = (int64_t)ve - tv.lo;
+                    if (vbr < TILE) {
+                        const uint32_t L = atomicAdd(&W.nlong, 1u);
+                        W.lvb[L] = (int32_t)vbr;
+                        W.lve[L] = ver > FAR ? FAR : (int32_t)ver;
+                        W.lidx[L] = (uint32_t)slot;
+                        W.bkey[vbr / SC + 1] = ((uint32_t)(vbr + 1) << 7) | L;
+                        if (ver > TILE) { ro.hand = 1; ro.vb = vb; ro.ve = ve; }
+                    } else {
+                        ro.hand = 2; ro.vb = vb; ro.ve = ve;
+                    }
+                }
+            }
+            if (slot < pool_cap) pool[slot] = t;
+            return ro;
+        }
+    }
     const uint64_t len = tv.len;
     const int64_t lo = tv.lo;
     const uint32_t op = tv.rd8(p);
     if (len - p < 5) { ro.err = j; ro.kind = KVR_E_KEY_LEN; return ro; }                 // engine.rs:96
     const uint64_t klen = tv.rd32(p + 1);
     const uint64_t kb = p + 5;
+    ro.klen = klen > 36u ? 36u : (uint32_t)klen;
     if (len - kb < klen) { ro.err = j; ro.kind = KVR_E_KEY; return ro; }                  // engine.rs:107
     uint64_t vu = 0;
     uint32_t el = 0;
@@ -467,7 +598,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
         if (lane == 0) atomicOr(&ctr->overflow, 4u);
     }
     uint64_t err_pos = NONE, err_aux = 0;
-    uint32_t err_kind = 0, total = 0, prev_n = 0;
+    uint32_t err_kind = 0, total = 0, prev_n = 0, kmax = 36;   // kmax: key bytes the record fast path takes
     uint64_t chunk_base = 0, chunk_left = 0;
     uint32_t carry = 0, c_state = 0;      // 1: a long value crosses the tile start (c_state valid);
     uint64_t c_vb = 0, c_ve = 0, c_idx = 0;   // 2: pending (its value starts in a later tile)
@@ -479,7 +610,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
     uint32_t k = sd.t_begin;
 #ifdef KVR_PROF
     unsigned long long t_last = __builtin_amdgcn_s_memtime();
-    unsigned long long prof_acc[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long prof_acc[16] = {};
 #endif
     for (;; ++k) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -533,7 +664,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
                 while (p < vhi && n_hop < HOP_MAX) {
                     if (lane == (int)n_hop) myrec = (uint32_t)((int64_t)p - lo);
                     ++n_hop;
-                    p = uni64(next_rec(tv, p));
+                    p = uni64(hop_next(tv, p));
                     if (p == ERRP) break;
                 }
             }
@@ -598,7 +729,8 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
         KVR_STAMP(1);
         // ---- R. records ----------------------------------------------------------------------
         RecRes ro;
-        ro.err = N32; ro.kind = 0; ro.aux = 0; ro.hand = 0; ro.vb = 0; ro.ve = 0; ro.slot = 0;
+        ro.err = N32; ro.kind = 0; ro.aux = 0; ro.hand = 0; ro.vb = 0; ro.ve = 0; ro.slot = 0; ro.klen = 0;
+        uint32_t my_kmax = 0;
         uint32_t hand = 0;
         uint64_t pvb = 0, pve = 0, pidx = 0;
         {   // this lane's records: its hop record (record index = lane), then its unit's speculated ones
@@ -609,19 +741,24 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
                 const bool h = i < has_hop;
                 const uint64_t p = h ? (uint64_t)(lo + (int64_t)myrec) : ps;
                 const uint32_t j = h ? (uint32_t)lane : n_hop + st.base + (i - has_hop);
-                ro = do_record(tv, W, S.T, p, j, pool_base + j, sd.seg, pool, pool_cap);
+                ro = do_record(tv, W, S.T, p, j, pool_base + j, sd.seg, pool, pool_cap, kmax);
                 if (ro.hand) { hand = ro.hand; pvb = ro.vb; pve = ro.ve; pidx = ro.slot; }
+                my_kmax = ro.klen > my_kmax ? ro.klen : my_kmax;
                 if (ro.err != N32) break;
                 if (!h && i + 1 < nmine) ps = next_spec(tv, ps);
             }
         }
-        // first error of the tile (lowest record index)
+        KVR_STAMP(6);
+        // first error of the tile (lowest record index); longest key (fast-path bound of the next tile)
         uint32_t err_rec = ro.err;
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) {
             const uint32_t o = __shfl_xor(err_rec, d, 64);
             err_rec = o < err_rec ? o : err_rec;
+            const uint32_t ok = __shfl_xor(my_kmax, d, 64);
+            my_kmax = ok > my_kmax ? ok : my_kmax;
         }
+        if (nrec) kmax = uni32(my_kmax) < 4u ? 4u : uni32(my_kmax);
         err_rec = uni32(err_rec);
         if (err_rec != N32) {
             const int el = __builtin_ctzll(__ballot(ro.err == err_rec));
@@ -639,6 +776,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
             }
             err_pos = uni64(__shfl(ep, el, 64));
         }
+        KVR_STAMP(7);
         // a long value crossing the tile end / starting later (one at most): its lane hands it over
         {
             const unsigned long long bp = __ballot(hand == 2u), bc = __ballot(hand == 1u);
@@ -673,6 +811,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
             } else if (carry == 1u && (int64_t)c_ve - lo > (int64_t)pb) {
                 Vend = VCARRY;
             }
+            KVR_STAMP(8);
             int32_t Vst = __shfl_up(Vend, 1, 64);
             if (lane == 0) Vst = carry == 1u ? VCARRY : VNONE;
             const int32_t us = SC * lane;
@@ -704,6 +843,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
                 c = crc4(c, w[kk] & (~0u << sh), S.T);
             }
             snap = qm == 16 ? c : snap;
+            KVR_STAMP(9);
             uint32_t v = 0, f = 1;
             if (Vend != VNONE) {
                 if (starts) v = c ^ S.IX[SC - a];
@@ -718,6 +858,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
                 const uint32_t of = __shfl_up(f, d, 64);
                 if (lane >= d && !f) { v ^= kmul(ov, S.KT + 128 * j); f = of; }
             }
+            KVR_STAMP(10);
             uint32_t sin = __shfl_up(v, 1, 64);
             if (lane == 0) sin = c_state;
             // the value crossing the unit's start ends in this unit at m: its register is
@@ -765,7 +906,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain an unused prefetch before exit
 #ifdef KVR_PROF
     if (lane == 0)
-        for (int i = 0; i < 6; ++i) atomicAdd(&g_prof[i], prof_acc[i]);
+        for (int i = 0; i < 16; ++i) atomicAdd(&g_prof[i], prof_acc[i]);
 #endif
     // tiles of the stripe that were never reached (error stop / pass-through) hold no tuples
     const uint32_t kfirst = k < sd.t_end ? k : sd.t_end;

@@ -56,9 +56,10 @@ for it in range(3):
     st = K.Stats()
     lib.kvr_last_stats(ctx, C.byref(st))
     lib.kvr_prof_read(prof, 0)
-names = ["setup(store+pref)", "framing", "records", "crc+scan+fin", "bookkeep", "wait(vmcnt)", "-", "-"]
+names = ["setup(store+pref)", "framing", "err+hand+halo", "crc-finalize", "bookkeep", "wait(vmcnt)", "records", "err-reduce",
+         "cover-scan", "unit-crc", "scan", "-", "-", "-", "-", "-"]
 tiles = st.n_tiles
-tot_c = sum(prof[i] for i in range(8))
+tot_c = sum(prof[i] for i in range(16))
 print(f"{cfg}: rc={rc} n={n.value}/{nrec} bytes={tot} tiles={tiles} stripes={st.n_stripes} ms_replay={st.ms_replay:.3f}"
       f" GB/s={tot / st.ms_replay / 1e6:.1f}")
 for i, nm in enumerate(names):
