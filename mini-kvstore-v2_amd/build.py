@@ -74,7 +74,27 @@ def build_prof():
     return out
 
 
+def build_ablate(masks=(0, 1, 2, 3, 7)):
+    """Diagnostic variants with parts of k_replay switched off (tools/ablate.py); not shipped."""
+    out = os.path.join(LIB, "ablate")
+    os.makedirs(out, exist_ok=True)
+    deps = _deps(*[f for f in os.listdir(CSRC) if f.endswith((".hip", ".h"))])
+    procs = []
+    for m in masks:
+        so = os.path.join(out, f"libkvreplay_a{m}.so")
+        if _newer(so, deps):
+            procs.append(subprocess.Popen([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+                                           f"-DKVR_ABLATE={m}", "-Wno-unused-result", "-o", so,
+                                           os.path.join(CSRC, "kvr_api.hip")]))
+    for p in procs:
+        if p.wait() != 0:
+            raise RuntimeError("ablation build failed")
+    return out
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
     if "--prof" in sys.argv:
         print("built", build_prof())
+    if "--ablate" in sys.argv:
+        print("built", build_ablate())

@@ -61,6 +61,10 @@ struct __align__(16) Smem {
     WaveLds w[WPB];
 };
 
+#ifndef KVR_ABLATE
+#define KVR_ABLATE 0   // diagnostic builds only: 1 skip records, 2 skip value CRC, 4 skip hops
+#endif
+
 #ifdef KVR_PROF
 __device__ unsigned long long g_prof[16];
 #define KVR_STAMP(i)                                                        \
@@ -85,6 +89,11 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {   // wave-uniform value 
     return ((uint64_t)hi << 32) | lo;
 }
 __device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+// lane l's value, l wave-uniform (v_readlane: no LDS traffic, unlike a shuffle)
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+    return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
+}
 
 // ---------------------------------------------------------------------------------------
 // CRC primitives on the LDS tables
@@ -301,8 +310,8 @@ __device__ __noinline__ Stitched stitch(WaveLds &W, const TileView tv, uint64_t 
         }
         const unsigned long long rm = __ballot(reach);
         const int smax = 63 - __builtin_clzll(rm);
-        const int Tl = __shfl(T, smax, 64);
-        const uint32_t xs = __shfl(x, smax, 64);
+        const int Tl = (int)rl32((uint32_t)T, smax);
+        const uint32_t xs = rl32(x, smax);
         if (Tl == T_MM) {
             if (lane == 0) repair(W, tv, (uint64_t)(lo + (int64_t)xs), vhi);
             wsync();
@@ -317,7 +326,7 @@ __device__ __noinline__ Stitched stitch(WaveLds &W, const TileView tv, uint64_t 
             if (lane >= d) inc += o;
         }
         R.base = inc - R.cnt;
-        R.total = uni32(__shfl(inc, 63, 64));
+        R.total = rl32(inc, 63);
         uint64_t xe;
         if (Tl == T_ERR) xe = ERRP;
         else if (xs != X_BEYOND) xe = (uint64_t)(lo + (int64_t)xs);
@@ -660,7 +669,8 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
         st.ent = N16; st.cnt = 0; st.base = 0; st.total = 0;
         if (walk) {
             uint64_t p = entry;
-            if (prev_n <= DENSE) {   // exact hops, all lanes together (LDS broadcast reads)
+            if (KVR_ABLATE & 4) { n_hop = 0; p = vhi; }
+            else if (prev_n <= DENSE) {   // exact hops, all lanes together (LDS broadcast reads)
                 while (p < vhi && n_hop < HOP_MAX) {
                     if (lane == (int)n_hop) myrec = (uint32_t)((int64_t)p - lo);
                     ++n_hop;
@@ -735,7 +745,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
         uint64_t pvb = 0, pve = 0, pidx = 0;
         {   // this lane's records: its hop record (record index = lane), then its unit's speculated ones
             const uint32_t has_hop = myrec != N32 ? 1u : 0u;
-            const uint32_t nmine = has_hop + (st.ent != N16 ? st.cnt : 0u);
+            const uint32_t nmine = (KVR_ABLATE & 1) ? 0u : has_hop + (st.ent != N16 ? st.cnt : 0u);
             uint64_t ps = (uint64_t)(lo + (int64_t)st.ent);
             for (uint32_t i = 0; i < nmine; ++i) {
                 const bool h = i < has_hop;
@@ -750,20 +760,30 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
         }
         KVR_STAMP(6);
         // first error of the tile (lowest record index); longest key (fast-path bound of the next tile)
-        uint32_t err_rec = ro.err;
+        uint32_t err_rec = N32;
+        if (__ballot(ro.err != N32)) {
+            err_rec = ro.err;
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            const uint32_t o = __shfl_xor(err_rec, d, 64);
-            err_rec = o < err_rec ? o : err_rec;
-            const uint32_t ok = __shfl_xor(my_kmax, d, 64);
-            my_kmax = ok > my_kmax ? ok : my_kmax;
+            for (int d = 32; d >= 1; d >>= 1) {
+                const uint32_t o = __shfl_xor(err_rec, d, 64);
+                err_rec = o < err_rec ? o : err_rec;
+            }
+            err_rec = uni32(err_rec);
         }
-        if (nrec) kmax = uni32(my_kmax) < 4u ? 4u : uni32(my_kmax);
-        err_rec = uni32(err_rec);
+        if (nrec && ((k - sd.t_begin) & 15u) == 0u) {   // refresh the fast path's key bound now and then
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+                const uint32_t ok = __shfl_xor(my_kmax, d, 64);
+                my_kmax = ok > my_kmax ? ok : my_kmax;
+            }
+            kmax = uni32(my_kmax) < 4u ? 4u : uni32(my_kmax);
+        } else if (__ballot(my_kmax > kmax)) {
+            kmax = 36u;                                  // a longer key appeared: widen at once
+        }
         if (err_rec != N32) {
             const int el = __builtin_ctzll(__ballot(ro.err == err_rec));
-            err_kind = uni32(__shfl(ro.kind, el, 64));
-            err_aux = uni64(__shfl(ro.aux, el, 64));
+            err_kind = rl32(ro.kind, el);
+            err_aux = rl64(ro.aux, el);
             // the failing record's start: hop records live in myrec, speculated ones are re-found
             uint64_t ep = NONE;
             if (ro.err == err_rec) {
@@ -774,7 +794,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
                     ep = p;
                 }
             }
-            err_pos = uni64(__shfl(ep, el, 64));
+            err_pos = rl64(ep, el);
         }
         KVR_STAMP(7);
         // a long value crossing the tile end / starting later (one at most): its lane hands it over
@@ -782,9 +802,9 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
             const unsigned long long bp = __ballot(hand == 2u), bc = __ballot(hand == 1u);
             if (bp | bc) {
                 const int ol = __builtin_ctzll(bp | bc);
-                n_vb = uni64(__shfl(pvb, ol, 64));
-                n_ve = uni64(__shfl(pve, ol, 64));
-                n_idx = uni64(__shfl(pidx, ol, 64));
+                n_vb = rl64(pvb, ol);
+                n_ve = rl64(pve, ol);
+                n_idx = rl64(pidx, ol);
                 if (bp) n_carry = 2;
             }
         }
@@ -794,7 +814,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
         KVR_STAMP(2);
         // ---- C. CRC of long values --------------------------------------------------------
         const uint32_t nlong = uni32(W.nlong);
-        if (nlong != 0u || carry == 1u) {
+        if (!(KVR_ABLATE & 2) && (nlong != 0u || carry == 1u)) {
             // which value crosses the end of this lane's unit: latest long value starting before
             // it (prefix max of boundary keys), if it reaches past it
             uint32_t key = W.bkey[lane + 1];
@@ -874,10 +894,10 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
                 if (idx < pool_cap) pool[idx].crc32 = ~(cf ^ rp);
             }
             // a value running past the tile: hand over its register state
-            const int32_t Vo = __shfl(Vend, 63, 64);
+            const int32_t Vo = (int32_t)rl32((uint32_t)Vend, 63);
             if (Vo != VNONE) {
                 n_carry = 1;
-                c_state = uni32(__shfl(v, 63, 64));
+                c_state = rl32(v, 63);
                 if (Vo == VCARRY) { n_vb = c_vb; n_ve = c_ve; n_idx = c_idx; }
             }
         }
