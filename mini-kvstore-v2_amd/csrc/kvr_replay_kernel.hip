@@ -535,16 +535,31 @@ __device__ __forceinline__ RecRes do_record(const TileView &tv, WaveLds &W, cons
     return ro;
 }
 
-// this lane's 64-B unit of tile k (16-B loads; bytes outside the segment read as 0)
+// this lane's 64-B unit of tile k: four 16-B raw buffer loads through a per-tile resource whose
+// range is the 16-B words touching the segment, so words outside it read as 0 in hardware (no
+// per-word compares, no select of pointers)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void load_unit(const uint8_t *abase, int64_t d0, uint64_t len, uint32_t k, int lane,
                                           uint4 &r0, uint4 &r1, uint4 &r2, uint4 &r3) {
-    const int64_t pos = (int64_t)k * TILE - d0 + lane * SC;
-    const uint4 *u = reinterpret_cast<const uint4 *>(abase + (int64_t)k * TILE + lane * SC);
-    const uint4 z = make_uint4(0, 0, 0, 0);
-    r0 = (pos + 16 > 0 && pos < (int64_t)len) ? u[0] : z;
-    r1 = (pos + 32 > 0 && pos + 16 < (int64_t)len) ? u[1] : z;
-    r2 = (pos + 48 > 0 && pos + 32 < (int64_t)len) ? u[2] : z;
-    r3 = (pos + 64 > 0 && pos + 48 < (int64_t)len) ? u[3] : z;
+    const int64_t t0 = (int64_t)k * TILE;
+    const int64_t first = d0 & ~(int64_t)15, endw = (d0 + (int64_t)len + 15) & ~(int64_t)15;
+    const int64_t skip = first > t0 ? first - t0 : 0;
+    int64_t nrec = endw - t0 - skip;
+    nrec = nrec < 0 ? 0 : (nrec > TILE ? TILE : nrec);
+    const uint64_t b = (uint64_t)(abase + t0 + skip);
+    const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)b), bhi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    const int nr = __builtin_amdgcn_readfirstlane((int)nrec);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(((uint64_t)bhi << 32) | blo), (short)0, nr, 0x00020000);
+    const int vo = lane * SC - (int)skip;   // negative -> out of range -> 0
+    const u32x4 a0 = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 0);
+    const u32x4 a1 = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16, 0, 0);
+    const u32x4 a2 = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 32, 0, 0);
+    const u32x4 a3 = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 48, 0, 0);
+    r0 = make_uint4(a0.x, a0.y, a0.z, a0.w);
+    r1 = make_uint4(a1.x, a1.y, a1.z, a1.w);
+    r2 = make_uint4(a2.x, a2.y, a2.z, a2.w);
+    r3 = make_uint4(a3.x, a3.y, a3.z, a3.w);
 }
 
 // halo of tile k: the next HALO bytes after it, LDS-DMA into tile + TILE (lanes 0 .. HALO/16-1)
