@@ -1,0 +1,48 @@
+#!/bin/bash
+# One GPU measurement batch, run through gpurun from the repo root:
+#   parity tests, the bench line, the rocprofv3 kernel-trace summary of the same bench command,
+#   the per-phase cycle breakdown, ablation timings and PMC counters.  Every GPU step has its
+#   own time limit and the steps are chained, so the first failure ends the batch.
+#   usage: tools/gpu_measure.sh <tag> [tests bench bench3 bench5 prof phases ablate pmc ...]
+set -o pipefail
+TAG=${1:-run}; shift
+STEPS=${*:-tests bench prof}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$R" || exit 1
+export TMPDIR=/tmp
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        > "$OUT/tests.log" 2>&1 || { echo "tests failed"; tail -40 "$OUT/tests.log"; exit 1; }
+      tail -3 "$OUT/tests.log" ;;
+    bench)
+      timeout -k 10 300 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; tail -20 "$OUT/bench.err"; exit 1; }
+      cat "$OUT/bench.json" ;;
+    bench3)
+      timeout -k 10 300 python -u bench.py --config cfg3 --no-cpu > "$OUT/bench_cfg3.json" 2> "$OUT/bench_cfg3.err" || { echo "bench cfg3 failed"; tail -20 "$OUT/bench_cfg3.err"; exit 1; }
+      cat "$OUT/bench_cfg3.json" ;;
+    bench5)
+      timeout -k 10 300 python -u bench.py --config cfg5 --segments 16 --no-cpu > "$OUT/bench_cfg5.json" 2> "$OUT/bench_cfg5.err" || { echo "bench cfg5 failed"; tail -20 "$OUT/bench_cfg5.err"; exit 1; }
+      cat "$OUT/bench_cfg5.json" ;;
+    prof)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+        python "$R/bench.py" --no-cpu > "$OUT/prof.log" 2>&1) || { echo "rocprof failed"; tail -20 "$OUT/prof.log"; exit 1; }
+      find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \; ;;
+    phases)
+      timeout -k 10 240 python -u tools/prof_phases.py cfg2 > "$OUT/phases_cfg2.txt" 2>&1 || { echo "phases failed"; tail -20 "$OUT/phases_cfg2.txt"; exit 1; }
+      cat "$OUT/phases_cfg2.txt" ;;
+    ablate)
+      for m in 0 1 2 3 7; do
+        timeout -k 10 120 python -u tools/ablate.py cfg2 0 $m >> "$OUT/ablate_cfg2.txt" 2>&1 || { echo "ablate failed"; tail -20 "$OUT/ablate_cfg2.txt"; exit 1; }
+      done
+      cat "$OUT/ablate_cfg2.txt" ;;
+    pmc)
+      timeout -k 10 900 bash tools/pmc.sh "$OUT/pmc" --no-cpu --steps 2 --warmup 1 > "$OUT/pmc.txt" 2>&1 || { echo "pmc failed"; tail -20 "$OUT/pmc.txt"; exit 1; }
+      cat "$OUT/pmc.txt" ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "batch $TAG done"
