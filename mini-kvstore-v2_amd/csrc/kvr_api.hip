@@ -47,7 +47,7 @@ constexpr uint32_t REDO_GRID = 1024;
 struct kvr_ctx {
     int device = 0;
     int n_cu = 256;
-    int wg_per_cu = 5;
+    int wg_per_cu = 1;
     hipStream_t own = nullptr, stream = nullptr;
     hipEvent_t ev[6] = {};
     DevBuf<uint8_t> arena;
@@ -101,13 +101,16 @@ static void build_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &kmul
     // nibble tables of "multiply by a constant": kmul[t][i][n] = (n << 4i) * K_t, with
     //   K_t = X(64 * 2^t) for t = 0 .. 7   (segmented scan across units)
     //   K_t = X(4 * (t - 8)) for t = 8 .. 24 (finishing a value: the register pushed through 4q bytes)
+    //   K_t = X(64 * (t - 24)) for t = 25 .. 56 (cross-row steps of the segmented scan)
     kmul.assign(KMUL_SETS * 8 * 16, 0);
-    uint32_t K = X[64];
+    uint32_t K = X[64], R = X[64];
     for (int t = 0; t < KMUL_SETS; ++t) {
-        const uint32_t Kt = t < 8 ? K : X[4 * (t - 8)];
+        uint32_t Kt;
+        if (t < KSET_Q) { Kt = K; K = gf_mul(K, K); }
+        else if (t < KSET_R) Kt = X[4 * (t - KSET_Q)];
+        else { Kt = R; R = gf_mul(R, X[64]); }
         for (int i = 0; i < 8; ++i)
             for (uint32_t n = 0; n < 16; ++n) kmul[(t * 8 + i) * 16 + n] = gf_mul(n << (4 * i), Kt);
-        if (t < 8) K = gf_mul(K, K);
     }
 }
 
@@ -180,7 +183,7 @@ int kvr_ctx_create(int device, kvr_ctx **out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->n_cu = prop.multiProcessorCount;
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_replay, NT, 0) == hipSuccess && occ > 0) c->wg_per_cu = occ;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_replay, RT, 0) == hipSuccess && occ > 0) c->wg_per_cu = occ;
     if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return KVR_EHIP; }
     c->stream = c->own;
     for (auto &e : c->ev) if (hipEventCreate(&e) != hipSuccess) { delete c; return KVR_EHIP; }
@@ -290,8 +293,8 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         total_tiles += g.n_tiles;
     }
     if (total_tiles >= 0xFFFFFFFFull) return KVR_EINVAL;
-    // one stripe per wave, two rounds of resident waves (k_replay: 4 stripes per workgroup)
-    const uint64_t target = (uint64_t)c->n_cu * (uint64_t)c->wg_per_cu * 4 * 2;
+    // one stripe per wave, two rounds of resident waves (k_replay: WPB stripes per workgroup)
+    const uint64_t target = (uint64_t)c->n_cu * (uint64_t)c->wg_per_cu * WPB * 2;
     const uint64_t tps = c->tps_override ? c->tps_override : std::max<uint64_t>(1, (total_tiles + target - 1) / target);
     c->h_stripes.clear();
     for (size_t i = 0; i < n; ++i) {
@@ -353,7 +356,7 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         HIPCHK(hipMemsetAsync(c->ctr.p, 0, sizeof(Counters), st));
         HIPCHK(hipMemsetAsync(c->link.p, 0, sizeof(LinkResult), st));
         HIPCHK(hipEventRecord(c->ev[0], st));
-        hipLaunchKernelGGL(k_replay, dim3((n_stripes + 3) / 4), dim3(NT), 0, st, c->segs.p, c->stripes.p, n_stripes,
+        hipLaunchKernelGGL(k_replay, dim3((n_stripes + WPB - 1) / WPB), dim3(RT), 0, st, c->segs.p, c->stripes.p, n_stripes,
                            c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, c->redo.p, c->link.p, 0, pool_chunk);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[1], st));
@@ -403,7 +406,7 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
             continue;
         }
         while (c->h_link->status == 3 && guard++ < n_stripes + 4) {
-            hipLaunchKernelGGL(k_replay, dim3((std::max(1u, std::min(c->h_link->n_redo, (uint32_t)c->redo.n)) + 3) / 4), dim3(NT),
+            hipLaunchKernelGGL(k_replay, dim3((std::max(1u, std::min(c->h_link->n_redo, (uint32_t)c->redo.n)) + WPB - 1) / WPB), dim3(RT),
                                0, st, c->segs.p, c->stripes.p, n_stripes, c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p,
                                tb, c->redo.p, c->link.p, 1, pool_chunk);
             hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes,

@@ -2,16 +2,15 @@
  * kvr_device.h — device-side building blocks of the replay engine (gfx950 / CDNA4).
  *
  * Geometry:
- *   - A workgroup (NT = 256 threads = 4 waves) owns one STRIPE: a run of consecutive TILEs of
- *     one segment, walked in order, so the record chain and the CRC register of a value that
- *     spans tiles are handed from tile to tile; only the stripe's first entry is speculated
- *     (verified by k_link).
- *   - A TILE (16 KiB, plus a HALO of the next 256 B for headers and short fields that straddle
- *     the tile end) is streamed HBM -> LDS by LDS-DMA, one tile ahead of the one processed.
- *   - Each thread owns one 64-B UNIT of the tile for framing speculation and value CRCs.
+ *   - A WAVE owns one STRIPE: a run of consecutive TILEs of one segment, walked in order, so the
+ *     record chain and the CRC register of a value that spans tiles are handed from tile to
+ *     tile; only the stripe's first entry is speculated (verified by k_link).
+ *   - A TILE is 4 KiB; lane l holds the 64-B UNIT [64 l, 64 l + 64) in registers (prefetched one
+ *     tile ahead) and copies it to the wave's LDS tile, behind which a HALO of the next 256 B
+ *     arrives by LDS-DMA for headers and short fields that straddle the tile end.
  *   - CRC-32 (reflected 0xEDB88320, crc32fast semantics, src/volume/storage.rs:27) runs on
- *     slice-by-4 byte tables in LDS; register states move across units with the constants
- *     x^(8*64*2^j) (nibble tables), never with a variable GF(2) multiply.
+ *     lane-replicated slice-by-2 byte tables in LDS; register states move across units with
+ *     the constants x^(8*64*d) (nibble tables), never with a variable GF(2) multiply.
  */
 #ifndef KVR_DEVICE_H
 #define KVR_DEVICE_H
@@ -27,7 +26,9 @@ constexpr int      TILE  = 4096;           // bytes per tile (one wave: 64 lanes
 constexpr int      SC    = 64;             // unit: framing sub-chunk = CRC unit per lane
 constexpr int      SMALL = 64;             // values <= SMALL: CRC'd whole by their record's thread
 constexpr int      HALO  = 256;            // bytes of the next tile staged behind each tile
-constexpr int      KMUL_SETS = 8 + 17;     // X(64*2^j) j<8, then X(4q) q<=16
+constexpr int      KSET_Q = 8;             // kmul sets: X(64*2^j) j<8, then X(4q) q<=16,
+constexpr int      KSET_R = 8 + 17;        //   then X(64(k+1)) k<32 (cross-row scan multipliers)
+constexpr int      KMUL_SETS = 8 + 17 + 32;
 constexpr uint64_t NONE  = ~0ull;          // "no position"
 constexpr uint64_t ERRP  = ~0ull - 1;      // chain ended in a framing error
 constexpr uint32_t POLY  = 0xEDB88320u;

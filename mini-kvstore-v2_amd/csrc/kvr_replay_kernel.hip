@@ -1,33 +1,44 @@
 /*
- * kvr_replay_kernel.hip — k_replay, the hot path (gfx950).
+ * kvr_replay_kernel.hip — k_replay (V6), the hot path (gfx950).
  *
  * One WAVE replays one stripe (consecutive 4-KiB tiles of one segment) exactly as
  * src/store/engine.rs:79-154 walks a segment file, and emits one 32-B kvr_tuple per record with
- * the CRC-32 of its key and value (crc32fast::hash semantics, src/volume/storage.rs:27).
- * A workgroup holds 4 independent stripes; after the CRC tables are staged in LDS there is no
- * workgroup barrier at all, so a wave waiting on a header hop or on HBM never holds up another.
+ * the CRC-32 of its key and of its value (crc32fast::hash semantics, src/volume/storage.rs:27).
+ * A workgroup holds 12 independent stripes that share the CRC tables; after the tables are
+ * staged in LDS there is no workgroup barrier, so a wave waiting on HBM never holds up another.
  *
- * Per tile, lane l owns the 64-B unit [64 l, 64 l + 64):
- *   load  the unit arrives in registers (prefetched one tile ahead with 16-B global loads) and is
- *         written to the wave's LDS tile for random access; the next 256 B (halo) come by LDS-DMA
- *   F     framing: the record starts, exactly, from the tile entry (the previous tile's exit).
- *         Sparse tiles: all lanes hop header to header together (LDS broadcast reads), lane j
- *         keeps record j.  Dense tiles (or past 64 records): every lane speculates a chain through
- *         its unit and the wave stitches the sub-chains by pointer jumping.  The stripe's first
- *         tile takes its first plausible record start; k_link verifies it.
- *   R     records: engine.rs checks in engine.rs order, key CRC, CRC of values <= 64 B, tuple.
- *         Longer values register the first unit boundary they cross.
- *   C     long values: each lane CRCs, from its registers, its unit's piece of the value crossing
- *         the unit's end; a 6-step segmented scan across the wave (multipliers are the constants
- *         x^(8*64*2^j)) gives the CRC register at every unit boundary; the lane holding a value's
- *         last byte finishes that CRC.  A value running past the tile hands its register to the
- *         next tile of the stripe (walked in order), so no variable GF(2) multiply is needed.
+ * Per tile, lane l owns the 64-B unit [64 l, 64 l + 64), prefetched one tile ahead into registers
+ * with 16-B buffer loads and stored to the wave's LDS tile:
+ *   F  framing, exact from the tile entry (the previous tile's exit).  The wave hops header to
+ *      header: one hop reads a 256-B window of the tile into the 64 lanes (one dword each) and
+ *      decodes op / key_len / val_len with scalar readlanes, so consecutive short records cost
+ *      no further LDS round trip.  Dense tiles (more than 48 records in the previous tile, or
+ *      more than 64 here) switch to per-unit speculation stitched by pointer jumping.  The
+ *      stripe's first tile takes its first plausible record start; k_link verifies it.
+ *   R  records: lane j emits hop record j with the engine.rs checks the hop did not already make
+ *      (UTF-8 of the key), the key CRC from registers, and the CRC of a value of at most 64 B.
+ *      Longer values stay in registers as (start, end, tuple slot).  Records found by
+ *      speculation and the record that broke the chain take the general path (every check in
+ *      engine.rs order).
+ *   C  long values: every lane learns, by a wave-uniform loop over the tile's long values, which
+ *      value crosses the end of its unit and which one ends inside it; it CRCs its unit's piece
+ *      in one pass (a snapshot at the inner end, a restart at an inner start);
+ *      a segmented scan across the wave (DPP row shifts, then row broadcasts; the multipliers
+ *      x^(8*64*d) come from nibble tables) gives the CRC register at every unit boundary; the
+ *      lane holding a value's last byte finishes that CRC.  A value running past the tile hands
+ *      its register to the next tile of the stripe, so no variable GF(2) multiply is needed.
+ *
+ * CRC tables: the slice-by-2 byte tables (T0: one byte, T1: a byte followed by a zero byte) are
+ * replicated once per LDS bank: the entry for byte b of table t in lane l's copy sits at byte
+ * address b*256 + t*128 + 4 (l & 31), in bank (l & 31), so no lookup of a wave ever conflicts,
+ * and its address is a single v_perm_b32 of the register byte and the lane's constant.
  */
 #include "kvr_device.h"
 
 namespace kvr {
 
-constexpr int WPB = NT / 64;              // stripes (waves) per workgroup
+constexpr int RT = 768;                   // threads per workgroup
+constexpr int WPB = RT / 64;              // stripes (waves) per workgroup
 constexpr int UNITS = TILE / SC;          // 64 units per tile = one per lane
 static_assert(UNITS == 64, "one 64-B unit per lane");
 constexpr uint16_t N16 = 0xFFFFu;
@@ -38,27 +49,26 @@ constexpr int T_END = 64, T_ERR = 65, T_MM = 66;
 constexpr uint32_t POOL_CHUNK = 2048;
 constexpr uint32_t HOP_MAX = 64;          // records found by hopping (one per lane)
 constexpr uint32_t DENSE = 48;            // previous tile's records above which we speculate at once
-constexpr int MAXLONG = UNITS + 2;        // long values touching a tile (one per first-crossed boundary + pending)
-constexpr int32_t VNONE = -1, VCARRY = -2;
 constexpr int32_t FAR = 1 << 30;          // "ends beyond the tile" (tile-relative clamp)
+constexpr int KEYW = 6;                   // key words the record fast path holds (keys <= 24 B)
+constexpr int WIN = (TILE + HALO) / 4;    // dwords of tile + halo
 
 struct WaveLds {                          // one stripe's scratch
     uint8_t  tile[TILE + HALO];
     uint32_t sc_exit[UNITS];
     uint16_t sc_cand[UNITS], sc_cnt[UNITS], sc_last[UNITS];
     uint8_t  reach[UNITS];
-    int32_t  lvb[MAXLONG], lve[MAXLONG];
-    uint32_t lidx[MAXLONG];
-    uint32_t bkey[UNITS + 1];
-    uint32_t nlong, pad[3];
 };
 
+// The tables come first: every table address is a lane-dependent VGPR plus a constant below
+// 64 KiB, which the ds_read instruction carries as its immediate offset.
 struct __align__(16) Smem {
-    uint32_t T[4 * 256];                  // slice-by-4 byte tables
-    uint32_t KT[6 * 8 * 16];              // [j][nibble i][n]: (n << 4i) * x^(8*64*2^j)
-    uint32_t KQ[17 * 8 * 16];             // [q][nibble i][n]: (n << 4i) * x^(8*4q)
+    uint32_t KR[8 * 16 * 32];             // [i][n][k]: (n << 4i) * x^(8*64*(k+1)), k < 32
+    uint32_t KT[4 * 8 * 16];              // [j][i][n]: (n << 4i) * x^(8*64*2^j), j < 4
+    uint32_t KQ[17 * 8 * 16];             // [q][i][n]: (n << 4i) * x^(8*4q), q <= 16
     uint32_t IX[68];                      // 0xFFFFFFFF * x^(8j): initial register pushed through j bytes
-    WaveLds w[WPB];
+    uint32_t C2[2 * 256 * 32];            // lane-replicated slice-by-2 byte tables (64 KiB)
+    WaveLds  w[WPB];
 };
 
 #ifndef KVR_ABLATE
@@ -94,48 +104,77 @@ __device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return __builtin_a
 __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
     return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
 }
-
-// ---------------------------------------------------------------------------------------
-// CRC primitives on the LDS tables
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t crc4(uint32_t c, uint32_t w, const uint32_t *T) {
-    c ^= w;
-    return T[768 + (c & 255u)] ^ T[512 + ((c >> 8) & 255u)] ^ T[256 + ((c >> 16) & 255u)] ^ T[c >> 24];
+// two consecutive dwords of a wave-spread window as one little-endian 64-bit value, from word i
+__device__ __forceinline__ uint64_t win64(uint32_t win, int i) {
+    return ((uint64_t)rl32(win, i + 1) << 32) | rl32(win, i);
 }
 
-__device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const uint32_t *T) {
-    return (c >> 8) ^ T[(c ^ b) & 255u];
+// DPP move (no LDS): CTRL = row_shr:d (0x110 + d), row_bcast:15 (0x142), row_bcast:31 (0x143),
+// wave_shr:1 (0x138); lanes without a source read 0
+template <int CTRL, int ROWS = 0xF, bool BC = true>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xF, BC);
 }
 
-// register state v times the constant x^(8*64*2^j): K = KT + 128 j
+// ---------------------------------------------------------------------------------------
+// CRC primitives
+// ---------------------------------------------------------------------------------------
+struct Crc {
+    const uint8_t *t;   // the lane-replicated slice-by-2 tables (Smem::C2)
+    uint32_t L;         // byte 0: 4 (lane & 31) (T0 copy), byte 1: 128 + 4 (lane & 31) (T1 copy)
+};
+// v_perm_b32 builds the LDS address: byte 1 = a byte of x, byte 0 = this lane's table copy
+constexpr uint32_t SEL_T1_B0 = 0x0C0C0401u, SEL_T0_B1 = 0x0C0C0500u, SEL_T0_B0 = 0x0C0C0400u;
+__device__ __forceinline__ uint32_t tget(const Crc &k, uint32_t x, uint32_t sel) {
+    return *reinterpret_cast<const uint32_t *>(k.t + __builtin_amdgcn_perm(x, k.L, sel));
+}
+// the register after the two bytes sitting in x's low half (x = register ^ data)
+__device__ __forceinline__ uint32_t crc2(const Crc &k, uint32_t x) {
+    return (x >> 16) ^ tget(k, x, SEL_T1_B0) ^ tget(k, x, SEL_T0_B1);
+}
+__device__ __forceinline__ uint32_t crc4(uint32_t c, uint32_t w, const Crc &k) { return crc2(k, crc2(k, c ^ w)); }
+__device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
+    const uint32_t x = c ^ b;
+    return (x >> 8) ^ tget(k, x, SEL_T0_B0);
+}
+
+// register state v times a constant K (nibble tables; every lane reads table i at once, so the
+// 16 entries sit in 16 banks and equal indices broadcast: conflict free)
 __device__ __forceinline__ uint32_t kmul(uint32_t v, const uint32_t *K) {
     uint32_t r = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) r ^= K[i * 16 + ((v >> (4 * i)) & 15u)];
     return r;
 }
+// v times x^(8*64*(k+1)), k per lane (column k of KR: bank k mod 32, conflict free)
+__device__ __forceinline__ uint32_t kmulr(uint32_t v, const uint32_t *KR, uint32_t k) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r ^= KR[(i * 16 + ((v >> (4 * i)) & 15u)) * 32 + k];
+    return r;
+}
 
 // CRC register update over segment bytes [p, p+n): LDS when resident (tile + halo), HBM otherwise
-__device__ inline uint32_t crc_range(const TileView &tv, uint32_t c, uint64_t p, uint64_t n, const uint32_t *T) {
+__device__ inline uint32_t crc_range(const TileView &tv, uint32_t c, uint64_t p, uint64_t n, const Crc &K) {
     if (tv.in_lds(p, n)) {
         int off = (int)((int64_t)p - tv.lo);
         const int end = off + (int)n;
         #pragma unroll 1
-        while (off < end && (off & 3)) { c = crc1(c, tv.lds[off], T); ++off; }
+        while (off < end && (off & 3)) { c = crc1(c, tv.lds[off], K); ++off; }
         const uint32_t *w = reinterpret_cast<const uint32_t *>(tv.lds);
         #pragma unroll 1
-        while (off + 4 <= end) { c = crc4(c, w[off >> 2], T); off += 4; }
+        while (off + 4 <= end) { c = crc4(c, w[off >> 2], K); off += 4; }
         #pragma unroll 1
-        while (off < end) { c = crc1(c, tv.lds[off], T); ++off; }
+        while (off < end) { c = crc1(c, tv.lds[off], K); ++off; }
         return c;
     }
     #pragma unroll 1
-    for (uint64_t i = 0; i < n; ++i) c = crc1(c, tv.rd8(p + i), T);
+    for (uint64_t i = 0; i < n; ++i) c = crc1(c, tv.rd8(p + i), K);
     return c;
 }
 
 // ---------------------------------------------------------------------------------------
-// speculative framing inside the tile (LDS only)
+// speculative framing inside the tile (LDS only) — the dense path
 // ---------------------------------------------------------------------------------------
 // End of the record at p, ERRP (broken framing) or BEYOND (a field lies past the tile: the
 // record ends beyond it).  p must be inside the tile and < len.
@@ -340,157 +379,26 @@ __device__ __noinline__ Stitched stitch(WaveLds &W, const TileView tv, uint64_t 
 }
 
 // ---------------------------------------------------------------------------------------
-// the kernel
+// records
 // ---------------------------------------------------------------------------------------
-
-// ---------------------------------------------------------------------------------------
-// 48 bytes of the tile + halo starting at any byte offset off (off + 52 <= TILE + HALO):
-// 13 aligned dword reads issued together, realigned in registers.
-// ---------------------------------------------------------------------------------------
-struct Win { uint32_t q[12]; };
-
-__device__ __forceinline__ Win lds_window(const uint8_t *lds, int off) {
-    const uint32_t *tw = reinterpret_cast<const uint32_t *>(lds) + (off >> 2);
-    const uint32_t sh = (uint32_t)off & 3u;
-    uint32_t r[13];
-#pragma unroll
-    for (int i = 0; i < 13; ++i) r[i] = tw[i];
-    Win w;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) w.q[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
-    return w;
-}
-
-// the u32 at window byte offset t (t <= 44), t per lane: a select chain over the 12 words
-__device__ __forceinline__ uint32_t win_u32(const Win &w, uint32_t t) {
-    const uint32_t j = t >> 2, s = t & 3u;
-    uint32_t lo = w.q[0], hi = w.q[1];
-#pragma unroll
-    for (int i = 1; i < 11; ++i) {
-        lo = j == (uint32_t)i ? w.q[i] : lo;
-        hi = j == (uint32_t)i ? w.q[i + 1] : hi;
-    }
-    return __builtin_amdgcn_alignbyte(hi, lo, s);
-}
-
-// Fast path for the common record shape: header, a key of at most 36 ASCII bytes and the value
-// length inside the tile + halo, no error.  Fills the tuple (crc32 of a value <= SMALL still to
-// do) and returns true; anything else returns false and takes the general path.
-__device__ __forceinline__ bool rec_fast(const TileView &tv, const uint32_t *T, uint64_t p, uint32_t kmax,
-                                         kvr_tuple &t, uint64_t &vb, uint64_t &vlen) {
-    const int64_t off = (int64_t)p - tv.lo;
-    const uint64_t len = tv.len;
-    if (off < 0 || off + 52 > TILE + HALO || len - p < 9) return false;
-    const Win w = lds_window(tv.lds, (int)off);
-    const uint32_t op = w.q[0] & 255u;
-    const uint32_t klen = __builtin_amdgcn_alignbyte(w.q[1], w.q[0], 1);
-    if (op > 1u || klen > kmax || len - p - 5 < klen) return false;
-    // key bytes start at window byte 5: key word i = bytes 5+4i .. 8+4i
-    uint32_t bad = 0, c = ~0u, tail = 0;
-    const uint32_t nw = (kmax + 3u) >> 2;                                 // wave-uniform trip count
-    for (uint32_t i = 0; i < nw; ++i) {
-        uint32_t kw = w.q[1];
-#pragma unroll
-        for (int s = 1; s < 10; ++s) kw = i == (uint32_t)(s - 1) ? __builtin_amdgcn_alignbyte(w.q[s + 1], w.q[s], 1) : kw;
-        const uint32_t n = klen > 4u * i ? klen - 4u * i : 0u;           // key bytes in this word
-        const uint32_t m = n >= 4u ? ~0u : ((1u << (8 * n)) - 1u);
-        bad |= kw & m & 0x80808080u;                                     // non-ASCII: the full check
-        const uint32_t cn = crc4(c, kw, T);
-        c = n >= 4u ? cn : c;
-        tail = (n > 0u && n < 4u) ? kw : tail;
-    }
-    if (bad) return false;
-    for (uint32_t b = 0; b < (klen & 3u); ++b) c = crc1(c, (tail >> (8 * b)) & 255u, T);
-    t.rec_off = p;
-    t.key_len = klen;
-    t.key_tag = ~c;
-    t.op = (uint8_t)op;
-    t.flags = 0;
-    t.reserved = 0;
-    t.crc32 = 0;
-    t.val_len = 0;
-    vb = p + 5 + klen;
-    vlen = 0;
-    if (op == 0u) {
-        if (len - vb < 4) return false;
-        vlen = win_u32(w, 5 + klen);
-        vb += 4;
-        if (len - vb < vlen) return false;
-        t.val_len = (uint32_t)vlen;
-    }
-    return true;
-}
-
-// next record start after the record at p (exact, = next_rec): one window read when the header
-// and a key of at most 36 bytes sit in the tile + halo; next_rec otherwise
-__device__ __forceinline__ uint64_t hop_next(const TileView &tv, uint64_t p) {
-    const int64_t off = (int64_t)p - tv.lo;
-    const uint64_t len = tv.len;
-    if (off >= 0 && off + 52 <= TILE + HALO && len - p >= 9) {
-        const Win w = lds_window(tv.lds, (int)off);
-        const uint32_t op = w.q[0] & 255u;
-        const uint32_t klen = __builtin_amdgcn_alignbyte(w.q[1], w.q[0], 1);
-        if (op <= 1u && klen <= 36u) {
-            const uint64_t e = p + 5 + klen;
-            if (e > len) return ERRP;
-            if (op == 1u) return e;
-            if (len - e < 4) return ERRP;
-            const uint64_t e2 = e + 4 + (uint64_t)win_u32(w, 5 + klen);
-            return e2 > len ? ERRP : e2;
-        }
-    }
-    return next_rec(tv, p);
-}
-
 struct RecRes {          // one record's outcome
     uint32_t err, kind;  // record index of an error (N32: none) and its KVR_E_* kind
     uint64_t aux;
-    uint32_t hand;       // 1: its long value crosses the tile end, 2: its value starts in a later tile
-    uint64_t vb, ve, slot;
-    uint32_t klen;       // key length (fast-path sizing for the next tile)
+    uint32_t lng;        // its value is longer than SMALL: 1 starts inside the tile, 2 starts later
+    int32_t vb;          // value start, tile-relative (lng 1)
+    uint64_t vbabs, ve;  // value start / end, segment offsets
 };
 
-// parse + emit the record at p (engine.rs order of checks); long values register with the tile
-__device__ __forceinline__ RecRes do_record(const TileView &tv, WaveLds &W, const uint32_t *T, uint64_t p, uint32_t j,
-                                         uint64_t slot, uint32_t seg, kvr_tuple *pool, uint64_t pool_cap,
-                                         uint32_t kmax) {
+// parse + emit the record at p with every engine.rs check, in engine.rs order
+__device__ inline RecRes do_record(const TileView &tv, const Crc &K, uint64_t p, uint32_t j, uint64_t slot,
+                                   uint32_t seg, kvr_tuple *pool, uint64_t pool_cap) {
     RecRes ro;
-    ro.err = N32; ro.kind = 0; ro.aux = 0; ro.hand = 0; ro.vb = 0; ro.ve = 0; ro.slot = slot; ro.klen = 0;
-    {
-        kvr_tuple t;
-        uint64_t vb, vlen;
-        if (rec_fast(tv, T, p, kmax, t, vb, vlen)) {
-            t.seg_idx = seg;
-            ro.klen = t.key_len;
-            if (t.op == 0u) {
-                if (vlen <= (uint64_t)SMALL) {
-                    t.crc32 = ~crc_range(tv, ~0u, vb, vlen, T);
-                } else {
-                    const uint64_t ve = vb + vlen;
-                    const int64_t vbr = (int64_t)vb - tv.lo, ver = (int64_t)ve - tv.lo;
-                    if (vbr < TILE) {
-                        const uint32_t L = atomicAdd(&W.nlong, 1u);
-                        W.lvb[L] = (int32_t)vbr;
-                        W.lve[L] = ver > FAR ? FAR : (int32_t)ver;
-                        W.lidx[L] = (uint32_t)slot;
-                        W.bkey[vbr / SC + 1] = ((uint32_t)(vbr + 1) << 7) | L;
-                        if (ver > TILE) { ro.hand = 1; ro.vb = vb; ro.ve = ve; }
-                    } else {
-                        ro.hand = 2; ro.vb = vb; ro.ve = ve;
-                    }
-                }
-            }
-            if (slot < pool_cap) pool[slot] = t;
-            return ro;
-        }
-    }
+    ro.err = N32; ro.kind = 0; ro.aux = 0; ro.lng = 0; ro.vb = 0; ro.vbabs = 0; ro.ve = 0;
     const uint64_t len = tv.len;
-    const int64_t lo = tv.lo;
     const uint32_t op = tv.rd8(p);
     if (len - p < 5) { ro.err = j; ro.kind = KVR_E_KEY_LEN; return ro; }                 // engine.rs:96
     const uint64_t klen = tv.rd32(p + 1);
     const uint64_t kb = p + 5;
-    ro.klen = klen > 36u ? 36u : (uint32_t)klen;
     if (len - kb < klen) { ro.err = j; ro.kind = KVR_E_KEY; return ro; }                  // engine.rs:107
     uint64_t vu = 0;
     uint32_t el = 0;
@@ -502,7 +410,7 @@ __device__ __forceinline__ RecRes do_record(const TileView &tv, WaveLds &W, cons
     t.rec_off = p;
     t.seg_idx = seg;
     t.key_len = (uint32_t)klen;
-    t.key_tag = ~crc_range(tv, ~0u, kb, klen, T);
+    t.key_tag = ~crc_range(tv, ~0u, kb, klen, K);
     t.op = (uint8_t)op;
     t.flags = 0;
     t.reserved = 0;
@@ -516,19 +424,13 @@ __device__ __forceinline__ RecRes do_record(const TileView &tv, WaveLds &W, cons
         if (len - vb < vlen) { ro.err = j; ro.kind = KVR_E_VAL; return ro; }              // engine.rs:130
         t.val_len = (uint32_t)vlen;
         if (vlen <= (uint64_t)SMALL) {
-            t.crc32 = ~crc_range(tv, ~0u, vb, vlen, T);
+            t.crc32 = ~crc_range(tv, ~0u, vb, vlen, K);
         } else {
-            const int64_t vbr = (int64_t)vb - lo, ver = (int64_t)ve - lo;
-            if (vbr < TILE) {
-                const uint32_t L = atomicAdd(&W.nlong, 1u);
-                W.lvb[L] = (int32_t)vbr;
-                W.lve[L] = ver > FAR ? FAR : (int32_t)ver;
-                W.lidx[L] = (uint32_t)slot;
-                W.bkey[vbr / SC + 1] = ((uint32_t)(vbr + 1) << 7) | L;
-                if (ver > TILE) { ro.hand = 1; ro.vb = vb; ro.ve = ve; }   // runs past the tile
-            } else {                       // the value starts in a later tile
-                ro.hand = 2; ro.vb = vb; ro.ve = ve;
-            }
+            const int64_t vbr = (int64_t)vb - tv.lo;
+            ro.lng = vbr < TILE ? 1u : 2u;
+            ro.vb = (int32_t)(vbr < TILE ? vbr : 0);
+            ro.vbabs = vb;
+            ro.ve = ve;
         }
     }
     if (slot < pool_cap) pool[slot] = t;
@@ -576,7 +478,10 @@ __device__ __forceinline__ void load_halo(const uint8_t *abase, int64_t d0, uint
     }
 }
 
-__global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ segs,
+// ---------------------------------------------------------------------------------------
+// the kernel
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                                                const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
                                                StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
                                                kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
@@ -585,13 +490,18 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
                                                uint32_t pool_chunk) {
     __shared__ Smem S;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    for (int i = tid; i < 4 * 256; i += NT) S.T[i] = tb.crc8[i];
-    for (int i = tid; i < 6 * 8 * 16; i += NT) S.KT[i] = tb.kmul[i];
-    for (int i = tid; i < 17 * 8 * 16; i += NT) S.KQ[i] = tb.kmul[8 * 8 * 16 + i];
+    for (int i = tid; i < 2 * 256 * 32; i += RT) S.C2[i] = tb.crc8[((i >> 5) & 1) * 256 + (i >> 6)];
+    for (int i = tid; i < 8 * 16 * 32; i += RT)
+        S.KR[i] = tb.kmul[((KSET_R + (i & 31)) * 8 + (i >> 9)) * 16 + ((i >> 5) & 15)];
+    for (int i = tid; i < 4 * 8 * 16; i += RT) S.KT[i] = tb.kmul[i];
+    for (int i = tid; i < 17 * 8 * 16; i += RT) S.KQ[i] = tb.kmul[KSET_Q * 8 * 16 + i];
     if (tid < 65) S.IX[tid] = tb.initx[tid];
     __syncthreads();   // the only workgroup barrier: from here on every wave is on its own
 
-    const uint32_t gw = blockIdx.x * WPB + wv;
+    const Crc K{reinterpret_cast<const uint8_t *>(S.C2),
+                ((uint32_t)(lane & 31) * 4u) | (((uint32_t)(lane & 31) * 4u + 128u) << 8)};
+    // the stripe index is wave-uniform: say so, so that the whole stripe state lives in SGPRs
+    const uint32_t gw = blockIdx.x * WPB + (uint32_t)__builtin_amdgcn_readfirstlane(wv);
     uint32_t si;
     uint64_t forced = NONE;
     if (redo_mode) {
@@ -603,6 +513,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
         si = gw;
     }
     WaveLds &W = S.w[wv];
+    const uint32_t *tw = reinterpret_cast<const uint32_t *>(W.tile);
     const StripeDesc sd = stripes[si];
     const SegDesc sg = segs[sd.seg];
     const uint64_t len = sg.len;
@@ -622,13 +533,13 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
         if (lane == 0) atomicOr(&ctr->overflow, 4u);
     }
     uint64_t err_pos = NONE, err_aux = 0;
-    uint32_t err_kind = 0, total = 0, prev_n = 0, kmax = 36;   // kmax: key bytes the record fast path takes
+    uint32_t err_kind = 0, total = 0, prev_n = 0;
     uint64_t chunk_base = 0, chunk_left = 0;
-    uint32_t carry = 0, c_state = 0;      // 1: a long value crosses the tile start (c_state valid);
-    uint64_t c_vb = 0, c_ve = 0, c_idx = 0;   // 2: pending (its value starts in a later tile)
+    uint32_t carry = 0, c_state = 0, c_idx = 0;   // 1: a long value crosses the tile start (c_state: its register);
+    uint64_t c_vb = 0, c_ve = 0;                  // 2: pending (its value starts in a later tile)
 
-    uint4 nx0, nx1, nx2, nx3;   // this lane's unit of the next tile (prefetch)
-    load_unit(abase, d0, len, sd.t_begin, lane, nx0, nx1, nx2, nx3);
+    uint4 n0, n1, n2, n3;   // this lane's unit of the next tile (prefetch)
+    load_unit(abase, d0, len, sd.t_begin, lane, n0, n1, n2, n3);
     load_halo(abase, d0, len, sd.t_begin, lane, W.tile);
     bool loaded = true;
     uint32_t k = sd.t_begin;
@@ -642,23 +553,23 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
         const bool in_stripe = k < sd.t_end;
         if (stop || (!in_stripe && !carry) || k >= sg.n_tiles) break;
         if (!loaded) {
-            load_unit(abase, d0, len, k, lane, nx0, nx1, nx2, nx3);
+            load_unit(abase, d0, len, k, lane, n0, n1, n2, n3);
             load_halo(abase, d0, len, k, lane, W.tile);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         {
             uint4 *tp = reinterpret_cast<uint4 *>(W.tile + lane * SC);
-            tp[0] = nx0; tp[1] = nx1; tp[2] = nx2; tp[3] = nx3;
+            tp[0] = n0; tp[1] = n1; tp[2] = n2; tp[3] = n3;
         }
         loaded = (k + 1 < sg.n_tiles) && (k + 1 < sd.t_end || carry);
-        if (loaded) load_unit(abase, d0, len, k + 1, lane, nx0, nx1, nx2, nx3);
-        if (lane == 0) W.nlong = 0;
-        W.bkey[lane + 1] = 0u;
+        if (loaded) load_unit(abase, d0, len, k + 1, lane, n0, n1, n2, n3);
         wsync();
 
-        const int64_t lo = (int64_t)k * TILE - d0;
+        const int64_t lo = (int64_t)k * TILE - d0;      // segment position of LDS byte 0
         const uint64_t vlo = lo < 0 ? 0ull : (uint64_t)lo;
         const uint64_t vhi = (uint64_t)(lo + TILE) > len ? len : (uint64_t)(lo + TILE);
+        const int64_t rem = (int64_t)len - lo;          // segment bytes from LDS byte 0 on
+        const int64_t vhi_r = (int64_t)vhi - lo;
         const TileView tv{sg.base, W.tile, len, lo};
         const int64_t cs_i = lo + (int64_t)lane * SC;
         const uint64_t cs = cs_i < (int64_t)vlo ? vlo : (uint64_t)cs_i;
@@ -679,25 +590,56 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
         }
         const bool walk = in_stripe && !search && entry < vhi;
         uint64_t tile_exit = entry;
-        uint32_t n_hop = 0, myrec = N32;
+        uint32_t n_hop = 0, kmx = 0;
+        int32_t myrec = -1;                 // hop record j = lane: tile offset, opcode, key / value lengths
+        uint32_t my_op = 0, my_klen = 0, my_vlen = 0;
+        bool hop_err = false;               // the chain broke at hop record n_hop - 1
         Stitched st;
         st.ent = N16; st.cnt = 0; st.base = 0; st.total = 0;
         if (walk) {
-            uint64_t p = entry;
-            if (KVR_ABLATE & 4) { n_hop = 0; p = vhi; }
-            else if (prev_n <= DENSE) {   // exact hops, all lanes together (LDS broadcast reads)
-                while (p < vhi && n_hop < HOP_MAX) {
-                    if (lane == (int)n_hop) myrec = (uint32_t)((int64_t)p - lo);
+            int64_t p = (int64_t)entry - lo;
+            if (KVR_ABLATE & 4) {
+                p = vhi_r;
+            } else if (prev_n <= DENSE) {   // exact hops: a 256-B window per LDS round trip
+                int wb = -4096;
+                uint32_t win = 0;
+#pragma unroll 1
+                while (p < vhi_r && n_hop < HOP_MAX) {
+                    const int pw = (int)(p >> 2);
+                    if (pw < wb || pw + 1 >= wb + 64) {
+                        wb = pw;
+                        win = wb + lane < WIN ? tw[wb + lane] : 0u;
+                    }
+                    const uint64_t x = win64(win, pw - wb) >> (8u * (uint32_t)(p & 3));
+                    const uint32_t op = (uint32_t)x & 255u;
+                    const uint64_t klen = (x >> 8) & 0xFFFFFFFFull;
+                    if (lane == (int)n_hop) { myrec = (int32_t)p; my_op = op; my_klen = (uint32_t)klen; }
                     ++n_hop;
-                    p = uni64(hop_next(tv, p));
-                    if (p == ERRP) break;
+                    const int64_t e = p + 5 + (int64_t)klen;
+                    if (op > 1u || rem - p < 5 || e > rem) { hop_err = true; break; }
+                    kmx = (uint32_t)klen > kmx ? (uint32_t)klen : kmx;
+                    if (op == 1u) { p = e; continue; }
+                    if (rem - e < 4) { hop_err = true; break; }
+                    uint32_t vlen;
+                    if (e + 4 <= TILE + HALO) {
+                        const int ew = (int)(e >> 2);
+                        if (ew >= wb && ew + 1 < wb + 64) vlen = (uint32_t)(win64(win, ew - wb) >> (8u * (uint32_t)(e & 3)));
+                        else vlen = uni32(tv.lds_u32(e));
+                    } else {
+                        vlen = uni32(tv.rd32((uint64_t)(lo + e)));
+                    }
+                    if (lane == (int)n_hop - 1) my_vlen = vlen;
+                    const int64_t e2 = e + 4 + (int64_t)vlen;
+                    if (e2 > rem) { hop_err = true; break; }
+                    p = e2;
                 }
             }
-            tile_exit = p;
-            if (p != ERRP && p < vhi) {   // dense: speculate per unit from the exact position p
+            tile_exit = hop_err ? ERRP : (uint64_t)(lo + p);
+            if (!hop_err && p < vhi_r) {   // dense: speculate per unit from the exact position
+                const uint64_t pa = (uint64_t)(lo + p);
                 uint16_t cand16 = N16, last16 = N16;
                 uint32_t x = X_BEYOND, cnt = 0;
-                const uint64_t p0 = cs > p ? cs : p;
+                const uint64_t p0 = cs > pa ? cs : pa;
                 if (p0 < ce) {
                     const uint64_t cand = find_cand(tv, p0, ce);
                     if (cand != NONE) {
@@ -710,7 +652,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
                 W.sc_cnt[lane] = (uint16_t)cnt;
                 W.sc_last[lane] = last16;
                 wsync();
-                st = stitch(W, tv, p, vhi, ctr);
+                st = stitch(W, tv, pa, vhi, ctr);
                 tile_exit = st.exit;
             }
         }
@@ -729,80 +671,131 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
         const uint64_t pool_base = chunk_base;
         chunk_base += nrec;
         chunk_left -= nrec;
-        // a value whose record started in an earlier tile begins in this one: register it
-        uint32_t n_carry = 0;
-        uint64_t n_vb = 0, n_ve = 0, n_idx = 0;
+        // a value whose record started in an earlier tile begins in this one
+        uint32_t n_carry = 0, n_idx = 0, n_state = 0;
+        uint64_t n_vb = 0, n_ve = 0;
+        bool pend_now = false;
         if (carry == 2u) {
-            if ((int64_t)c_vb - lo < TILE) {
-                if (lane == 0) {
-                    const int32_t pvb = (int32_t)((int64_t)c_vb - lo);
-                    const int64_t ve = (int64_t)c_ve - lo;
-                    W.lvb[0] = pvb;
-                    W.lve[0] = ve > FAR ? FAR : (int32_t)ve;
-                    W.lidx[0] = (uint32_t)c_idx;
-                    W.bkey[pvb / SC + 1] = (uint32_t)(pvb + 1) << 7;
-                    W.nlong = 1;
-                }
-                carry = 0;
-                n_vb = c_vb; n_ve = c_ve; n_idx = c_idx;   // in case it also runs past this tile
-            } else {                        // still further on: hand it over untouched
-                n_carry = 2; n_vb = c_vb; n_ve = c_ve; n_idx = c_idx;
-            }
+            if ((int64_t)c_vb - lo < TILE) { pend_now = true; carry = 0; }
+            else { n_carry = 2; n_vb = c_vb; n_ve = c_ve; n_idx = c_idx; }   // still further on
         }
-        wsync();
 
         KVR_STAMP(1);
         // ---- R. records ----------------------------------------------------------------------
-        RecRes ro;
-        ro.err = N32; ro.kind = 0; ro.aux = 0; ro.hand = 0; ro.vb = 0; ro.ve = 0; ro.slot = 0; ro.klen = 0;
-        uint32_t my_kmax = 0;
-        uint32_t hand = 0;
-        uint64_t pvb = 0, pve = 0, pidx = 0;
-        {   // this lane's records: its hop record (record index = lane), then its unit's speculated ones
-            const uint32_t has_hop = myrec != N32 ? 1u : 0u;
-            const uint32_t nmine = (KVR_ABLATE & 1) ? 0u : has_hop + (st.ent != N16 ? st.cnt : 0u);
-            uint64_t ps = (uint64_t)(lo + (int64_t)st.ent);
-            for (uint32_t i = 0; i < nmine; ++i) {
-                const bool h = i < has_hop;
-                const uint64_t p = h ? (uint64_t)(lo + (int64_t)myrec) : ps;
-                const uint32_t j = h ? (uint32_t)lane : n_hop + st.base + (i - has_hop);
-                ro = do_record(tv, W, S.T, p, j, pool_base + j, sd.seg, pool, pool_cap, kmax);
-                if (ro.hand) { hand = ro.hand; pvb = ro.vb; pve = ro.ve; pidx = ro.slot; }
-                my_kmax = ro.klen > my_kmax ? ro.klen : my_kmax;
-                if (ro.err != N32) break;
-                if (!h && i + 1 < nmine) ps = next_spec(tv, ps);
+        uint32_t rerr = N32, rkind = 0;
+        uint64_t raux = 0;
+        bool lA = false, lB = false;             // long value of the hop record / of a speculated record
+        int32_t lA_b = 0, lB_b = 0;
+        uint64_t lA_e = 0, lB_e = 0;
+        uint32_t lA_s = 0, lB_s = 0;
+        uint32_t hand = 0, pidx = 0;             // a value starting past the tile end (at most one)
+        uint64_t pvb = 0, pve = 0;
+        if (!(KVR_ABLATE & 1)) {
+            const bool fast = myrec >= 0 && !(hop_err && lane == (int)n_hop - 1);
+            if (myrec >= 0 && !fast) {           // the record that broke the chain: every check
+                const RecRes r = do_record(tv, K, (uint64_t)(lo + myrec), (uint32_t)lane, pool_base + lane, sd.seg,
+                                           pool, pool_cap);
+                rerr = r.err; rkind = r.kind; raux = r.aux;
+                if (r.err == N32) {              // defensive: a chain break is always an error
+                    rerr = (uint32_t)lane; rkind = KVR_E_VAL;
+                }
+            }
+            const uint32_t kc = kmx > 4u * KEYW ? 4u * KEYW : kmx;
+            const uint32_t nw = (kc + 3u) >> 2;  // key words of the longest fast-path key (uniform)
+            if (fast) {
+                const int p = myrec, kb = p + 5;
+                const uint32_t klen = my_klen;
+                const uint64_t slot = pool_base + (uint64_t)lane;
+                uint32_t c = ~0u;
+                bool done = false;
+                if (klen <= 4u * KEYW && kb + (int)klen + 4 <= TILE + HALO) {
+                    const int q = kb >> 2;
+                    const uint32_t sh = (uint32_t)kb & 3u;
+                    uint32_t r[KEYW + 1];
+#pragma unroll
+                    for (int i = 0; i <= KEYW; ++i) r[i] = (uint32_t)i <= nw ? tw[q + i] : 0u;
+                    uint32_t bad = 0, tail = 0;
+#pragma unroll
+                    for (int i = 0; i < KEYW; ++i) {
+                        if ((uint32_t)i < nw) {
+                            const uint32_t kw = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
+                            const uint32_t n = klen > 4u * i ? klen - 4u * i : 0u;
+                            const uint32_t msk = n >= 4u ? ~0u : ((1u << (8 * n)) - 1u);
+                            bad |= kw & msk & 0x80808080u;
+                            const uint32_t cn = crc4(c, kw, K);
+                            c = n >= 4u ? cn : c;
+                            tail = (n > 0u && n < 4u) ? kw : tail;
+                        }
+                    }
+                    for (uint32_t b = 0; b < (klen & 3u); ++b) c = crc1(c, (tail >> (8 * b)) & 255u, K);
+                    done = bad == 0u;
+                }
+                if (!done) {                     // non-ASCII or long key: the full UTF-8 check
+                    uint64_t vu = 0;
+                    uint32_t el = 0;
+                    if (!utf8_check(tv, (uint64_t)(lo + kb), klen, &vu, &el)) {       // engine.rs:114
+                        rerr = (uint32_t)lane; rkind = KVR_E_UTF8; raux = vu | ((uint64_t)el << 32);
+                    } else {
+                        c = crc_range(tv, ~0u, (uint64_t)(lo + kb), klen, K);
+                    }
+                }
+                if (rerr == N32) {
+                    kvr_tuple t;
+                    t.rec_off = (uint64_t)(lo + p);
+                    t.seg_idx = sd.seg;
+                    t.key_len = klen;
+                    t.val_len = 0;
+                    t.crc32 = 0;
+                    t.key_tag = ~c;
+                    t.op = (uint8_t)my_op;
+                    t.flags = 0;
+                    t.reserved = 0;
+                    if (my_op == 0u) {
+                        const int64_t vb = (int64_t)kb + klen + 4;
+                        t.val_len = my_vlen;
+                        if (my_vlen <= (uint32_t)SMALL) {
+                            t.crc32 = ~crc_range(tv, ~0u, (uint64_t)(lo + vb), my_vlen, K);
+                        } else if (vb < TILE) {
+                            lA = true; lA_b = (int32_t)vb; lA_e = (uint64_t)(lo + vb) + my_vlen; lA_s = (uint32_t)slot;
+                        } else {
+                            hand = 2; pvb = (uint64_t)(lo + vb); pve = pvb + my_vlen; pidx = (uint32_t)slot;
+                        }
+                    }
+                    if (slot < pool_cap) pool[slot] = t;
+                }
+            }
+            // records the dense path found in this lane's unit
+            if (st.ent != N16 && rerr == N32) {
+                uint64_t ps = (uint64_t)(lo + (int64_t)st.ent);
+#pragma unroll 1
+                for (uint32_t i = 0; i < st.cnt; ++i) {
+                    const uint32_t j = n_hop + st.base + i;
+                    const RecRes r = do_record(tv, K, ps, j, pool_base + j, sd.seg, pool, pool_cap);
+                    if (r.err != N32) { rerr = r.err; rkind = r.kind; raux = r.aux; break; }
+                    if (r.lng == 1u) { lB = true; lB_b = r.vb; lB_e = r.ve; lB_s = (uint32_t)(pool_base + j); }
+                    if (r.lng == 2u) { hand = 2; pvb = r.vbabs; pve = r.ve; pidx = (uint32_t)(pool_base + j); }
+                    if (i + 1 < st.cnt) ps = next_spec(tv, ps);
+                }
             }
         }
         KVR_STAMP(6);
-        // first error of the tile (lowest record index); longest key (fast-path bound of the next tile)
+        // first error of the tile (lowest record index)
         uint32_t err_rec = N32;
-        if (__ballot(ro.err != N32)) {
-            err_rec = ro.err;
+        if (__ballot(rerr != N32)) {
+            err_rec = rerr;
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) {
                 const uint32_t o = __shfl_xor(err_rec, d, 64);
                 err_rec = o < err_rec ? o : err_rec;
             }
             err_rec = uni32(err_rec);
-        }
-        if (nrec && ((k - sd.t_begin) & 15u) == 0u) {   // refresh the fast path's key bound now and then
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) {
-                const uint32_t ok = __shfl_xor(my_kmax, d, 64);
-                my_kmax = ok > my_kmax ? ok : my_kmax;
-            }
-            kmax = uni32(my_kmax) < 4u ? 4u : uni32(my_kmax);
-        } else if (__ballot(my_kmax > kmax)) {
-            kmax = 36u;                                  // a longer key appeared: widen at once
-        }
-        if (err_rec != N32) {
-            const int el = __builtin_ctzll(__ballot(ro.err == err_rec));
-            err_kind = rl32(ro.kind, el);
-            err_aux = rl64(ro.aux, el);
+            const int el = __builtin_ctzll(__ballot(rerr == err_rec));
+            err_kind = rl32(rkind, el);
+            err_aux = rl64(raux, el);
             // the failing record's start: hop records live in myrec, speculated ones are re-found
             uint64_t ep = NONE;
-            if (ro.err == err_rec) {
-                if (err_rec < n_hop) ep = (uint64_t)(lo + (int64_t)myrec);
+            if (rerr == err_rec) {
+                if (err_rec < n_hop) ep = (uint64_t)(lo + myrec);
                 else {
                     uint64_t p = (uint64_t)(lo + (int64_t)st.ent);
                     for (uint32_t i = n_hop + st.base; i < err_rec; ++i) p = next_spec(tv, p);
@@ -812,15 +805,14 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
             err_pos = rl64(ep, el);
         }
         KVR_STAMP(7);
-        // a long value crossing the tile end / starting later (one at most): its lane hands it over
-        {
-            const unsigned long long bp = __ballot(hand == 2u), bc = __ballot(hand == 1u);
-            if (bp | bc) {
-                const int ol = __builtin_ctzll(bp | bc);
+        {   // a value starting past the tile end (the tile's last record): hand it over
+            const unsigned long long bp = __ballot(hand == 2u);
+            if (bp) {
+                const int ol = __builtin_ctzll(bp);
+                n_carry = 2;
                 n_vb = rl64(pvb, ol);
                 n_ve = rl64(pve, ol);
-                n_idx = rl64(pidx, ol);
-                if (bp) n_carry = 2;
+                n_idx = rl32(pidx, ol);
             }
         }
         wsync();
@@ -828,92 +820,116 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
 
         KVR_STAMP(2);
         // ---- C. CRC of long values --------------------------------------------------------
-        const uint32_t nlong = uni32(W.nlong);
-        if (!(KVR_ABLATE & 2) && (nlong != 0u || carry == 1u)) {
-            // which value crosses the end of this lane's unit: latest long value starting before
-            // it (prefix max of boundary keys), if it reaches past it
-            uint32_t key = W.bkey[lane + 1];
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t o = __shfl_up(key, d, 64);
-                if (lane >= d && o > key) key = o;
+        const unsigned long long lmA = __ballot(lA), lmB = __ballot(lB);
+        if (!(KVR_ABLATE & 2) && (lmA || lmB || carry == 1u || pend_now)) {
+            const int32_t us = lane * SC, ue = us + SC;
+            bool vx = false;                     // a long value crosses the end of this unit
+            int32_t a_off = -1;                  // ... starting inside the unit at a_off
+            bool vx_carry = false;               // ... the value carried in from the previous tile
+            int32_t m = 0;                       // a long value ends inside this unit, at m (1 .. 64)
+            uint32_t m_slot = 0;
+            bool out = false;                    // (uniform) a value crosses the tile end
+            uint64_t out_ve = 0;
+            uint32_t out_slot = 0;
+            auto consider = [&](int32_t vb, uint64_t ve_abs, uint32_t slot, bool from_carry) {
+                const int64_t v64 = (int64_t)ve_abs - lo;
+                const int32_t ver = v64 > FAR ? FAR : (int32_t)v64;
+                if (vb < ue && ver > ue) { vx = true; a_off = vb >= us ? vb - us : -1; vx_carry = from_carry; }
+                if (vb < us && ver > us && ver <= ue) { m = ver - us; m_slot = slot; }
+                if (ver > TILE) { out = true; out_ve = ve_abs; out_slot = slot; }
+            };
+            if (carry == 1u) consider(-FAR, c_ve, c_idx, true);
+            if (pend_now) consider((int32_t)((int64_t)c_vb - lo), c_ve, c_idx, false);
+#pragma unroll 1
+            for (unsigned long long mm = lmA; mm; mm &= mm - 1ull) {
+                const int j = __builtin_ctzll(mm);
+                consider((int32_t)rl32((uint32_t)lA_b, j), rl64(lA_e, j), rl32(lA_s, j), false);
             }
-            const int32_t pb = SC * (lane + 1);
-            int32_t Vend = VNONE;
-            if (key != 0u) {
-                const int32_t L = (int32_t)(key & 127u);
-                if (W.lve[L] > pb) Vend = L;
-            } else if (carry == 1u && (int64_t)c_ve - lo > (int64_t)pb) {
-                Vend = VCARRY;
+#pragma unroll 1
+            for (unsigned long long mm = lmB; mm; mm &= mm - 1ull) {
+                const int j = __builtin_ctzll(mm);
+                consider((int32_t)rl32((uint32_t)lB_b, j), rl64(lB_e, j), rl32(lB_s, j), false);
             }
             KVR_STAMP(8);
-            int32_t Vst = __shfl_up(Vend, 1, 64);
-            if (lane == 0) Vst = carry == 1u ? VCARRY : VNONE;
-            const int32_t us = SC * lane;
-            const uint4 *up = reinterpret_cast<const uint4 *>(W.tile + us);   // this lane's unit
-            const uint4 cu0 = up[0], cu1 = up[1], cu2 = up[2], cu3 = up[3];
-            const uint32_t w[16] = {cu0.x, cu0.y, cu0.z, cu0.w, cu1.x, cu1.y, cu1.z, cu1.w,
-                                    cu2.x, cu2.y, cu2.z, cu2.w, cu3.x, cu3.y, cu3.z, cu3.w};
-            // One pass over the unit's bytes gives both register pieces this lane owns:
-            //  - raw CRC of [0, m) (bytes of the value crossing the unit start, if it ends here at m),
-            //    snapshotted on the way, and
-            //  - raw CRC of [a, 64) (the value crossing the unit end; a > 0 if it starts here), by
-            //    restarting the register at a's word with the bytes before a zeroed.
-            int32_t m = 0;                               // 1 .. 64 if the start-crossing value ends here
-            if (Vst != VNONE) {
-                const int64_t ve_rel = Vst == VCARRY ? (int64_t)c_ve - lo : (int64_t)W.lve[Vst];
-                if (ve_rel <= (int64_t)us + SC) m = (int32_t)(ve_rel - us);
-            }
-            int32_t a = 0;
-            bool starts = false;
-            if (Vend >= 0 && W.lvb[Vend] >= us) { a = W.lvb[Vend] - us; starts = true; }
-            const int qm = m >> 2, qa = starts ? (a >> 2) : -1;
+            // one pass over the unit (registers) gives both register pieces this lane owns:
+            //  - raw CRC of [0, m) (the value ending here), snapshotted on the way, and
+            //  - raw CRC of [a, 64) (the value crossing the unit end), restarting at a's word with
+            //    the bytes before a zeroed
+            const uint4 *up = reinterpret_cast<const uint4 *>(W.tile + lane * SC);   // this lane's unit
+            const uint4 v0 = up[0], v1 = up[1], v2 = up[2], v3 = up[3];
+            const uint32_t w[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+                                    v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
+            const int qm = m >> 2;
+            const int qa = (vx && a_off >= 0) ? (a_off >> 2) : -1;
+            const uint32_t amask = ~0u << (8 * (a_off & 3));
             uint32_t c = 0, snap = 0, wm = 0;
+            if (!__ballot(m != 0 || qa >= 0)) {
 #pragma unroll
-            for (int kk = 0; kk < 16; ++kk) {
-                snap = kk == qm ? c : snap;
-                wm = kk == qm ? w[kk] : wm;
-                c = kk == qa ? 0u : c;
-                const int sh = kk == qa ? 8 * (a & 3) : 0;   // bytes of a's word before a are zeroed
-                c = crc4(c, w[kk] & (~0u << sh), S.T);
+                for (int kk = 0; kk < 16; ++kk) c = crc4(c, w[kk], K);
+            } else {
+#pragma unroll
+                for (int kk = 0; kk < 16; ++kk) {
+                    snap = kk == qm ? c : snap;
+                    wm = kk == qm ? w[kk] : wm;
+                    const bool rs = kk == qa;
+                    c = rs ? 0u : c;
+                    c = crc4(c, rs ? (w[kk] & amask) : w[kk], K);
+                }
+                snap = qm == 16 ? c : snap;
             }
-            snap = qm == 16 ? c : snap;
             KVR_STAMP(9);
-            uint32_t v = 0, f = 1;
-            if (Vend != VNONE) {
-                if (starts) v = c ^ S.IX[SC - a];
-                else if (lane == 0) v = c ^ kmul(c_state, S.KT);   // the carried register across unit 0
+            uint32_t v = 0, f = 1;               // segment start f: no inflow from the previous unit
+            if (vx) {
+                if (a_off >= 0) v = c ^ S.IX[SC - a_off];
+                else if (lane == 0 && vx_carry) v = c ^ kmul(c_state, S.KT);   // carried register across unit 0
                 else { v = c; f = 0; }
             }
-            // segmented scan across the wave: state at boundary s+1 = f ? v : state(s) * X(64) ^ v
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                const int d = 1 << j;
-                const uint32_t ov = __shfl_up(v, d, 64);
-                const uint32_t of = __shfl_up(f, d, 64);
-                if (lane >= d && !f) { v ^= kmul(ov, S.KT + 128 * j); f = of; }
+            // segmented scan: state at the end of unit l = f ? v : state(l-1) * x^(8*64) ^ v
+#define KVR_SCAN_ROW(CTRL, D, KTAB)                                          \
+            {                                                                \
+                const uint32_t ov = dpp<CTRL>(v), of = dpp<CTRL>(f);         \
+                const uint32_t t_ = kmul(ov, KTAB);                          \
+                const bool ok = (lane & 15) >= (D) && !f;                    \
+                v = ok ? (v ^ t_) : v;                                       \
+                f = ok ? of : f;                                             \
+            }
+            KVR_SCAN_ROW(0x111, 1, S.KT)
+            KVR_SCAN_ROW(0x112, 2, S.KT + 128)
+            KVR_SCAN_ROW(0x114, 4, S.KT + 256)
+            KVR_SCAN_ROW(0x118, 8, S.KT + 384)
+#undef KVR_SCAN_ROW
+            {   // rows 1 and 3 take the end of rows 0 and 2 (lane 15, 47): distance (l & 15) + 1 units
+                const uint32_t ov = dpp<0x142, 0xA, false>(v), of = dpp<0x142, 0xA, false>(f);
+                const uint32_t t_ = kmulr(ov, S.KR, (uint32_t)(lane & 15));
+                const bool ok = (lane & 16) != 0 && !f;
+                v = ok ? (v ^ t_) : v;
+                f = ok ? of : f;
+            }
+            {   // rows 2 and 3 take the end of row 1 (lane 31): distance (l & 31) + 1 units
+                const uint32_t ov = dpp<0x143, 0xC, false>(v);
+                const uint32_t t_ = kmulr(ov, S.KR, (uint32_t)(lane & 31));
+                const bool ok = lane >= 32 && !f;
+                v = ok ? (v ^ t_) : v;
             }
             KVR_STAMP(10);
-            uint32_t sin = __shfl_up(v, 1, 64);
+            uint32_t sin = dpp<0x138>(v);        // wave_shr:1: the state at this unit's start
             if (lane == 0) sin = c_state;
-            // the value crossing the unit's start ends in this unit at m: its register is
-            // sin * x^(8m) ^ raw[0, m)  (the x^(8m) push: a constant table for 4q bytes + r zero bytes)
+            // the value ending in this unit at m: its register is sin * x^(8m) ^ raw[0, m)
+            // (the x^(8m) push: a constant table for 4q bytes + r zero bytes)
             if (m != 0) {
                 const int r = m & 3;
                 uint32_t rp = snap, cf = kmul(sin, S.KQ + 128 * qm);
                 for (int b = 0; b < r; ++b) {
-                    rp = crc1(rp, (wm >> (8 * b)) & 255u, S.T);
-                    cf = crc1(cf, 0u, S.T);
+                    rp = crc1(rp, (wm >> (8 * b)) & 255u, K);
+                    cf = crc1(cf, 0u, K);
                 }
-                const uint64_t idx = Vst == VCARRY ? c_idx : (uint64_t)W.lidx[Vst];
-                if (idx < pool_cap) pool[idx].crc32 = ~(cf ^ rp);
+                if (m_slot < pool_cap) pool[m_slot].crc32 = ~(cf ^ rp);
             }
-            // a value running past the tile: hand over its register state
-            const int32_t Vo = (int32_t)rl32((uint32_t)Vend, 63);
-            if (Vo != VNONE) {
+            if (out) {                           // the value running past the tile: hand over its register
                 n_carry = 1;
-                c_state = rl32(v, 63);
-                if (Vo == VCARRY) { n_vb = c_vb; n_ve = c_ve; n_idx = c_idx; }
+                n_state = rl32(v, 63);
+                n_ve = out_ve;
+                n_idx = out_slot;
             }
         }
 
@@ -930,6 +946,7 @@ __global__ __launch_bounds__(NT, 3) void k_replay(const SegDesc *__restrict__ se
             prev_n = nrec;
         }
         carry = n_carry;
+        c_state = n_state;
         c_vb = n_vb; c_ve = n_ve; c_idx = n_idx;
         if (err_pos != NONE) stop = 1;
         else if (walk && tile_exit == ERRP) {   // defensive: a broken chain must have reported
