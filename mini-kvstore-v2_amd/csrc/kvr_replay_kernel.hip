@@ -4,29 +4,28 @@
  * One WAVE replays one stripe (consecutive 4-KiB tiles of one segment) exactly as
  * src/store/engine.rs:79-154 walks a segment file, and emits one 32-B kvr_tuple per record with
  * the CRC-32 of its key and of its value (crc32fast::hash semantics, src/volume/storage.rs:27).
- * A workgroup holds 12 independent stripes that share the CRC tables; after the tables are
+ * A workgroup holds 16 independent stripes that share the CRC tables; after the tables are
  * staged in LDS there is no workgroup barrier, so a wave waiting on HBM never holds up another.
  *
  * Per tile, lane l owns the 64-B unit [64 l, 64 l + 64), prefetched one tile ahead into registers
  * with 16-B buffer loads and stored to the wave's LDS tile:
  *   F  framing, exact from the tile entry (the previous tile's exit).  The wave hops header to
- *      header: one hop reads a 256-B window of the tile into the 64 lanes (one dword each) and
- *      decodes op / key_len / val_len with scalar readlanes, so consecutive short records cost
- *      no further LDS round trip.  Dense tiles (more than 48 records in the previous tile, or
- *      more than 64 here) switch to per-unit speculation stitched by pointer jumping.  The
- *      stripe's first tile takes its first plausible record start; k_link verifies it.
- *   R  records: lane j emits hop record j with the engine.rs checks the hop did not already make
- *      (UTF-8 of the key), the key CRC from registers, and the CRC of a value of at most 64 B.
- *      Longer values stay in registers as (start, end, tuple slot).  Records found by
- *      speculation and the record that broke the chain take the general path (every check in
- *      engine.rs order).
- *   C  long values: every lane learns, by a wave-uniform loop over the tile's long values, which
- *      value crosses the end of its unit and which one ends inside it; it CRCs its unit's piece
- *      in one pass (a snapshot at the inner end, a restart at an inner start);
- *      a segmented scan across the wave (DPP row shifts, then row broadcasts; the multipliers
- *      x^(8*64*d) come from nibble tables) gives the CRC register at every unit boundary; the
- *      lane holding a value's last byte finishes that CRC.  A value running past the tile hands
- *      its register to the next tile of the stripe, so no variable GF(2) multiply is needed.
+ *      header in scalar registers: one hop reads a 256-B window of the tile into the 64 lanes
+ *      (one dword each) and decodes op / key_len / val_len with readlanes, so consecutive short
+ *      records cost no further LDS round trip.  Records are taken in batches of 64.  Only the
+ *      stripe's first tile guesses: it takes its first plausible record start, which k_link
+ *      checks against the previous stripe's exit (a wrong guess is re-walked from the true one).
+ *   R  records: lane j emits record j of the batch with the engine.rs check the hops did not
+ *      already make (UTF-8 of the key), the key CRC, and the CRC of a value of at most 64 B; the
+ *      record that broke the chain takes the general path (every check in engine.rs order).
+ *      A longer value is folded, per unit, into "which value crosses this unit's end, and where
+ *      does it start" / "which value ends inside this unit, and where".
+ *   C  long values: each lane CRCs its unit's piece in one pass (a snapshot at the inner end, a
+ *      restart at an inner start); a segmented scan across the wave (DPP row shifts, then row
+ *      broadcasts; the multipliers x^(8*64*d) come from nibble tables) gives the CRC
+ *      register at every unit boundary; the lane holding a value's last byte finishes that CRC.
+ *      A value running past the tile hands its register to the next tile of the stripe, so no
+ *      variable GF(2) multiply is needed.
  *
  * CRC tables: the slice-by-2 byte tables (T0: one byte, T1: a byte followed by a zero byte) are
  * replicated once per LDS bank: the entry for byte b of table t in lane l's copy sits at byte
@@ -37,27 +36,19 @@
 
 namespace kvr {
 
-constexpr int RT = 768;                   // threads per workgroup
+constexpr int RT = 1024;                  // threads per workgroup
 constexpr int WPB = RT / 64;              // stripes (waves) per workgroup
 constexpr int UNITS = TILE / SC;          // 64 units per tile = one per lane
 static_assert(UNITS == 64, "one 64-B unit per lane");
-constexpr uint16_t N16 = 0xFFFFu;
 constexpr uint32_t N32 = 0xFFFFFFFFu;
-constexpr uint32_t X_BEYOND = 0xFFFFFFFEu, X_ERR = 0xFFFFFFFFu;
 constexpr uint64_t BEYOND = ~0ull - 2;    // record end not readable from the tile (>= tile end)
-constexpr int T_END = 64, T_ERR = 65, T_MM = 66;
 constexpr uint32_t POOL_CHUNK = 2048;
-constexpr uint32_t HOP_MAX = 64;          // records found by hopping (one per lane)
-constexpr uint32_t DENSE = 48;            // previous tile's records above which we speculate at once
 constexpr int32_t FAR = 1 << 30;          // "ends beyond the tile" (tile-relative clamp)
 constexpr int KEYW = 6;                   // key words the record fast path holds (keys <= 24 B)
 constexpr int WIN = (TILE + HALO) / 4;    // dwords of tile + halo
 
-struct WaveLds {                          // one stripe's scratch
+struct WaveLds {                          // one stripe's scratch: the tile and its halo
     uint8_t  tile[TILE + HALO];
-    uint32_t sc_exit[UNITS];
-    uint16_t sc_cand[UNITS], sc_cnt[UNITS], sc_last[UNITS];
-    uint8_t  reach[UNITS];
 };
 
 // The tables come first: every table address is a lane-dependent VGPR plus a constant below
@@ -174,7 +165,7 @@ __device__ inline uint32_t crc_range(const TileView &tv, uint32_t c, uint64_t p,
 }
 
 // ---------------------------------------------------------------------------------------
-// speculative framing inside the tile (LDS only) — the dense path
+// the stripe's entry: its first plausible record start (LDS only; k_link verifies it)
 // ---------------------------------------------------------------------------------------
 // End of the record at p, ERRP (broken framing) or BEYOND (a field lies past the tile: the
 // record ends beyond it).  p must be inside the tile and < len.
@@ -198,8 +189,8 @@ __device__ __forceinline__ uint64_t next_spec(const TileView &tv, uint64_t p) {
 // without NUL?  Keys are String (engine.rs:114): a candidate whose "key" is random value bytes
 // fails the UTF-8 test, and one that starts a few bytes before a true header ([0][len LE]
 // makes an in-range length whose "key" is the zero bytes of the true length) fails the NUL test.
-// Heuristic only: a true record rejected here (a key holding NUL) is found again by the exact
-// chain walk or by the stripe link check, so results never depend on it.
+// Heuristic only: a true record rejected here (a key holding NUL) is found again by the stripe
+// link check and the exact re-walk, so results never depend on it.
 __device__ __forceinline__ bool key_prefix_ok(const TileView &tv, int off_k, uint32_t klen) {
     int m = TILE - off_k;
     m = m > 16 ? 16 : m;
@@ -264,118 +255,6 @@ __device__ __noinline__ uint64_t find_cand(const TileView tv, uint64_t p0, uint6
         }
     }
     return NONE;
-}
-
-// Walk from p while p < pe: records walked (a record whose framing fails counts: its parse
-// reports the error), last record start, exit offset (X_BEYOND / X_ERR)
-__device__ inline uint32_t walk_spec(const TileView &tv, uint64_t p, uint64_t pe, uint32_t *exit_off,
-                                     uint16_t *last_off) {
-    uint32_t cnt = 0;
-    uint16_t last = N16;
-    uint32_t x;
-    for (;;) {
-        if (p >= pe) {
-            const uint64_t r = p - (uint64_t)tv.lo;
-            x = r < (uint64_t)X_BEYOND ? (uint32_t)r : X_BEYOND;
-            break;
-        }
-        const uint64_t nx = next_spec(tv, p);
-        ++cnt;
-        last = (uint16_t)((int64_t)p - tv.lo);
-        if (nx == ERRP) { x = X_ERR; break; }
-        if (nx == BEYOND) { x = X_BEYOND; break; }
-        p = nx;
-    }
-    *exit_off = x;
-    *last_off = last;
-    return cnt;
-}
-
-// lane 0: the true chain enters the unit holding y at y; re-walk it and the following units
-// whose speculation disagrees with the true chain (bounded per call)
-__device__ void repair(WaveLds &W, const TileView &tv, uint64_t y, uint64_t vhi) {
-    const int64_t lo = tv.lo;
-    for (int k = 0; k < UNITS; ++k) {
-        const int t = (int)(((int64_t)y - lo) / SC);
-        const int64_t ce = lo + (int64_t)(t + 1) * SC;
-        const uint64_t pe = (uint64_t)ce > vhi ? vhi : (uint64_t)ce;
-        uint32_t x;
-        uint16_t last;
-        const uint32_t cnt = walk_spec(tv, y, pe, &x, &last);
-        W.sc_cand[t] = (uint16_t)((int64_t)y - lo);
-        W.sc_exit[t] = x;
-        W.sc_cnt[t] = (uint16_t)cnt;
-        W.sc_last[t] = last;
-        if (x >= X_BEYOND || lo + (int64_t)x >= (int64_t)vhi) return;
-        if (W.sc_cand[x / SC] == x) return;        // back in step with the speculation
-        y = (uint64_t)(lo + (int64_t)x);
-    }
-}
-
-struct Stitched { uint16_t ent; uint32_t cnt, base, total; uint64_t exit; };
-
-// Stitch the per-unit chains from the exact position e (vlo <= e < vhi) by pointer jumping:
-// per lane its unit's entry on the true chain (or N16) and record count/base; the tile exit.
-__device__ __noinline__ Stitched stitch(WaveLds &W, const TileView tv, uint64_t e, uint64_t vhi, Counters *ctr) {
-    const int lane = threadIdx.x & 63;
-    const int64_t lo = tv.lo;
-    const int s0 = (int)(((int64_t)e - lo) / SC);
-    const uint16_t e_off = (uint16_t)((int64_t)e - lo);
-    const uint32_t vhi_off = (uint32_t)((int64_t)vhi - lo);
-    Stitched R;
-    for (int guard = 0; guard < 2 * UNITS + 8; ++guard) {
-        if (W.sc_cand[s0] != e_off) {
-            if (lane == 0) repair(W, tv, e, vhi);
-            wsync();
-            continue;
-        }
-        const uint16_t c = W.sc_cand[lane];
-        const uint32_t x = W.sc_exit[lane];
-        int T;
-        if (c == N16) T = T_END;
-        else if (x == X_ERR) T = T_ERR;
-        else if (x >= vhi_off) T = T_END;              // includes X_BEYOND
-        else { const int t = (int)(x / SC); T = (W.sc_cand[t] == x) ? t : T_MM; }
-        W.reach[lane] = lane == s0 ? 1 : 0;
-        wsync();
-        int J = T;
-        bool reach = lane == s0;
-        for (int r = 0; r < 7 && __any(J < UNITS); ++r) {   // J <- J o J, reach <- reach U J(reach)
-            if (J < UNITS && reach) W.reach[J] = 1;
-            const int jn = J < UNITS ? __shfl(J, J, 64) : J;
-            wsync();
-            reach = W.reach[lane] != 0;
-            J = jn;
-        }
-        const unsigned long long rm = __ballot(reach);
-        const int smax = 63 - __builtin_clzll(rm);
-        const int Tl = (int)rl32((uint32_t)T, smax);
-        const uint32_t xs = rl32(x, smax);
-        if (Tl == T_MM) {
-            if (lane == 0) repair(W, tv, (uint64_t)(lo + (int64_t)xs), vhi);
-            wsync();
-            continue;
-        }
-        R.ent = reach ? c : N16;
-        R.cnt = reach ? W.sc_cnt[lane] : 0u;
-        uint32_t inc = R.cnt;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = __shfl_up(inc, d, 64);
-            if (lane >= d) inc += o;
-        }
-        R.base = inc - R.cnt;
-        R.total = rl32(inc, 63);
-        uint64_t xe;
-        if (Tl == T_ERR) xe = ERRP;
-        else if (xs != X_BEYOND) xe = (uint64_t)(lo + (int64_t)xs);
-        else xe = next_rec(tv, (uint64_t)(lo + (int64_t)W.sc_last[smax]));   // exact, halo / HBM
-        R.exit = uni64(xe);
-        return R;
-    }
-    if (lane == 0) atomicOr(&ctr->overflow, 2u);   // unreachable: every round repairs one more unit (bug trap)
-    R.ent = N16; R.cnt = 0; R.base = 0; R.total = 0; R.exit = ERRP;
-    return R;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -533,7 +412,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         if (lane == 0) atomicOr(&ctr->overflow, 4u);
     }
     uint64_t err_pos = NONE, err_aux = 0;
-    uint32_t err_kind = 0, total = 0, prev_n = 0;
+    uint32_t err_kind = 0, total = 0;
     uint64_t chunk_base = 0, chunk_left = 0;
     uint32_t carry = 0, c_state = 0, c_idx = 0;   // 1: a long value crosses the tile start (c_state: its register);
     uint64_t c_vb = 0, c_ve = 0;                  // 2: pending (its value starts in a later tile)
@@ -576,35 +455,75 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         const uint64_t ce = (uint64_t)(cs_i + SC) > vhi ? vhi : (uint64_t)(cs_i + SC);
 
         KVR_STAMP(0);
-        // ---- F. framing ------------------------------------------------------------------------
+        // ---- F + R. framing and records -------------------------------------------------------
         if (in_stripe && search) {   // the stripe's entry: the first plausible record start
             const uint64_t cand = cs < ce ? find_cand(tv, cs, ce) : NONE;
-            uint64_t m = cand;
+            uint64_t mn = cand;
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) {
-                const uint64_t o = __shfl_xor(m, d, 64);
-                m = o < m ? o : m;
+                const uint64_t o = __shfl_xor(mn, d, 64);
+                mn = o < mn ? o : mn;
             }
-            m = uni64(m);
-            if (m != NONE) { entry = m; search = false; stripe_entry = m; }
+            mn = uni64(mn);
+            if (mn != NONE) { entry = mn; search = false; stripe_entry = mn; }
         }
         const bool walk = in_stripe && !search && entry < vhi;
         uint64_t tile_exit = entry;
-        uint32_t n_hop = 0, kmx = 0;
-        int32_t myrec = -1;                 // hop record j = lane: tile offset, opcode, key / value lengths
-        uint32_t my_op = 0, my_klen = 0, my_vlen = 0;
-        bool hop_err = false;               // the chain broke at hop record n_hop - 1
-        Stitched st;
-        st.ent = N16; st.cnt = 0; st.base = 0; st.total = 0;
+        // the long values touching this tile, folded into every unit's view as they are found
+        const int32_t us = lane * SC, ue = us + SC;
+        bool vx = false;                     // a long value crosses the end of this unit
+        int32_t a_off = -1;                  // ... starting inside the unit at a_off
+        bool vx_carry = false;               // ... the value carried in from the previous tile
+        int32_t m = 0;                       // a long value ends inside this unit, at m (1 .. 64)
+        uint32_t m_slot = 0;
+        bool any_long = false;               // (uniform) some long value touches the tile
+        bool out = false;                    // (uniform) a value crosses the tile end
+        uint64_t out_ve = 0;
+        uint32_t out_slot = 0;
+        auto consider = [&](int32_t vb, uint64_t ve_abs, uint32_t slot, bool from_carry) {
+            const int64_t v64 = (int64_t)ve_abs - lo;
+            const int32_t ver = v64 > FAR ? FAR : (int32_t)v64;
+            if (vb < ue && ver > ue) { vx = true; a_off = vb >= us ? vb - us : -1; vx_carry = from_carry; }
+            if (vb < us && ver > us && ver <= ue) { m = ver - us; m_slot = slot; }
+            if (ver > TILE) { out = true; out_ve = ve_abs; out_slot = slot; }
+            any_long = true;
+        };
+        uint32_t n_carry = 0, n_idx = 0, n_state = 0;
+        uint64_t n_vb = 0, n_ve = 0;
+        if (carry == 1u) consider(-FAR, c_ve, c_idx, true);
+        if (carry == 2u) {                   // a value whose record started in an earlier tile
+            if ((int64_t)c_vb - lo < TILE) consider((int32_t)((int64_t)c_vb - lo), c_ve, c_idx, false);
+            else { n_carry = 2; n_vb = c_vb; n_ve = c_ve; n_idx = c_idx; }   // still further on
+        }
+        // pool slots: a tile's records take one contiguous run (k_compact reads them so); a tile
+        // holds at most TILE / 5 + 1 record starts
+        constexpr uint32_t TILE_RECS = TILE / 5 + 1;
+        if (walk && chunk_left < TILE_RECS) {
+            const uint64_t cm = pool_chunk > TILE_RECS ? pool_chunk : TILE_RECS;
+            unsigned long long b = 0;
+            if (lane == 0) {
+                b = atomicAdd(&ctr->pool_cursor, (unsigned long long)cm);
+                if (b + cm > pool_cap) atomicOr(&ctr->overflow, 1u);
+            }
+            chunk_base = uni64(b);
+            chunk_left = cm;
+        }
+        const uint64_t pool_base = chunk_base;
+        uint32_t nrec = 0, err_rec = N32;    // records emitted; index of the tile's first error
         if (walk) {
             int64_t p = (int64_t)entry - lo;
-            if (KVR_ABLATE & 4) {
-                p = vhi_r;
-            } else if (prev_n <= DENSE) {   // exact hops: a 256-B window per LDS round trip
+            bool broke = false;              // the chain broke at the last record walked
+            if (KVR_ABLATE & 4) p = vhi_r;
+#pragma unroll 1
+            while (p < vhi_r && !broke && err_rec == N32) {
+                // exact hops, a 256-B window per LDS round trip; lane j keeps record nrec + j
+                uint32_t nb = 0, kmx = 0;
+                int32_t myrec = -1;
+                uint32_t my_op = 0, my_klen = 0, my_vlen = 0;
                 int wb = -4096;
                 uint32_t win = 0;
 #pragma unroll 1
-                while (p < vhi_r && n_hop < HOP_MAX) {
+                while (p < vhi_r && nb < 64u) {
                     const int pw = (int)(p >> 2);
                     if (pw < wb || pw + 1 >= wb + 64) {
                         wb = pw;
@@ -613,13 +532,13 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     const uint64_t x = win64(win, pw - wb) >> (8u * (uint32_t)(p & 3));
                     const uint32_t op = (uint32_t)x & 255u;
                     const uint64_t klen = (x >> 8) & 0xFFFFFFFFull;
-                    if (lane == (int)n_hop) { myrec = (int32_t)p; my_op = op; my_klen = (uint32_t)klen; }
-                    ++n_hop;
+                    if (lane == (int)nb) { myrec = (int32_t)p; my_op = op; my_klen = (uint32_t)klen; }
+                    ++nb;
                     const int64_t e = p + 5 + (int64_t)klen;
-                    if (op > 1u || rem - p < 5 || e > rem) { hop_err = true; break; }
+                    if (op > 1u || rem - p < 5 || e > rem) { broke = true; break; }
                     kmx = (uint32_t)klen > kmx ? (uint32_t)klen : kmx;
                     if (op == 1u) { p = e; continue; }
-                    if (rem - e < 4) { hop_err = true; break; }
+                    if (rem - e < 4) { broke = true; break; }
                     uint32_t vlen;
                     if (e + 4 <= TILE + HALO) {
                         const int ew = (int)(e >> 2);
@@ -628,228 +547,135 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     } else {
                         vlen = uni32(tv.rd32((uint64_t)(lo + e)));
                     }
-                    if (lane == (int)n_hop - 1) my_vlen = vlen;
+                    if (lane == (int)nb - 1) my_vlen = vlen;
                     const int64_t e2 = e + 4 + (int64_t)vlen;
-                    if (e2 > rem) { hop_err = true; break; }
+                    if (e2 > rem) { broke = true; break; }
                     p = e2;
                 }
-            }
-            tile_exit = hop_err ? ERRP : (uint64_t)(lo + p);
-            if (!hop_err && p < vhi_r) {   // dense: speculate per unit from the exact position
-                const uint64_t pa = (uint64_t)(lo + p);
-                uint16_t cand16 = N16, last16 = N16;
-                uint32_t x = X_BEYOND, cnt = 0;
-                const uint64_t p0 = cs > pa ? cs : pa;
-                if (p0 < ce) {
-                    const uint64_t cand = find_cand(tv, p0, ce);
-                    if (cand != NONE) {
-                        cand16 = (uint16_t)((int64_t)cand - lo);
-                        cnt = walk_spec(tv, cand, ce, &x, &last16);
+                KVR_STAMP(1);
+                // the batch's records: lane j emits record nrec + j
+                uint32_t rerr = N32, rkind = 0;
+                uint64_t raux = 0;
+                bool lng = false;            // its value is longer than SMALL and starts in the tile
+                int32_t l_b = 0;
+                uint64_t l_e = 0;
+                uint32_t hand = 0;           // ... or starts past the tile end
+                uint64_t pvb = 0, pve = 0;
+                const uint32_t j = nrec + (uint32_t)lane;
+                const uint64_t slot = pool_base + j;
+                if (!(KVR_ABLATE & 1) && myrec >= 0) {
+                    if (broke && lane == (int)nb - 1) {   // the record that broke the chain: every check
+                        const RecRes r = do_record(tv, K, (uint64_t)(lo + myrec), j, slot, sd.seg, pool, pool_cap);
+                        rerr = r.err; rkind = r.kind; raux = r.aux;
+                        if (r.err == N32) { rerr = j; rkind = KVR_E_VAL; }   // defensive: a break is an error
+                    } else {
+                        const uint32_t kc = kmx > 4u * KEYW ? 4u * KEYW : kmx;
+                        const uint32_t nw = (kc + 3u) >> 2;   // key words of the longest fast-path key
+                        const int kb = myrec + 5;
+                        const uint32_t klen = my_klen;
+                        uint32_t c = ~0u;
+                        bool done = false;
+                        if (klen <= 4u * KEYW && kb + (int)klen + 4 <= TILE + HALO) {
+                            const int q = kb >> 2;
+                            const uint32_t sh = (uint32_t)kb & 3u;
+                            uint32_t r[KEYW + 1];
+#pragma unroll
+                            for (int i = 0; i <= KEYW; ++i) r[i] = (uint32_t)i <= nw ? tw[q + i] : 0u;
+                            uint32_t bad = 0, tail = 0;
+#pragma unroll
+                            for (int i = 0; i < KEYW; ++i) {
+                                if ((uint32_t)i < nw) {
+                                    const uint32_t kw = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
+                                    const uint32_t n = klen > 4u * i ? klen - 4u * i : 0u;
+                                    const uint32_t msk = n >= 4u ? ~0u : ((1u << (8 * n)) - 1u);
+                                    bad |= kw & msk & 0x80808080u;
+                                    const uint32_t cn = crc4(c, kw, K);
+                                    c = n >= 4u ? cn : c;
+                                    tail = (n > 0u && n < 4u) ? kw : tail;
+                                }
+                            }
+                            for (uint32_t bb = 0; bb < (klen & 3u); ++bb) c = crc1(c, (tail >> (8 * bb)) & 255u, K);
+                            done = bad == 0u;
+                        }
+                        if (!done) {                  // non-ASCII or long key: the full UTF-8 check
+                            uint64_t vu = 0;
+                            uint32_t el = 0;
+                            if (!utf8_check(tv, (uint64_t)(lo + kb), klen, &vu, &el)) {   // engine.rs:114
+                                rerr = j; rkind = KVR_E_UTF8; raux = vu | ((uint64_t)el << 32);
+                            } else {
+                                c = crc_range(tv, ~0u, (uint64_t)(lo + kb), klen, K);
+                            }
+                        }
+                        if (rerr == N32) {
+                            kvr_tuple t;
+                            t.rec_off = (uint64_t)(lo + myrec);
+                            t.seg_idx = sd.seg;
+                            t.key_len = klen;
+                            t.val_len = 0;
+                            t.crc32 = 0;
+                            t.key_tag = ~c;
+                            t.op = (uint8_t)my_op;
+                            t.flags = 0;
+                            t.reserved = 0;
+                            if (my_op == 0u) {
+                                const int64_t vb = (int64_t)kb + klen + 4;
+                                t.val_len = my_vlen;
+                                if (my_vlen <= (uint32_t)SMALL) {
+                                    t.crc32 = ~crc_range(tv, ~0u, (uint64_t)(lo + vb), my_vlen, K);
+                                } else if (vb < TILE) {
+                                    lng = true; l_b = (int32_t)vb; l_e = (uint64_t)(lo + vb) + my_vlen;
+                                } else {
+                                    hand = 2; pvb = (uint64_t)(lo + vb); pve = pvb + my_vlen;
+                                }
+                            }
+                            if (slot < pool_cap) pool[slot] = t;
+                        }
                     }
                 }
-                W.sc_cand[lane] = cand16;
-                W.sc_exit[lane] = x;
-                W.sc_cnt[lane] = (uint16_t)cnt;
-                W.sc_last[lane] = last16;
-                wsync();
-                st = stitch(W, tv, pa, vhi, ctr);
-                tile_exit = st.exit;
+                KVR_STAMP(6);
+                // first error of the batch (lowest record index)
+                if (__ballot(rerr != N32)) {
+                    uint32_t er = rerr;
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) {
+                        const uint32_t o = __shfl_xor(er, d, 64);
+                        er = o < er ? o : er;
+                    }
+                    err_rec = uni32(er);
+                    const int el = (int)(err_rec - nrec);
+                    err_kind = rl32(rkind, el);
+                    err_aux = rl64(raux, el);
+                    err_pos = (uint64_t)(lo + (int64_t)rl32((uint32_t)myrec, el));
+                }
+                // the batch's long values before the error, folded into every unit's view
+#pragma unroll 1
+                for (unsigned long long mm = __ballot(lng && j < err_rec); mm; mm &= mm - 1ull) {
+                    const int l = __builtin_ctzll(mm);
+                    consider((int32_t)rl32((uint32_t)l_b, l), rl64(l_e, l), (uint32_t)(pool_base + nrec) + (uint32_t)l, false);
+                }
+                {   // a value starting past the tile end (the tile's last record): hand it over
+                    const unsigned long long bp = __ballot(hand == 2u && j < err_rec);
+                    if (bp) {
+                        const int ol = __builtin_ctzll(bp);
+                        n_carry = 2;
+                        n_vb = rl64(pvb, ol);
+                        n_ve = rl64(pve, ol);
+                        n_idx = (uint32_t)(pool_base + nrec) + (uint32_t)ol;
+                    }
+                }
+                nrec = err_rec != N32 ? err_rec : nrec + nb;
+                KVR_STAMP(7);
             }
+            tile_exit = broke ? ERRP : (uint64_t)(lo + p);
         }
-        const uint32_t nrec = n_hop + st.total;
-        // pool slots for this tile's records (bulk chunks)
-        if (nrec > chunk_left) {
-            const uint64_t m = nrec > pool_chunk ? nrec : pool_chunk;
-            unsigned long long b = 0;
-            if (lane == 0) {
-                b = atomicAdd(&ctr->pool_cursor, (unsigned long long)m);
-                if (b + m > pool_cap) atomicOr(&ctr->overflow, 1u);
-            }
-            chunk_base = uni64(b);
-            chunk_left = m;
-        }
-        const uint64_t pool_base = chunk_base;
         chunk_base += nrec;
         chunk_left -= nrec;
-        // a value whose record started in an earlier tile begins in this one
-        uint32_t n_carry = 0, n_idx = 0, n_state = 0;
-        uint64_t n_vb = 0, n_ve = 0;
-        bool pend_now = false;
-        if (carry == 2u) {
-            if ((int64_t)c_vb - lo < TILE) { pend_now = true; carry = 0; }
-            else { n_carry = 2; n_vb = c_vb; n_ve = c_ve; n_idx = c_idx; }   // still further on
-        }
-
-        KVR_STAMP(1);
-        // ---- R. records ----------------------------------------------------------------------
-        uint32_t rerr = N32, rkind = 0;
-        uint64_t raux = 0;
-        bool lA = false, lB = false;             // long value of the hop record / of a speculated record
-        int32_t lA_b = 0, lB_b = 0;
-        uint64_t lA_e = 0, lB_e = 0;
-        uint32_t lA_s = 0, lB_s = 0;
-        uint32_t hand = 0, pidx = 0;             // a value starting past the tile end (at most one)
-        uint64_t pvb = 0, pve = 0;
-        if (!(KVR_ABLATE & 1)) {
-            const bool fast = myrec >= 0 && !(hop_err && lane == (int)n_hop - 1);
-            if (myrec >= 0 && !fast) {           // the record that broke the chain: every check
-                const RecRes r = do_record(tv, K, (uint64_t)(lo + myrec), (uint32_t)lane, pool_base + lane, sd.seg,
-                                           pool, pool_cap);
-                rerr = r.err; rkind = r.kind; raux = r.aux;
-                if (r.err == N32) {              // defensive: a chain break is always an error
-                    rerr = (uint32_t)lane; rkind = KVR_E_VAL;
-                }
-            }
-            const uint32_t kc = kmx > 4u * KEYW ? 4u * KEYW : kmx;
-            const uint32_t nw = (kc + 3u) >> 2;  // key words of the longest fast-path key (uniform)
-            if (fast) {
-                const int p = myrec, kb = p + 5;
-                const uint32_t klen = my_klen;
-                const uint64_t slot = pool_base + (uint64_t)lane;
-                uint32_t c = ~0u;
-                bool done = false;
-                if (klen <= 4u * KEYW && kb + (int)klen + 4 <= TILE + HALO) {
-                    const int q = kb >> 2;
-                    const uint32_t sh = (uint32_t)kb & 3u;
-                    uint32_t r[KEYW + 1];
-#pragma unroll
-                    for (int i = 0; i <= KEYW; ++i) r[i] = (uint32_t)i <= nw ? tw[q + i] : 0u;
-                    uint32_t bad = 0, tail = 0;
-#pragma unroll
-                    for (int i = 0; i < KEYW; ++i) {
-                        if ((uint32_t)i < nw) {
-                            const uint32_t kw = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
-                            const uint32_t n = klen > 4u * i ? klen - 4u * i : 0u;
-                            const uint32_t msk = n >= 4u ? ~0u : ((1u << (8 * n)) - 1u);
-                            bad |= kw & msk & 0x80808080u;
-                            const uint32_t cn = crc4(c, kw, K);
-                            c = n >= 4u ? cn : c;
-                            tail = (n > 0u && n < 4u) ? kw : tail;
-                        }
-                    }
-                    for (uint32_t b = 0; b < (klen & 3u); ++b) c = crc1(c, (tail >> (8 * b)) & 255u, K);
-                    done = bad == 0u;
-                }
-                if (!done) {                     // non-ASCII or long key: the full UTF-8 check
-                    uint64_t vu = 0;
-                    uint32_t el = 0;
-                    if (!utf8_check(tv, (uint64_t)(lo + kb), klen, &vu, &el)) {       // engine.rs:114
-                        rerr = (uint32_t)lane; rkind = KVR_E_UTF8; raux = vu | ((uint64_t)el << 32);
-                    } else {
-                        c = crc_range(tv, ~0u, (uint64_t)(lo + kb), klen, K);
-                    }
-                }
-                if (rerr == N32) {
-                    kvr_tuple t;
-                    t.rec_off = (uint64_t)(lo + p);
-                    t.seg_idx = sd.seg;
-                    t.key_len = klen;
-                    t.val_len = 0;
-                    t.crc32 = 0;
-                    t.key_tag = ~c;
-                    t.op = (uint8_t)my_op;
-                    t.flags = 0;
-                    t.reserved = 0;
-                    if (my_op == 0u) {
-                        const int64_t vb = (int64_t)kb + klen + 4;
-                        t.val_len = my_vlen;
-                        if (my_vlen <= (uint32_t)SMALL) {
-                            t.crc32 = ~crc_range(tv, ~0u, (uint64_t)(lo + vb), my_vlen, K);
-                        } else if (vb < TILE) {
-                            lA = true; lA_b = (int32_t)vb; lA_e = (uint64_t)(lo + vb) + my_vlen; lA_s = (uint32_t)slot;
-                        } else {
-                            hand = 2; pvb = (uint64_t)(lo + vb); pve = pvb + my_vlen; pidx = (uint32_t)slot;
-                        }
-                    }
-                    if (slot < pool_cap) pool[slot] = t;
-                }
-            }
-            // records the dense path found in this lane's unit
-            if (st.ent != N16 && rerr == N32) {
-                uint64_t ps = (uint64_t)(lo + (int64_t)st.ent);
-#pragma unroll 1
-                for (uint32_t i = 0; i < st.cnt; ++i) {
-                    const uint32_t j = n_hop + st.base + i;
-                    const RecRes r = do_record(tv, K, ps, j, pool_base + j, sd.seg, pool, pool_cap);
-                    if (r.err != N32) { rerr = r.err; rkind = r.kind; raux = r.aux; break; }
-                    if (r.lng == 1u) { lB = true; lB_b = r.vb; lB_e = r.ve; lB_s = (uint32_t)(pool_base + j); }
-                    if (r.lng == 2u) { hand = 2; pvb = r.vbabs; pve = r.ve; pidx = (uint32_t)(pool_base + j); }
-                    if (i + 1 < st.cnt) ps = next_spec(tv, ps);
-                }
-            }
-        }
-        KVR_STAMP(6);
-        // first error of the tile (lowest record index)
-        uint32_t err_rec = N32;
-        if (__ballot(rerr != N32)) {
-            err_rec = rerr;
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) {
-                const uint32_t o = __shfl_xor(err_rec, d, 64);
-                err_rec = o < err_rec ? o : err_rec;
-            }
-            err_rec = uni32(err_rec);
-            const int el = __builtin_ctzll(__ballot(rerr == err_rec));
-            err_kind = rl32(rkind, el);
-            err_aux = rl64(raux, el);
-            // the failing record's start: hop records live in myrec, speculated ones are re-found
-            uint64_t ep = NONE;
-            if (rerr == err_rec) {
-                if (err_rec < n_hop) ep = (uint64_t)(lo + myrec);
-                else {
-                    uint64_t p = (uint64_t)(lo + (int64_t)st.ent);
-                    for (uint32_t i = n_hop + st.base; i < err_rec; ++i) p = next_spec(tv, p);
-                    ep = p;
-                }
-            }
-            err_pos = rl64(ep, el);
-        }
-        KVR_STAMP(7);
-        {   // a value starting past the tile end (the tile's last record): hand it over
-            const unsigned long long bp = __ballot(hand == 2u);
-            if (bp) {
-                const int ol = __builtin_ctzll(bp);
-                n_carry = 2;
-                n_vb = rl64(pvb, ol);
-                n_ve = rl64(pve, ol);
-                n_idx = rl32(pidx, ol);
-            }
-        }
         wsync();
         if (loaded) load_halo(abase, d0, len, k + 1, lane, W.tile);   // this tile's halo reads are done
 
         KVR_STAMP(2);
         // ---- C. CRC of long values --------------------------------------------------------
-        const unsigned long long lmA = __ballot(lA), lmB = __ballot(lB);
-        if (!(KVR_ABLATE & 2) && (lmA || lmB || carry == 1u || pend_now)) {
-            const int32_t us = lane * SC, ue = us + SC;
-            bool vx = false;                     // a long value crosses the end of this unit
-            int32_t a_off = -1;                  // ... starting inside the unit at a_off
-            bool vx_carry = false;               // ... the value carried in from the previous tile
-            int32_t m = 0;                       // a long value ends inside this unit, at m (1 .. 64)
-            uint32_t m_slot = 0;
-            bool out = false;                    // (uniform) a value crosses the tile end
-            uint64_t out_ve = 0;
-            uint32_t out_slot = 0;
-            auto consider = [&](int32_t vb, uint64_t ve_abs, uint32_t slot, bool from_carry) {
-                const int64_t v64 = (int64_t)ve_abs - lo;
-                const int32_t ver = v64 > FAR ? FAR : (int32_t)v64;
-                if (vb < ue && ver > ue) { vx = true; a_off = vb >= us ? vb - us : -1; vx_carry = from_carry; }
-                if (vb < us && ver > us && ver <= ue) { m = ver - us; m_slot = slot; }
-                if (ver > TILE) { out = true; out_ve = ve_abs; out_slot = slot; }
-            };
-            if (carry == 1u) consider(-FAR, c_ve, c_idx, true);
-            if (pend_now) consider((int32_t)((int64_t)c_vb - lo), c_ve, c_idx, false);
-#pragma unroll 1
-            for (unsigned long long mm = lmA; mm; mm &= mm - 1ull) {
-                const int j = __builtin_ctzll(mm);
-                consider((int32_t)rl32((uint32_t)lA_b, j), rl64(lA_e, j), rl32(lA_s, j), false);
-            }
-#pragma unroll 1
-            for (unsigned long long mm = lmB; mm; mm &= mm - 1ull) {
-                const int j = __builtin_ctzll(mm);
-                consider((int32_t)rl32((uint32_t)lB_b, j), rl64(lB_e, j), rl32(lB_s, j), false);
-            }
+        if (!(KVR_ABLATE & 2) && any_long) {
             KVR_STAMP(8);
             // one pass over the unit (registers) gives both register pieces this lane owns:
             //  - raw CRC of [0, m) (the value ending here), snapshotted on the way, and
@@ -936,14 +762,12 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         KVR_STAMP(3);
         // ---- bookkeeping ------------------------------------------------------------------
         if (in_stripe) {
-            const uint32_t n_ok = err_rec < nrec ? err_rec : nrec;
             if (lane == 0) {
-                tres[sg.tile0 + k].pool_off = n_ok ? pool_base : 0ull;
-                tres[sg.tile0 + k].count = n_ok;
+                tres[sg.tile0 + k].pool_off = nrec ? pool_base : 0ull;
+                tres[sg.tile0 + k].count = nrec;
             }
-            total += n_ok;
+            total += nrec;
             if (walk) entry = tile_exit;
-            prev_n = nrec;
         }
         carry = n_carry;
         c_state = n_state;
