@@ -120,8 +120,12 @@ __device__ __forceinline__ uint32_t tget(const Crc &k, uint32_t x, uint32_t sel)
     return *reinterpret_cast<const uint32_t *>(k.t + __builtin_amdgcn_perm(x, k.L, sel));
 }
 // the register after the two bytes sitting in x's low half (x = register ^ data)
+// (both lookups are issued before either is used: the empty asm keeps the scheduler from
+// serialising them, which would cost a third LDS round trip per word)
 __device__ __forceinline__ uint32_t crc2(const Crc &k, uint32_t x) {
-    return (x >> 16) ^ tget(k, x, SEL_T1_B0) ^ tget(k, x, SEL_T0_B1);
+    uint32_t t0 = tget(k, x, SEL_T1_B0), t1 = tget(k, x, SEL_T0_B1);
+    asm volatile("" : "+v"(t0), "+v"(t1));
+    return (x >> 16) ^ t0 ^ t1;
 }
 __device__ __forceinline__ uint32_t crc4(uint32_t c, uint32_t w, const Crc &k) { return crc2(k, crc2(k, c ^ w)); }
 __device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
@@ -131,18 +135,24 @@ __device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
 
 // register state v times a constant K (nibble tables; every lane reads table i at once, so the
 // 16 entries sit in 16 banks and equal indices broadcast: conflict free)
+// (the eight lookups are independent: the empty asm makes the scheduler issue them all before
+// the first use instead of one LDS round trip each)
+__device__ __forceinline__ uint32_t xor8(uint32_t *t) {
+    asm volatile("" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]), "+v"(t[7]));
+    return ((t[0] ^ t[1]) ^ (t[2] ^ t[3])) ^ ((t[4] ^ t[5]) ^ (t[6] ^ t[7]));
+}
 __device__ __forceinline__ uint32_t kmul(uint32_t v, const uint32_t *K) {
-    uint32_t r = 0;
+    uint32_t t[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) r ^= K[i * 16 + ((v >> (4 * i)) & 15u)];
-    return r;
+    for (int i = 0; i < 8; ++i) t[i] = K[i * 16 + ((v >> (4 * i)) & 15u)];
+    return xor8(t);
 }
 // v times x^(8*64*(k+1)), k per lane (column k of KR: bank k mod 32, conflict free)
 __device__ __forceinline__ uint32_t kmulr(uint32_t v, const uint32_t *KR, uint32_t k) {
-    uint32_t r = 0;
+    uint32_t t[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) r ^= KR[(i * 16 + ((v >> (4 * i)) & 15u)) * 32 + k];
-    return r;
+    for (int i = 0; i < 8; ++i) t[i] = KR[(i * 16 + ((v >> (4 * i)) & 15u)) * 32 + k];
+    return xor8(t);
 }
 
 // CRC register update over segment bytes [p, p+n): LDS when resident (tile + halo), HBM otherwise
@@ -688,21 +698,34 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             const int qm = m >> 2;
             const int qa = (vx && a_off >= 0) ? (a_off >> 2) : -1;
             const uint32_t amask = ~0u << (8 * (a_off & 3));
-            uint32_t c = 0, snap = 0, wm = 0;
+            // two independent chains, words 0..7 (A) and 8..15 (B), each from a zero register
+            uint32_t ca = 0, cb = 0, sa = 0, sb = 0, wm = 0;
             if (!__ballot(m != 0 || qa >= 0)) {
 #pragma unroll
-                for (int kk = 0; kk < 16; ++kk) c = crc4(c, w[kk], K);
+                for (int kk = 0; kk < 8; ++kk) {
+                    ca = crc4(ca, w[kk], K);
+                    cb = crc4(cb, w[kk + 8], K);
+                }
             } else {
 #pragma unroll
-                for (int kk = 0; kk < 16; ++kk) {
-                    snap = kk == qm ? c : snap;
-                    wm = kk == qm ? w[kk] : wm;
-                    const bool rs = kk == qa;
-                    c = rs ? 0u : c;
-                    c = crc4(c, rs ? (w[kk] & amask) : w[kk], K);
+                for (int kk = 0; kk < 8; ++kk) {
+                    sa = kk == qm ? ca : sa;
+                    sb = kk + 8 == qm ? cb : sb;
+                    wm = kk == qm ? w[kk] : (kk + 8 == qm ? w[kk + 8] : wm);
+                    const bool ra = kk == qa, rb = kk + 8 == qa;
+                    ca = crc4(ra ? 0u : ca, ra ? (w[kk] & amask) : w[kk], K);
+                    cb = crc4(rb ? 0u : cb, rb ? (w[kk + 8] & amask) : w[kk + 8], K);
                 }
-                snap = qm == 16 ? c : snap;
+                sa = qm == 8 ? ca : sa;
+                sb = qm == 16 ? cb : sb;
             }
+            // the piece of the value crossing the unit end: A pushed through B's 32 bytes, then B
+            // (A does not count when that value starts in B's half); the raw CRC of the unit's
+            // first 4 qm bytes: A's snapshot, or all of A pushed through 4 (qm - 8) bytes, then B's
+            const uint32_t pa = kmul(ca, S.KQ + 128 * 8);
+            const uint32_t ps = kmul(ca, S.KQ + 128 * (qm > 8 ? qm - 8 : 0));
+            const uint32_t c = qa >= 8 ? cb : (pa ^ cb);
+            const uint32_t snap = qm <= 8 ? sa : (ps ^ sb);
             KVR_STAMP(9);
             uint32_t v = 0, f = 1;               // segment start f: no inflow from the previous unit
             if (vx) {
