@@ -93,22 +93,22 @@ static void build_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &kmul
             crc[t * 256 + i] = (prev >> 8) ^ crc[prev & 0xFF];
         }
     // X(n) = x^(8n) mod P (reflected): "push the register through n zero bytes"
-    std::vector<uint32_t> X(65);
+    std::vector<uint32_t> X(SC + 1);
     X[0] = GF_ONE;
-    for (int i = 1; i <= 64; ++i) X[i] = gf_mul(X[i - 1], 0x00800000u);   // * x^8
-    initx.assign(68, 0);
-    for (int j = 0; j <= 64; ++j) initx[j] = gf_mul(0xFFFFFFFFu, X[j]);
+    for (int i = 1; i <= SC; ++i) X[i] = gf_mul(X[i - 1], 0x00800000u);   // * x^8
+    initx.assign(NIX + 3, 0);
+    for (int j = 0; j < NIX; ++j) initx[j] = gf_mul(0xFFFFFFFFu, X[j]);
     // nibble tables of "multiply by a constant": kmul[t][i][n] = (n << 4i) * K_t, with
-    //   K_t = X(64 * 2^t) for t = 0 .. 7   (segmented scan across units)
-    //   K_t = X(4 * (t - 8)) for t = 8 .. 24 (finishing a value: the register pushed through 4q bytes)
-    //   K_t = X(64 * (t - 24)) for t = 25 .. 56 (cross-row steps of the segmented scan)
+    //   K_t = X(SC * 2^t)        for t < KSET_Q          (in-row steps of the segmented scan)
+    //   K_t = X(4 (t - KSET_Q))  for KSET_Q <= t < KSET_R (a register pushed through 4q bytes)
+    //   K_t = X(SC (t - KSET_R + 1)) for t >= KSET_R     (cross-row steps of the scan)
     kmul.assign(KMUL_SETS * 8 * 16, 0);
-    uint32_t K = X[64], R = X[64];
+    uint32_t K = X[SC], R = X[SC];
     for (int t = 0; t < KMUL_SETS; ++t) {
         uint32_t Kt;
         if (t < KSET_Q) { Kt = K; K = gf_mul(K, K); }
         else if (t < KSET_R) Kt = X[4 * (t - KSET_Q)];
-        else { Kt = R; R = gf_mul(R, X[64]); }
+        else { Kt = R; R = gf_mul(R, X[SC]); }
         for (int i = 0; i < 8; ++i)
             for (uint32_t n = 0; n < 16; ++n) kmul[(t * 8 + i) * 16 + n] = gf_mul(n << (4 * i), Kt);
     }
@@ -338,7 +338,7 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
     for (int attempt = 0; attempt < 10; ++attempt) {
         // each workgroup claims pool space in chunks of >= pool_chunk tuples: budget one partly
         // used chunk per stripe on top of the expected record count
-        const uint32_t pool_chunk = (uint32_t)std::min<uint64_t>(POOL_CHUNK, std::max<uint64_t>(256, tps * (TILE / 64)));
+        const uint32_t pool_chunk = POOL_CHUNK;
         const uint64_t pool_cap = std::max<uint64_t>(
             c->pool_hint, std::max<uint64_t>(65536, total_bytes / 192 + n + (uint64_t)n_stripes * pool_chunk));
         if (pool_cap > 0xFFFFFF00ull) return KVR_ENOMEM;   // k_replay keeps 32-bit pool slots in LDS

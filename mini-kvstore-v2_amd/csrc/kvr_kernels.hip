@@ -230,7 +230,9 @@ __global__ __launch_bounds__(CT) void k_compact(const TileRes *__restrict__ tres
             if (off[mid] - b0 <= k) lo_i = mid; else hi_i = mid - 1;
         }
         const uint64_t o = b0 + k;
-        const uint64_t src = tres[tb + lo_i].pool_off + (o - off[lo_i]);
+        const TileRes &tr = tres[tb + lo_i];
+        const uint64_t r = o - off[lo_i];                    // the tuple's index in its tile
+        const uint64_t src = r < tr.count1 ? tr.pool_off + r : tr.pool_off2 + (r - tr.count1);
         if (src >= pool_cap) continue;
         kvr_tuple tp = pool[src];
         if (expected && o < n_expected && tp.op == 0) {

@@ -1,31 +1,34 @@
 /*
- * kvr_replay_kernel.hip — k_replay (V6), the hot path (gfx950).
+ * kvr_replay_kernel.hip — k_replay (V7), the hot path (gfx950).
  *
- * One WAVE replays one stripe (consecutive 4-KiB tiles of one segment) exactly as
+ * One WAVE replays one stripe (consecutive 8-KiB tiles of one segment) exactly as
  * src/store/engine.rs:79-154 walks a segment file, and emits one 32-B kvr_tuple per record with
  * the CRC-32 of its key and of its value (crc32fast::hash semantics, src/volume/storage.rs:27).
- * A workgroup holds 16 independent stripes that share the CRC tables; after the tables are
- * staged in LDS there is no workgroup barrier, so a wave waiting on HBM never holds up another.
+ * A workgroup holds 12 independent stripes that share the CRC tables (the only LDS use); after
+ * the tables are staged there is no workgroup barrier.
  *
- * Per tile, lane l owns the 64-B unit [64 l, 64 l + 64), prefetched one tile ahead into registers
- * with 16-B buffer loads and stored to the wave's LDS tile:
+ * Per tile, lane l owns the 128-B unit [128 l, 128 l + 128), held in 32 registers and prefetched
+ * one tile ahead with 16-B buffer loads.  The tile is never copied anywhere else:
  *   F  framing, exact from the tile entry (the previous tile's exit).  The wave hops header to
- *      header in scalar registers: one hop reads a 256-B window of the tile into the 64 lanes
- *      (one dword each) and decodes op / key_len / val_len with readlanes, so consecutive short
- *      records cost no further LDS round trip.  Records are taken in batches of 64.  Only the
- *      stripe's first tile guesses: it takes its first plausible record start, which k_link
- *      checks against the previous stripe's exit (a wrong guess is re-walked from the true one).
+ *      header in scalar registers, reading the header words straight out of the lanes'
+ *      registers (uniform register index + readlane).  Each SET value longer than 64 B that
+ *      crosses a unit boundary is folded on the spot into every unit's view: "which value
+ *      crosses my end, and where does it start" / "which value ends inside me, and where".
+ *      Records are taken in batches of 64.
+ *      Only a stripe's first tile guesses: it takes its first plausible record start, which
+ *      k_link checks against the previous stripe's exit (a wrong guess is re-walked).
  *   R  records: lane j emits record j of the batch with the engine.rs check the hops did not
- *      already make (UTF-8 of the key), the key CRC, and the CRC of a value of at most 64 B; the
- *      record that broke the chain takes the general path (every check in engine.rs order).
- *      A longer value is folded, per unit, into "which value crosses this unit's end, and where
- *      does it start" / "which value ends inside this unit, and where".
- *   C  long values: each lane CRCs its unit's piece in one pass (a snapshot at the inner end, a
- *      restart at an inner start); a segmented scan across the wave (DPP row shifts, then row
- *      broadcasts; the multipliers x^(8*64*d) come from nibble tables) gives the CRC
- *      register at every unit boundary; the lane holding a value's last byte finishes that CRC.
- *      A value running past the tile hands its register to the next tile of the stripe, so no
- *      variable GF(2) multiply is needed.
+ *      make (UTF-8 of the key), the key CRC and the CRC of a value of at most 64 B or lying
+ *      inside one unit, reading key
+ *      and value bytes through a range-checked buffer resource (they are L2-hot: this wave just
+ *      streamed them).  The record that broke the chain takes the general path (every check in
+ *      engine.rs order).
+ *   C  long values: each lane CRCs its unit from registers in two independent chains, with a
+ *      snapshot where a value ends and a restart where one starts; a segmented scan across the
+ *      wave (DPP row shifts, then row broadcasts; the multipliers x^(8*128*d) come from
+ *      conflict-free nibble tables) gives the CRC register at every unit boundary; the lane
+ *      holding a value's last byte finishes that CRC.  A value running past the tile hands its
+ *      register to the next tile of the stripe, so no variable GF(2) multiply is needed.
  *
  * CRC tables: the slice-by-2 byte tables (T0: one byte, T1: a byte followed by a zero byte) are
  * replicated once per LDS bank: the entry for byte b of table t in lane l's copy sits at byte
@@ -36,30 +39,29 @@
 
 namespace kvr {
 
-constexpr int RT = 1024;                  // threads per workgroup
+constexpr int RT = 768;                   // threads per workgroup: 12 stripes, one per wave
 constexpr int WPB = RT / 64;              // stripes (waves) per workgroup
-constexpr int UNITS = TILE / SC;          // 64 units per tile = one per lane
-static_assert(UNITS == 64, "one 64-B unit per lane");
+constexpr int UW = SC / 4;                // dwords of a lane's unit
+constexpr int SC_LOG = 7;
+static_assert(SC == 1 << SC_LOG, "unit size");
+static_assert(TILE == 64 * SC, "one unit per lane");
+static_assert(UW == 32, "unit = 32 dwords");
 constexpr uint32_t N32 = 0xFFFFFFFFu;
-constexpr uint64_t BEYOND = ~0ull - 2;    // record end not readable from the tile (>= tile end)
-constexpr uint32_t POOL_CHUNK = 2048;
+constexpr uint32_t POOL_CHUNK = 2048;     // pool slots a wave claims at once
+constexpr uint32_t TILE_RECS = TILE / 5 + 1;   // most record starts a tile can hold
+static_assert(POOL_CHUNK >= TILE_RECS, "the rest of a tile's records fits in one fresh chunk");
 constexpr int32_t FAR = 1 << 30;          // "ends beyond the tile" (tile-relative clamp)
-constexpr int KEYW = 6;                   // key words the record fast path holds (keys <= 24 B)
-constexpr int WIN = (TILE + HALO) / 4;    // dwords of tile + halo
+constexpr int KEYW = 6;                   // key words the record fast path reads at once (<= 24 B)
+constexpr int VALW = SMALL / 4;           // value words of a short value
 
-struct WaveLds {                          // one stripe's scratch: the tile and its halo
-    uint8_t  tile[TILE + HALO];
-};
-
-// The tables come first: every table address is a lane-dependent VGPR plus a constant below
-// 64 KiB, which the ds_read instruction carries as its immediate offset.
+// The small tables come first: every table address is a lane-dependent VGPR plus a constant
+// below 64 KiB, which the ds_read instruction carries as its immediate offset.
 struct __align__(16) Smem {
-    uint32_t KR[8 * 16 * 32];             // [i][n][k]: (n << 4i) * x^(8*64*(k+1)), k < 32
-    uint32_t KT[4 * 8 * 16];              // [j][i][n]: (n << 4i) * x^(8*64*2^j), j < 4
-    uint32_t KQ[17 * 8 * 16];             // [q][i][n]: (n << 4i) * x^(8*4q), q <= 16
-    uint32_t IX[68];                      // 0xFFFFFFFF * x^(8j): initial register pushed through j bytes
+    uint32_t KR[8 * 16 * 32];             // [i][n][k]: (n << 4i) * x^(8*SC*(k+1)), k < 32
+    uint32_t KT[4 * 8 * 16];              // [j][i][n]: (n << 4i) * x^(8*SC*2^j), j < 4
+    uint32_t KQ[NQ * 8 * 16];             // [q][i][n]: (n << 4i) * x^(8*4q), q <= SC/4
+    uint32_t IX[NIX + 3];                 // 0xFFFFFFFF * x^(8j): initial register pushed through j bytes
     uint32_t C2[2 * 256 * 32];            // lane-replicated slice-by-2 byte tables (64 KiB)
-    WaveLds  w[WPB];
 };
 
 #ifndef KVR_ABLATE
@@ -78,12 +80,6 @@ __device__ unsigned long long g_prof[16];
 #define KVR_STAMP(i) do { } while (0)
 #endif
 
-__device__ __forceinline__ void wsync() {   // LDS writes of this wave visible to its other lanes
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-}
-
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {   // wave-uniform value into SGPRs
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
@@ -94,10 +90,6 @@ __device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
     return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
-}
-// two consecutive dwords of a wave-spread window as one little-endian 64-bit value, from word i
-__device__ __forceinline__ uint64_t win64(uint32_t win, int i) {
-    return ((uint64_t)rl32(win, i + 1) << 32) | rl32(win, i);
 }
 
 // DPP move (no LDS): CTRL = row_shr:d (0x110 + d), row_bcast:15 (0x142), row_bcast:31 (0x143),
@@ -134,9 +126,8 @@ __device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
 }
 
 // register state v times a constant K (nibble tables; every lane reads table i at once, so the
-// 16 entries sit in 16 banks and equal indices broadcast: conflict free)
-// (the eight lookups are independent: the empty asm makes the scheduler issue them all before
-// the first use instead of one LDS round trip each)
+// 16 entries sit in 16 banks and equal indices broadcast: conflict free).  The eight lookups
+// are independent: the empty asm makes the scheduler issue them all before the first use.
 __device__ __forceinline__ uint32_t xor8(uint32_t *t) {
     asm volatile("" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]), "+v"(t[7]));
     return ((t[0] ^ t[1]) ^ (t[2] ^ t[3])) ^ ((t[4] ^ t[5]) ^ (t[6] ^ t[7]));
@@ -147,7 +138,7 @@ __device__ __forceinline__ uint32_t kmul(uint32_t v, const uint32_t *K) {
     for (int i = 0; i < 8; ++i) t[i] = K[i * 16 + ((v >> (4 * i)) & 15u)];
     return xor8(t);
 }
-// v times x^(8*64*(k+1)), k per lane (column k of KR: bank k mod 32, conflict free)
+// v times x^(8*SC*(k+1)), k per lane (column k of KR: bank k mod 32, conflict free)
 __device__ __forceinline__ uint32_t kmulr(uint32_t v, const uint32_t *KR, uint32_t k) {
     uint32_t t[8];
 #pragma unroll
@@ -155,60 +146,149 @@ __device__ __forceinline__ uint32_t kmulr(uint32_t v, const uint32_t *KR, uint32
     return xor8(t);
 }
 
-// CRC register update over segment bytes [p, p+n): LDS when resident (tile + halo), HBM otherwise
-__device__ inline uint32_t crc_range(const TileView &tv, uint32_t c, uint64_t p, uint64_t n, const Crc &K) {
-    if (tv.in_lds(p, n)) {
-        int off = (int)((int64_t)p - tv.lo);
-        const int end = off + (int)n;
-        #pragma unroll 1
-        while (off < end && (off & 3)) { c = crc1(c, tv.lds[off], K); ++off; }
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(tv.lds);
-        #pragma unroll 1
-        while (off + 4 <= end) { c = crc4(c, w[off >> 2], K); off += 4; }
-        #pragma unroll 1
-        while (off < end) { c = crc1(c, tv.lds[off], K); ++off; }
-        return c;
+// ---------------------------------------------------------------------------------------
+// Segment reads relative to a tile's first byte (offset o = segment position lo + o), through a
+// buffer resource that ends at the segment's last 16-B word (words past it read as 0).  Used
+// for what is not in the registers: key and value bytes of the records, headers past the tile
+// end, the stripe's entry search.  Offsets the resource cannot reach (before the tile, or past
+// 2^31) go through plain loads; callers stay inside the segment.
+// ---------------------------------------------------------------------------------------
+struct TileSeg {
+    __amdgpu_buffer_rsrc_t rs;
+    int64_t lo;           // segment position of offset 0
+    uint64_t len;         // segment length
+    const uint8_t *seg;   // segment byte 0
+    int64_t lim;          // the resource covers offsets [0, lim)
+
+    __device__ __forceinline__ uint32_t b8(int64_t o) const {
+        if (o >= 0 && o < lim) return __builtin_amdgcn_raw_buffer_load_b8(rs, (int)o, 0, 0);
+        return seg[lo + o];
+    }
+    __device__ __forceinline__ uint32_t w32a(int o) const {   // 4-aligned, 0 <= o < lim
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0);
+    }
+    __device__ __forceinline__ uint32_t u32(int64_t o) const {   // any alignment; o .. o+3 in the segment
+        if (o >= 0 && o + 8 <= lim) {
+            const int a = (int)o & ~3;
+            return __builtin_amdgcn_alignbyte(w32a(a + 4), w32a(a), (uint32_t)o & 3u);
+        }
+        return b8(o) | (b8(o + 1) << 8) | (b8(o + 2) << 16) | (b8(o + 3) << 24);
+    }
+};
+
+// raw CRC register (from ~0) over the n <= 4 NW bytes at offset o >= 0 (o + 4 NW + 4 <= lim),
+// and in *bad the 0x80 bits of those bytes; nw (wave-uniform) >= the words any lane needs
+template <int NW>
+__device__ __forceinline__ uint32_t crc_span(const TileSeg &ts, const Crc &K, int o, uint32_t n, uint32_t nw,
+                                             uint32_t *bad) {
+    const int a = o & ~3;
+    const uint32_t sh = (uint32_t)o & 3u;
+    uint32_t r[NW + 1];
+#pragma unroll
+    for (int i = 0; i <= NW; ++i) r[i] = (uint32_t)i <= nw ? ts.w32a(a + 4 * i) : 0u;
+    uint32_t c = ~0u, tail = 0, bd = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        if ((uint32_t)i < nw) {
+            const uint32_t kw = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
+            const uint32_t m = n > 4u * i ? n - 4u * i : 0u;
+            const uint32_t msk = m >= 4u ? ~0u : ((1u << (8 * m)) - 1u);
+            bd |= kw & msk & 0x80808080u;
+            const uint32_t cn = crc4(c, kw, K);
+            c = m >= 4u ? cn : c;
+            tail = (m > 0u && m < 4u) ? kw : tail;
+        }
+    }
+    for (uint32_t b = 0; b < (n & 3u); ++b) c = crc1(c, (tail >> (8 * b)) & 255u, K);
+    *bad = bd;
+    return c;
+}
+
+// CRC register update over segment bytes [o, o + n) (any length; the general path)
+__device__ inline uint32_t crc_long(const TileSeg &ts, uint32_t c, int64_t o, uint64_t n, const Crc &K) {
+    const int64_t e = o + (int64_t)n;
+    #pragma unroll 1
+    while (o < e && ((o & 3) || o < 0 || o + 8 > ts.lim)) {
+        c = crc1(c, ts.b8(o), K);
+        ++o;
     }
     #pragma unroll 1
-    for (uint64_t i = 0; i < n; ++i) c = crc1(c, tv.rd8(p + i), K);
+    while (o + 4 <= e && o + 8 <= ts.lim) { c = crc4(c, ts.w32a((int)o), K); o += 4; }
+    #pragma unroll 1
+    while (o < e) { c = crc1(c, ts.b8(o), K); ++o; }
     return c;
 }
 
 // ---------------------------------------------------------------------------------------
-// the stripe's entry: its first plausible record start (LDS only; k_link verifies it)
+// UTF-8 validation with Rust's Utf8Error semantics (engine.rs:114, String::from_utf8).
+// Returns true if valid, else *vu = valid_up_to and *el = error_len (0 = incomplete).
 // ---------------------------------------------------------------------------------------
-// End of the record at p, ERRP (broken framing) or BEYOND (a field lies past the tile: the
-// record ends beyond it).  p must be inside the tile and < len.
-__device__ __forceinline__ uint64_t next_spec(const TileView &tv, uint64_t p) {
-    const uint64_t n = tv.len;
-    const int64_t off = (int64_t)p - tv.lo;
-    const uint32_t op = tv.lds[off];
-    if (op > 1u || n - p < 5) return ERRP;
-    if (off + 5 > TILE) return BEYOND;
-    const uint64_t e = p + 5 + (uint64_t)tv.lds_u32(off + 1);
-    if (e > n) return ERRP;
-    if (op == 1u) return e;
-    if (n - e < 4) return ERRP;
-    const int64_t eo = (int64_t)e - tv.lo;
-    if (eo + 4 > TILE) return BEYOND;
-    const uint64_t e2 = e + 4 + (uint64_t)tv.lds_u32(eo);
-    return e2 > n ? ERRP : e2;
+__device__ inline bool utf8_check(const TileSeg &ts, int64_t p, uint64_t n, uint64_t *vu, uint32_t *el) {
+    uint64_t i = 0;
+#pragma unroll 1
+    while (i < n) {
+        const int64_t q = p + (int64_t)i;
+        if (n - i >= 4 && q >= 0 && q + 8 <= ts.lim) {   // ASCII fast path, 4 bytes at a time
+            if ((ts.u32(q) & 0x80808080u) == 0) { i += 4; continue; }
+        }
+        const uint32_t b = ts.b8(q);
+        if (b < 0x80u) { ++i; continue; }
+        const uint64_t start = i;
+        int width = 0;
+        if (b >= 0xC2u && b <= 0xDFu) width = 2;
+        else if (b >= 0xE0u && b <= 0xEFu) width = 3;
+        else if (b >= 0xF0u && b <= 0xF4u) width = 4;
+        *vu = start;
+        if (width == 0) { *el = 1; return false; }
+        if (++i >= n) { *el = 0; return false; }
+        const uint32_t c1 = ts.b8(p + (int64_t)i);
+        bool ok1;
+        if (width == 2) ok1 = (c1 & 0xC0u) == 0x80u;
+        else if (width == 3)
+            ok1 = (b == 0xE0u && c1 >= 0xA0u && c1 <= 0xBFu) || (b >= 0xE1u && b <= 0xECu && c1 >= 0x80u && c1 <= 0xBFu) ||
+                  (b == 0xEDu && c1 >= 0x80u && c1 <= 0x9Fu) || (b >= 0xEEu && c1 >= 0x80u && c1 <= 0xBFu);
+        else
+            ok1 = (b == 0xF0u && c1 >= 0x90u && c1 <= 0xBFu) || (b >= 0xF1u && b <= 0xF3u && c1 >= 0x80u && c1 <= 0xBFu) ||
+                  (b == 0xF4u && c1 >= 0x80u && c1 <= 0x8Fu);
+        if (!ok1) { *el = 1; return false; }
+        for (int k = 2; k < width; ++k) {
+            if (++i >= n) { *el = 0; return false; }
+            if ((ts.b8(p + (int64_t)i) & 0xC0u) != 0x80u) { *el = (uint32_t)k; return false; }
+        }
+        ++i;
+    }
+    return true;
 }
 
-// Could the first min(klen, 16) key bytes (those inside the tile) begin a valid UTF-8 string
-// without NUL?  Keys are String (engine.rs:114): a candidate whose "key" is random value bytes
-// fails the UTF-8 test, and one that starts a few bytes before a true header ([0][len LE]
-// makes an in-range length whose "key" is the zero bytes of the true length) fails the NUL test.
-// Heuristic only: a true record rejected here (a key holding NUL) is found again by the stripe
-// link check and the exact re-walk, so results never depend on it.
-__device__ __forceinline__ bool key_prefix_ok(const TileView &tv, int off_k, uint32_t klen) {
-    int m = TILE - off_k;
-    m = m > 16 ? 16 : m;
-    m = (uint32_t)m > klen ? (int)klen : m;
+// ---------------------------------------------------------------------------------------
+// the stripe's entry: its first plausible record start (k_link verifies it)
+// ---------------------------------------------------------------------------------------
+// End of the record at o (engine.rs framing, exact), or -1 if the framing is broken there:
+// opcode outside {0,1} or a field running past the segment end.  o inside the segment.
+__device__ inline int64_t next_rec(const TileSeg &ts, int64_t o) {
+    const int64_t rem = (int64_t)ts.len - ts.lo;          // segment end, tile-relative
+    const uint32_t op = ts.b8(o);
+    if (op > 1u || rem - o < 5) return -1;
+    const int64_t e = o + 5 + (int64_t)ts.u32(o + 1);
+    if (e > rem) return -1;
+    if (op == 1u) return e;
+    if (rem - e < 4) return -1;
+    const int64_t e2 = e + 4 + (int64_t)ts.u32(e);
+    return e2 > rem ? -1 : e2;
+}
+
+// Could the first min(klen, 16) key bytes begin a valid UTF-8 string without NUL?  Keys are
+// String (engine.rs:114): a candidate whose "key" is random value bytes fails the UTF-8 test,
+// and one that starts a few bytes before a true header ([0][len LE] makes an in-range length
+// whose "key" is the zero bytes of the true length) fails the NUL test.  Heuristic only: a true
+// record rejected here (a key holding NUL) is found again by the stripe link check and the
+// exact re-walk, so results never depend on it.
+__device__ inline bool key_prefix_ok(const TileSeg &ts, int64_t ok, uint32_t klen) {
+    const int m = klen > 16u ? 16 : (int)klen;
     int i = 0;
     #pragma unroll 1
     while (i < m) {
-        const uint32_t b = tv.lds[off_k + i];
+        const uint32_t b = ts.b8(ok + i);
         if (b == 0u) return false;
         if (b < 0x80u) { ++i; continue; }
         int w;
@@ -218,120 +298,99 @@ __device__ __forceinline__ bool key_prefix_ok(const TileView &tv, int off_k, uin
         else if (b >= 0xF0u && b <= 0xF4u) { w = 4; if (b == 0xF0u) c_lo = 0x90u; if (b == 0xF4u) c_hi = 0x8Fu; }
         else return false;
         if (i + 1 >= m) return true;
-        const uint32_t c1 = tv.lds[off_k + i + 1];
+        const uint32_t c1 = ts.b8(ok + i + 1);
         if (c1 < c_lo || c1 > c_hi) return false;
         for (int k = 2; k < w; ++k) {
             if (i + k >= m) return true;
-            if ((tv.lds[off_k + i + k] & 0xC0u) != 0x80u) return false;
+            if ((ts.b8(ok + i + k) & 0xC0u) != 0x80u) return false;
         }
         i += w;
     }
     return true;
 }
 
-__device__ __forceinline__ bool plausible(const TileView &tv, uint64_t p) {
-    const uint64_t nx = next_spec(tv, p);
-    if (nx == ERRP) return false;
-    {
-        const int off = (int)((int64_t)p - tv.lo);
-        if (off + 5 < TILE && !key_prefix_ok(tv, off + 5, tv.lds_u32(off + 1))) return false;
-    }
-    const uint64_t n = tv.len;
-    if (nx == BEYOND || nx == n) return true;
-    const int64_t o = (int64_t)nx - tv.lo;
-    if (o + 5 > TILE) return true;                 // next header outside the tile: cannot check cheaply
-    if (tv.lds[o] > 1u || n - nx < 5) return false;
-    return nx + 5 + (uint64_t)tv.lds_u32(o + 1) <= n;
+__device__ inline bool plausible(const TileSeg &ts, int64_t o) {
+    const int64_t rem = (int64_t)ts.len - ts.lo;
+    const int64_t nx = next_rec(ts, o);
+    if (nx < 0) return false;
+    if (!key_prefix_ok(ts, o + 5, ts.u32(o + 1))) return false;
+    if (nx == rem) return true;
+    if (ts.b8(nx) > 1u || rem - nx < 5) return false;
+    return nx + 5 + (int64_t)ts.u32(nx + 1) <= rem;
 }
 
-// first plausible record start in [p0, p1) (inside the tile), or NONE
-__device__ __noinline__ uint64_t find_cand(const TileView tv, uint64_t p0, uint64_t p1) {
-    if (p0 >= p1) return NONE;
-    const int o0 = (int)((int64_t)p0 - tv.lo), o1 = (int)((int64_t)p1 - tv.lo);
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(tv.lds);
+// first plausible record start in [o0, o1) (tile offsets, inside this lane's unit), or -1
+__device__ __noinline__ int64_t find_cand(const TileSeg ts, int o0, int o1) {
     #pragma unroll 1
     for (int q = o0 >> 2; q <= (o1 - 1) >> 2; ++q) {
-        const uint32_t y = w[q] & 0xFEFEFEFEu;                 // bytes 0x00 / 0x01 become 0
+        const uint32_t y = ts.w32a(q * 4) & 0xFEFEFEFEu;        // bytes 0x00 / 0x01 become 0
         uint32_t z = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
         const int bq = q * 4;
         if (bq < o0) z &= ~0u << (8 * (o0 - bq));
         if (bq + 4 > o1) z &= (1u << (8 * (o1 - bq))) - 1u;
         #pragma unroll 1
         while (z) {
-            const int b = __builtin_ctz(z) >> 3;
-            const uint64_t p = (uint64_t)(tv.lo + bq + b);
-            if (plausible(tv, p)) return p;
+            const int o = bq + (__builtin_ctz(z) >> 3);
+            if (plausible(ts, o)) return o;
             z &= z - 1u;
         }
     }
-    return NONE;
+    return -1;
 }
 
 // ---------------------------------------------------------------------------------------
 // records
 // ---------------------------------------------------------------------------------------
-struct RecRes {          // one record's outcome
+struct RecRes {          // one record's outcome on the general path
     uint32_t err, kind;  // record index of an error (N32: none) and its KVR_E_* kind
     uint64_t aux;
-    uint32_t lng;        // its value is longer than SMALL: 1 starts inside the tile, 2 starts later
-    int32_t vb;          // value start, tile-relative (lng 1)
-    uint64_t vbabs, ve;  // value start / end, segment offsets
 };
 
-// parse + emit the record at p with every engine.rs check, in engine.rs order
-__device__ inline RecRes do_record(const TileView &tv, const Crc &K, uint64_t p, uint32_t j, uint64_t slot,
-                                   uint32_t seg, kvr_tuple *pool, uint64_t pool_cap) {
+// parse + emit the record at tile offset o with every engine.rs check, in engine.rs order
+// (its value, if longer than SMALL, was folded by the hop loop)
+__device__ inline RecRes do_record(const TileSeg &ts, const Crc &K, int64_t o, uint32_t j, uint64_t slot, uint32_t seg,
+                                   kvr_tuple *pool, uint64_t pool_cap) {
     RecRes ro;
-    ro.err = N32; ro.kind = 0; ro.aux = 0; ro.lng = 0; ro.vb = 0; ro.vbabs = 0; ro.ve = 0;
-    const uint64_t len = tv.len;
-    const uint32_t op = tv.rd8(p);
-    if (len - p < 5) { ro.err = j; ro.kind = KVR_E_KEY_LEN; return ro; }                 // engine.rs:96
-    const uint64_t klen = tv.rd32(p + 1);
-    const uint64_t kb = p + 5;
-    if (len - kb < klen) { ro.err = j; ro.kind = KVR_E_KEY; return ro; }                  // engine.rs:107
+    ro.err = N32; ro.kind = 0; ro.aux = 0;
+    const int64_t rem = (int64_t)ts.len - ts.lo;
+    const uint32_t op = ts.b8(o);
+    if (rem - o < 5) { ro.err = j; ro.kind = KVR_E_KEY_LEN; return ro; }                  // engine.rs:96
+    const uint64_t klen = ts.u32(o + 1);
+    const int64_t kb = o + 5;
+    if ((uint64_t)(rem - kb) < klen) { ro.err = j; ro.kind = KVR_E_KEY; return ro; }      // engine.rs:107
     uint64_t vu = 0;
     uint32_t el = 0;
-    if (!utf8_check(tv, kb, klen, &vu, &el)) {                                          // engine.rs:114
+    if (!utf8_check(ts, kb, klen, &vu, &el)) {                                          // engine.rs:114
         ro.err = j; ro.kind = KVR_E_UTF8; ro.aux = vu | ((uint64_t)el << 32); return ro;
     }
     if (op > 1u) { ro.err = j; ro.kind = KVR_E_OPCODE; ro.aux = op; return ro; }          // engine.rs:143
     kvr_tuple t;
-    t.rec_off = p;
+    t.rec_off = (uint64_t)(ts.lo + o);
     t.seg_idx = seg;
     t.key_len = (uint32_t)klen;
-    t.key_tag = ~crc_range(tv, ~0u, kb, klen, K);
+    t.key_tag = ~crc_long(ts, ~0u, kb, klen, K);
     t.op = (uint8_t)op;
     t.flags = 0;
     t.reserved = 0;
     t.crc32 = 0;
     t.val_len = 0;
     if (op == 0u) {
-        const uint64_t q = kb + klen;
-        if (len - q < 4) { ro.err = j; ro.kind = KVR_E_VAL_LEN; return ro; }              // engine.rs:121
-        const uint64_t vlen = tv.rd32(q);
-        const uint64_t vb = q + 4, ve = vb + vlen;
-        if (len - vb < vlen) { ro.err = j; ro.kind = KVR_E_VAL; return ro; }              // engine.rs:130
+        const int64_t q = kb + (int64_t)klen;
+        if (rem - q < 4) { ro.err = j; ro.kind = KVR_E_VAL_LEN; return ro; }              // engine.rs:121
+        const uint64_t vlen = ts.u32(q);
+        if ((uint64_t)(rem - q - 4) < vlen) { ro.err = j; ro.kind = KVR_E_VAL; return ro; }   // engine.rs:130
         t.val_len = (uint32_t)vlen;
-        if (vlen <= (uint64_t)SMALL) {
-            t.crc32 = ~crc_range(tv, ~0u, vb, vlen, K);
-        } else {
-            const int64_t vbr = (int64_t)vb - tv.lo;
-            ro.lng = vbr < TILE ? 1u : 2u;
-            ro.vb = (int32_t)(vbr < TILE ? vbr : 0);
-            ro.vbabs = vb;
-            ro.ve = ve;
-        }
+        if (vlen <= (uint64_t)SMALL) t.crc32 = ~crc_long(ts, ~0u, q + 4, vlen, K);
     }
     if (slot < pool_cap) pool[slot] = t;
     return ro;
 }
 
-// this lane's 64-B unit of tile k: four 16-B raw buffer loads through a per-tile resource whose
-// range is the 16-B words touching the segment, so words outside it read as 0 in hardware (no
-// per-word compares, no select of pointers)
+// this lane's 128-B unit of tile k: eight 16-B raw buffer loads through a per-tile resource whose
+// range is the 16-B words touching the segment, so words outside it read as 0 in hardware
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void load_unit(const uint8_t *abase, int64_t d0, uint64_t len, uint32_t k, int lane,
-                                          uint4 &r0, uint4 &r1, uint4 &r2, uint4 &r3) {
+                                          uint32_t *r) {
     const int64_t t0 = (int64_t)k * TILE;
     const int64_t first = d0 & ~(int64_t)15, endw = (d0 + (int64_t)len + 15) & ~(int64_t)15;
     const int64_t skip = first > t0 ? first - t0 : 0;
@@ -343,28 +402,30 @@ __device__ __forceinline__ void load_unit(const uint8_t *abase, int64_t d0, uint
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(((uint64_t)bhi << 32) | blo), (short)0, nr, 0x00020000);
     const int vo = lane * SC - (int)skip;   // negative -> out of range -> 0
-    const u32x4 a0 = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 0);
-    const u32x4 a1 = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16, 0, 0);
-    const u32x4 a2 = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 32, 0, 0);
-    const u32x4 a3 = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 48, 0, 0);
-    r0 = make_uint4(a0.x, a0.y, a0.z, a0.w);
-    r1 = make_uint4(a1.x, a1.y, a1.z, a1.w);
-    r2 = make_uint4(a2.x, a2.y, a2.z, a2.w);
-    r3 = make_uint4(a3.x, a3.y, a3.z, a3.w);
+#pragma unroll
+    for (int i = 0; i < UW / 4; ++i) {
+        const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16 * i, 0, 0);
+        r[4 * i] = a.x; r[4 * i + 1] = a.y; r[4 * i + 2] = a.z; r[4 * i + 3] = a.w;
+    }
 }
 
-// halo of tile k: the next HALO bytes after it, LDS-DMA into tile + TILE (lanes 0 .. HALO/16-1)
-__device__ __forceinline__ void load_halo(const uint8_t *abase, int64_t d0, uint64_t len, uint32_t k, int lane,
-                                          uint8_t *tile) {
-    if (lane < HALO / 16) {
-        const int64_t pos = (int64_t)k * TILE - d0 + TILE + 16 * lane;
-        if (pos < (int64_t)len)
-            __builtin_amdgcn_global_load_lds(
-                reinterpret_cast<const void *>(abase + (int64_t)k * TILE + TILE + 16 * lane),
-                reinterpret_cast<__attribute__((address_space(3))) void *>(
-                    (__attribute__((address_space(3))) uint8_t *)(tile + TILE)),
-                16, 0, 0);
-    }
+// the reads of tile k relative to its first byte (see TileSeg)
+__device__ __forceinline__ TileSeg tile_seg(const uint8_t *abase, const uint8_t *seg, int64_t d0, uint64_t len,
+                                            uint32_t k) {
+    TileSeg ts;
+    const int64_t t0 = (int64_t)k * TILE;
+    const int64_t endw = (d0 + (int64_t)len + 15) & ~(int64_t)15;
+    int64_t lim = endw - t0;
+    lim = lim > 0x7FFFFF00ll ? 0x7FFFFF00ll : lim;
+    const uint64_t b = (uint64_t)(abase + t0);
+    const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)b), bhi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    ts.rs = __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)bhi << 32) | blo), (short)0,
+                                              __builtin_amdgcn_readfirstlane((int)lim), 0x00020000);
+    ts.lo = t0 - d0;
+    ts.len = len;
+    ts.seg = seg;
+    ts.lim = lim;
+    return ts;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -383,8 +444,8 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     for (int i = tid; i < 8 * 16 * 32; i += RT)
         S.KR[i] = tb.kmul[((KSET_R + (i & 31)) * 8 + (i >> 9)) * 16 + ((i >> 5) & 15)];
     for (int i = tid; i < 4 * 8 * 16; i += RT) S.KT[i] = tb.kmul[i];
-    for (int i = tid; i < 17 * 8 * 16; i += RT) S.KQ[i] = tb.kmul[KSET_Q * 8 * 16 + i];
-    if (tid < 65) S.IX[tid] = tb.initx[tid];
+    for (int i = tid; i < NQ * 8 * 16; i += RT) S.KQ[i] = tb.kmul[KSET_Q * 8 * 16 + i];
+    if (tid < NIX) S.IX[tid] = tb.initx[tid];
     __syncthreads();   // the only workgroup barrier: from here on every wave is on its own
 
     const Crc K{reinterpret_cast<const uint8_t *>(S.C2),
@@ -401,8 +462,6 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         if (gw >= n_stripes) return;
         si = gw;
     }
-    WaveLds &W = S.w[wv];
-    const uint32_t *tw = reinterpret_cast<const uint32_t *>(W.tile);
     const StripeDesc sd = stripes[si];
     const SegDesc sg = segs[sd.seg];
     const uint64_t len = sg.len;
@@ -424,12 +483,11 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     uint64_t err_pos = NONE, err_aux = 0;
     uint32_t err_kind = 0, total = 0;
     uint64_t chunk_base = 0, chunk_left = 0;
-    uint32_t carry = 0, c_state = 0, c_idx = 0;   // 1: a long value crosses the tile start (c_state: its register);
-    uint64_t c_vb = 0, c_ve = 0;                  // 2: pending (its value starts in a later tile)
+    uint32_t carry = 0, c_state = 0;              // 1: a long value crosses the tile start (c_state: its register);
+    uint64_t c_vb = 0, c_ve = 0, c_slot = 0;      // 2: pending (its value starts in a later tile)
 
-    uint4 n0, n1, n2, n3;   // this lane's unit of the next tile (prefetch)
-    load_unit(abase, d0, len, sd.t_begin, lane, n0, n1, n2, n3);
-    load_halo(abase, d0, len, sd.t_begin, lane, W.tile);
+    uint32_t nxt[UW];   // this lane's unit of the next tile (prefetch)
+    load_unit(abase, d0, len, sd.t_begin, lane, nxt);
     bool loaded = true;
     uint32_t k = sd.t_begin;
 #ifdef KVR_PROF
@@ -442,33 +500,36 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         const bool in_stripe = k < sd.t_end;
         if (stop || (!in_stripe && !carry) || k >= sg.n_tiles) break;
         if (!loaded) {
-            load_unit(abase, d0, len, k, lane, n0, n1, n2, n3);
-            load_halo(abase, d0, len, k, lane, W.tile);
+            load_unit(abase, d0, len, k, lane, nxt);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        {
-            uint4 *tp = reinterpret_cast<uint4 *>(W.tile + lane * SC);
-            tp[0] = n0; tp[1] = n1; tp[2] = n2; tp[3] = n3;
-        }
+        uint32_t w[UW];                  // this tile's unit
+#pragma unroll
+        for (int i = 0; i < UW; ++i) w[i] = nxt[i];
         loaded = (k + 1 < sg.n_tiles) && (k + 1 < sd.t_end || carry);
-        if (loaded) load_unit(abase, d0, len, k + 1, lane, n0, n1, n2, n3);
-        wsync();
+        if (loaded) load_unit(abase, d0, len, k + 1, lane, nxt);
 
-        const int64_t lo = (int64_t)k * TILE - d0;      // segment position of LDS byte 0
+        const int64_t lo = (int64_t)k * TILE - d0;      // segment position of tile byte 0
         const uint64_t vlo = lo < 0 ? 0ull : (uint64_t)lo;
         const uint64_t vhi = (uint64_t)(lo + TILE) > len ? len : (uint64_t)(lo + TILE);
-        const int64_t rem = (int64_t)len - lo;          // segment bytes from LDS byte 0 on
-        const int64_t vhi_r = (int64_t)vhi - lo;
-        const TileView tv{sg.base, W.tile, len, lo};
-        const int64_t cs_i = lo + (int64_t)lane * SC;
-        const uint64_t cs = cs_i < (int64_t)vlo ? vlo : (uint64_t)cs_i;
-        const uint64_t ce = (uint64_t)(cs_i + SC) > vhi ? vhi : (uint64_t)(cs_i + SC);
+        const int64_t rem = (int64_t)len - lo;          // segment bytes from tile byte 0 on
+        const int64_t vlo_r = (int64_t)vlo - lo, vhi_r = (int64_t)vhi - lo;
+        const TileSeg ts = tile_seg(abase, sg.base, d0, len, k);
+        const int us = lane * SC, ue = us + SC;
+        // the little-endian u64 at tile offset o (uniform, 0 <= o, o + 8 <= TILE): out of the
+        // lanes' registers (uniform register index + readlane), no memory access
+        auto tword = [&](int j) -> uint32_t { return rl32(w[j & (UW - 1)], j >> 5); };
+        auto tu64 = [&](int o) -> uint64_t {
+            const int j = o >> 2;
+            return ((((uint64_t)tword(j + 1)) << 32) | tword(j)) >> (8u * (uint32_t)(o & 3));
+        };
 
         KVR_STAMP(0);
         // ---- F + R. framing and records -------------------------------------------------------
         if (in_stripe && search) {   // the stripe's entry: the first plausible record start
-            const uint64_t cand = cs < ce ? find_cand(tv, cs, ce) : NONE;
-            uint64_t mn = cand;
+            const int o0 = us > (int)vlo_r ? us : (int)vlo_r, o1 = ue < (int)vhi_r ? ue : (int)vhi_r;
+            const int64_t cand = o0 < o1 ? find_cand(ts, o0, o1) : -1;
+            uint64_t mn = cand >= 0 ? (uint64_t)(lo + cand) : NONE;
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) {
                 const uint64_t o = __shfl_xor(mn, d, 64);
@@ -480,45 +541,35 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         const bool walk = in_stripe && !search && entry < vhi;
         uint64_t tile_exit = entry;
         // the long values touching this tile, folded into every unit's view as they are found
-        const int32_t us = lane * SC, ue = us + SC;
         bool vx = false;                     // a long value crosses the end of this unit
         int32_t a_off = -1;                  // ... starting inside the unit at a_off
         bool vx_carry = false;               // ... the value carried in from the previous tile
-        int32_t m = 0;                       // a long value ends inside this unit, at m (1 .. 64)
-        uint32_t m_slot = 0;
+        int32_t m = 0;                       // a long value ends inside this unit, at m (1 .. SC)
+        uint64_t m_ref = 0;                  // ... its tuple: a slot (m_abs) or a record index of the tile
+        bool m_abs = false;
         bool any_long = false;               // (uniform) some long value touches the tile
         bool out = false;                    // (uniform) a value crosses the tile end
-        uint64_t out_ve = 0;
-        uint32_t out_slot = 0;
-        auto consider = [&](int32_t vb, uint64_t ve_abs, uint32_t slot, bool from_carry) {
+        uint64_t out_ve = 0, out_ref = 0;
+        bool out_abs = false;
+        auto consider = [&](int32_t vb, uint64_t ve_abs, uint64_t ref, bool is_abs, bool from_carry) {
             const int64_t v64 = (int64_t)ve_abs - lo;
             const int32_t ver = v64 > FAR ? FAR : (int32_t)v64;
             if (vb < ue && ver > ue) { vx = true; a_off = vb >= us ? vb - us : -1; vx_carry = from_carry; }
-            if (vb < us && ver > us && ver <= ue) { m = ver - us; m_slot = slot; }
-            if (ver > TILE) { out = true; out_ve = ve_abs; out_slot = slot; }
+            if (vb < us && ver > us && ver <= ue) { m = ver - us; m_ref = ref; m_abs = is_abs; }
+            if (ver > TILE) { out = true; out_ve = ve_abs; out_ref = ref; out_abs = is_abs; }
             any_long = true;
         };
-        uint32_t n_carry = 0, n_idx = 0, n_state = 0;
-        uint64_t n_vb = 0, n_ve = 0;
-        if (carry == 1u) consider(-FAR, c_ve, c_idx, true);
+        uint32_t n_carry = 0;
+        uint64_t n_vb = 0, n_ve = 0, n_ref = 0;   // the next tile's carry (n_ref: a slot, or a record index)
+        bool n_abs = true;
+        if (carry == 1u) consider(-FAR, c_ve, c_slot, true, true);
         if (carry == 2u) {                   // a value whose record started in an earlier tile
-            if ((int64_t)c_vb - lo < TILE) consider((int32_t)((int64_t)c_vb - lo), c_ve, c_idx, false);
-            else { n_carry = 2; n_vb = c_vb; n_ve = c_ve; n_idx = c_idx; }   // still further on
+            if ((int64_t)c_vb - lo < TILE) consider((int32_t)((int64_t)c_vb - lo), c_ve, c_slot, true, false);
+            else { n_carry = 2; n_vb = c_vb; n_ve = c_ve; n_ref = c_slot; }   // still further on
         }
-        // pool slots: a tile's records take one contiguous run (k_compact reads them so); a tile
-        // holds at most TILE / 5 + 1 record starts
-        constexpr uint32_t TILE_RECS = TILE / 5 + 1;
-        if (walk && chunk_left < TILE_RECS) {
-            const uint64_t cm = pool_chunk > TILE_RECS ? pool_chunk : TILE_RECS;
-            unsigned long long b = 0;
-            if (lane == 0) {
-                b = atomicAdd(&ctr->pool_cursor, (unsigned long long)cm);
-                if (b + cm > pool_cap) atomicOr(&ctr->overflow, 1u);
-            }
-            chunk_base = uni64(b);
-            chunk_left = cm;
-        }
-        const uint64_t pool_base = chunk_base;
+        // pool slots: the tile's records take at most two runs, [b1, b1 + c1) then [b2, ...)
+        uint64_t b1 = 0, b2 = 0;
+        uint32_t c1 = N32;
         uint32_t nrec = 0, err_rec = N32;    // records emitted; index of the tile's first error
         if (walk) {
             int64_t p = (int64_t)entry - lo;
@@ -526,22 +577,22 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             if (KVR_ABLATE & 4) p = vhi_r;
 #pragma unroll 1
             while (p < vhi_r && !broke && err_rec == N32) {
-                // exact hops, a 256-B window per LDS round trip; lane j keeps record nrec + j
+                // exact hops; lane j keeps record nrec + j
                 uint32_t nb = 0, kmx = 0;
                 int32_t myrec = -1;
                 uint32_t my_op = 0, my_klen = 0, my_vlen = 0;
-                int wb = -4096;
-                uint32_t win = 0;
 #pragma unroll 1
                 while (p < vhi_r && nb < 64u) {
-                    const int pw = (int)(p >> 2);
-                    if (pw < wb || pw + 1 >= wb + 64) {
-                        wb = pw;
-                        win = wb + lane < WIN ? tw[wb + lane] : 0u;
+                    uint32_t op;
+                    uint64_t klen;
+                    if (p + 8 <= TILE) {
+                        const uint64_t x = tu64((int)p);
+                        op = (uint32_t)x & 255u;
+                        klen = (x >> 8) & 0xFFFFFFFFull;
+                    } else {
+                        op = uni32(ts.b8(p));
+                        klen = rem - p >= 5 ? uni32(ts.u32(p + 1)) : 0u;
                     }
-                    const uint64_t x = win64(win, pw - wb) >> (8u * (uint32_t)(p & 3));
-                    const uint32_t op = (uint32_t)x & 255u;
-                    const uint64_t klen = (x >> 8) & 0xFFFFFFFFull;
                     if (lane == (int)nb) { myrec = (int32_t)p; my_op = op; my_klen = (uint32_t)klen; }
                     ++nb;
                     const int64_t e = p + 5 + (int64_t)klen;
@@ -549,33 +600,43 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     kmx = (uint32_t)klen > kmx ? (uint32_t)klen : kmx;
                     if (op == 1u) { p = e; continue; }
                     if (rem - e < 4) { broke = true; break; }
-                    uint32_t vlen;
-                    if (e + 4 <= TILE + HALO) {
-                        const int ew = (int)(e >> 2);
-                        if (ew >= wb && ew + 1 < wb + 64) vlen = (uint32_t)(win64(win, ew - wb) >> (8u * (uint32_t)(e & 3)));
-                        else vlen = uni32(tv.lds_u32(e));
-                    } else {
-                        vlen = uni32(tv.rd32((uint64_t)(lo + e)));
-                    }
+                    const uint32_t vlen = e + 8 <= TILE ? (uint32_t)tu64((int)e) : uni32(ts.u32(e));
                     if (lane == (int)nb - 1) my_vlen = vlen;
-                    const int64_t e2 = e + 4 + (int64_t)vlen;
+                    const int64_t vb = e + 4, e2 = vb + (int64_t)vlen;
                     if (e2 > rem) { broke = true; break; }
+                    // a value longer than SMALL that crosses a unit boundary: fold it into every
+                    // unit's view (one inside a single unit is CRC'd by its record's lane)
+                    if (vlen > (uint32_t)SMALL && (vb >> SC_LOG) != ((e2 - 1) >> SC_LOG)) {
+                        const uint64_t idx = nrec + nb - 1;
+                        if (vb < TILE) consider((int32_t)vb, (uint64_t)(lo + e2), idx, false, false);
+                        else { n_carry = 2; n_vb = (uint64_t)(lo + vb); n_ve = (uint64_t)(lo + e2); n_ref = idx; n_abs = false; }
+                    }
                     p = e2;
                 }
                 KVR_STAMP(1);
+                // pool slots of the batch (one run: a fresh chunk holds any tile's rest)
+                if (nb > chunk_left) {
+                    const uint64_t cm = pool_chunk > TILE_RECS ? pool_chunk : TILE_RECS;
+                    unsigned long long bb = 0;
+                    if (lane == 0) {
+                        bb = atomicAdd(&ctr->pool_cursor, (unsigned long long)cm);
+                        if (bb + cm > pool_cap) atomicOr(&ctr->overflow, 1u);
+                    }
+                    chunk_base = uni64(bb);
+                    chunk_left = cm;
+                    if (nrec) { b2 = chunk_base; c1 = nrec; }   // the tile's second run
+                }
+                if (nrec == 0) b1 = chunk_base;
+                const uint64_t slot = chunk_base + (uint64_t)lane;
+                chunk_base += nb;
+                chunk_left -= nb;
                 // the batch's records: lane j emits record nrec + j
                 uint32_t rerr = N32, rkind = 0;
                 uint64_t raux = 0;
-                bool lng = false;            // its value is longer than SMALL and starts in the tile
-                int32_t l_b = 0;
-                uint64_t l_e = 0;
-                uint32_t hand = 0;           // ... or starts past the tile end
-                uint64_t pvb = 0, pve = 0;
                 const uint32_t j = nrec + (uint32_t)lane;
-                const uint64_t slot = pool_base + j;
                 if (!(KVR_ABLATE & 1) && myrec >= 0) {
                     if (broke && lane == (int)nb - 1) {   // the record that broke the chain: every check
-                        const RecRes r = do_record(tv, K, (uint64_t)(lo + myrec), j, slot, sd.seg, pool, pool_cap);
+                        const RecRes r = do_record(ts, K, myrec, j, slot, sd.seg, pool, pool_cap);
                         rerr = r.err; rkind = r.kind; raux = r.aux;
                         if (r.err == N32) { rerr = j; rkind = KVR_E_VAL; }   // defensive: a break is an error
                     } else {
@@ -583,37 +644,15 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                         const uint32_t nw = (kc + 3u) >> 2;   // key words of the longest fast-path key
                         const int kb = myrec + 5;
                         const uint32_t klen = my_klen;
-                        uint32_t c = ~0u;
-                        bool done = false;
-                        if (klen <= 4u * KEYW && kb + (int)klen + 4 <= TILE + HALO) {
-                            const int q = kb >> 2;
-                            const uint32_t sh = (uint32_t)kb & 3u;
-                            uint32_t r[KEYW + 1];
-#pragma unroll
-                            for (int i = 0; i <= KEYW; ++i) r[i] = (uint32_t)i <= nw ? tw[q + i] : 0u;
-                            uint32_t bad = 0, tail = 0;
-#pragma unroll
-                            for (int i = 0; i < KEYW; ++i) {
-                                if ((uint32_t)i < nw) {
-                                    const uint32_t kw = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
-                                    const uint32_t n = klen > 4u * i ? klen - 4u * i : 0u;
-                                    const uint32_t msk = n >= 4u ? ~0u : ((1u << (8 * n)) - 1u);
-                                    bad |= kw & msk & 0x80808080u;
-                                    const uint32_t cn = crc4(c, kw, K);
-                                    c = n >= 4u ? cn : c;
-                                    tail = (n > 0u && n < 4u) ? kw : tail;
-                                }
-                            }
-                            for (uint32_t bb = 0; bb < (klen & 3u); ++bb) c = crc1(c, (tail >> (8 * bb)) & 255u, K);
-                            done = bad == 0u;
-                        }
-                        if (!done) {                  // non-ASCII or long key: the full UTF-8 check
+                        uint32_t c = ~0u, bad = 0x80u;
+                        if (klen <= 4u * KEYW && kb + 4 * KEYW + 8 <= ts.lim) c = crc_span<KEYW>(ts, K, kb, klen, nw, &bad);
+                        if (bad != 0u) {              // non-ASCII or long key: the full UTF-8 check
                             uint64_t vu = 0;
                             uint32_t el = 0;
-                            if (!utf8_check(tv, (uint64_t)(lo + kb), klen, &vu, &el)) {   // engine.rs:114
+                            if (!utf8_check(ts, kb, klen, &vu, &el)) {   // engine.rs:114
                                 rerr = j; rkind = KVR_E_UTF8; raux = vu | ((uint64_t)el << 32);
                             } else {
-                                c = crc_range(tv, ~0u, (uint64_t)(lo + kb), klen, K);
+                                c = crc_long(ts, ~0u, kb, klen, K);
                             }
                         }
                         if (rerr == N32) {
@@ -628,14 +667,15 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                             t.flags = 0;
                             t.reserved = 0;
                             if (my_op == 0u) {
-                                const int64_t vb = (int64_t)kb + klen + 4;
                                 t.val_len = my_vlen;
+                                const int vb = kb + (int)klen + 4;
+                                uint32_t vbad;
                                 if (my_vlen <= (uint32_t)SMALL) {
-                                    t.crc32 = ~crc_range(tv, ~0u, (uint64_t)(lo + vb), my_vlen, K);
-                                } else if (vb < TILE) {
-                                    lng = true; l_b = (int32_t)vb; l_e = (uint64_t)(lo + vb) + my_vlen;
-                                } else {
-                                    hand = 2; pvb = (uint64_t)(lo + vb); pve = pvb + my_vlen;
+                                    if (vb + 4 * VALW + 8 <= ts.lim) t.crc32 = ~crc_span<VALW>(ts, K, vb, my_vlen, (uint32_t)VALW, &vbad);
+                                    else t.crc32 = ~crc_long(ts, ~0u, vb, my_vlen, K);
+                                } else if ((vb >> SC_LOG) == ((vb + (int)my_vlen - 1) >> SC_LOG)) {   // inside one unit
+                                    if (vb + 4 * UW + 8 <= ts.lim) t.crc32 = ~crc_span<UW>(ts, K, vb, my_vlen, (uint32_t)UW, &vbad);
+                                    else t.crc32 = ~crc_long(ts, ~0u, vb, my_vlen, K);
                                 }
                             }
                             if (slot < pool_cap) pool[slot] = t;
@@ -655,77 +695,58 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     const int el = (int)(err_rec - nrec);
                     err_kind = rl32(rkind, el);
                     err_aux = rl64(raux, el);
-                    err_pos = (uint64_t)(lo + (int64_t)rl32((uint32_t)myrec, el));
-                }
-                // the batch's long values before the error, folded into every unit's view
-#pragma unroll 1
-                for (unsigned long long mm = __ballot(lng && j < err_rec); mm; mm &= mm - 1ull) {
-                    const int l = __builtin_ctzll(mm);
-                    consider((int32_t)rl32((uint32_t)l_b, l), rl64(l_e, l), (uint32_t)(pool_base + nrec) + (uint32_t)l, false);
-                }
-                {   // a value starting past the tile end (the tile's last record): hand it over
-                    const unsigned long long bp = __ballot(hand == 2u && j < err_rec);
-                    if (bp) {
-                        const int ol = __builtin_ctzll(bp);
-                        n_carry = 2;
-                        n_vb = rl64(pvb, ol);
-                        n_ve = rl64(pve, ol);
-                        n_idx = (uint32_t)(pool_base + nrec) + (uint32_t)ol;
-                    }
+                    err_pos = (uint64_t)(lo + (int64_t)(int32_t)rl32((uint32_t)myrec, el));
                 }
                 nrec = err_rec != N32 ? err_rec : nrec + nb;
                 KVR_STAMP(7);
             }
             tile_exit = broke ? ERRP : (uint64_t)(lo + p);
         }
-        chunk_base += nrec;
-        chunk_left -= nrec;
-        wsync();
-        if (loaded) load_halo(abase, d0, len, k + 1, lane, W.tile);   // this tile's halo reads are done
+        if (c1 == N32) c1 = nrec;
+        // a record index of this tile -> its pool slot
+        auto slot_of = [&](uint64_t ref, bool is_abs) -> uint64_t {
+            return is_abs ? ref : (ref < c1 ? b1 + ref : b2 + (ref - c1));
+        };
+        if (n_carry == 2u && !n_abs) n_ref = slot_of(n_ref, false);
 
         KVR_STAMP(2);
         // ---- C. CRC of long values --------------------------------------------------------
         if (!(KVR_ABLATE & 2) && any_long) {
             KVR_STAMP(8);
-            // one pass over the unit (registers) gives both register pieces this lane owns:
-            //  - raw CRC of [0, m) (the value ending here), snapshotted on the way, and
-            //  - raw CRC of [a, 64) (the value crossing the unit end), restarting at a's word with
-            //    the bytes before a zeroed
-            const uint4 *up = reinterpret_cast<const uint4 *>(W.tile + lane * SC);   // this lane's unit
-            const uint4 v0 = up[0], v1 = up[1], v2 = up[2], v3 = up[3];
-            const uint32_t w[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
-                                    v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
+            // the unit's two halves, words 0..15 (A) and 16..31 (B), CRC'd as independent chains
+            // from a zero register, with the snapshot of the raw CRC of the unit's first 4 qm
+            // bytes (the value ending here) and the restart at the value starting here (a)
+            constexpr int H = UW / 2;
             const int qm = m >> 2;
             const int qa = (vx && a_off >= 0) ? (a_off >> 2) : -1;
             const uint32_t amask = ~0u << (8 * (a_off & 3));
-            // two independent chains, words 0..7 (A) and 8..15 (B), each from a zero register
             uint32_t ca = 0, cb = 0, sa = 0, sb = 0, wm = 0;
             if (!__ballot(m != 0 || qa >= 0)) {
 #pragma unroll
-                for (int kk = 0; kk < 8; ++kk) {
+                for (int kk = 0; kk < H; ++kk) {
                     ca = crc4(ca, w[kk], K);
-                    cb = crc4(cb, w[kk + 8], K);
+                    cb = crc4(cb, w[kk + H], K);
                 }
             } else {
 #pragma unroll
-                for (int kk = 0; kk < 8; ++kk) {
+                for (int kk = 0; kk < H; ++kk) {
                     sa = kk == qm ? ca : sa;
-                    sb = kk + 8 == qm ? cb : sb;
-                    wm = kk == qm ? w[kk] : (kk + 8 == qm ? w[kk + 8] : wm);
-                    const bool ra = kk == qa, rb = kk + 8 == qa;
+                    sb = kk + H == qm ? cb : sb;
+                    wm = kk == qm ? w[kk] : (kk + H == qm ? w[kk + H] : wm);
+                    const bool ra = kk == qa, rb = kk + H == qa;
                     ca = crc4(ra ? 0u : ca, ra ? (w[kk] & amask) : w[kk], K);
-                    cb = crc4(rb ? 0u : cb, rb ? (w[kk + 8] & amask) : w[kk + 8], K);
+                    cb = crc4(rb ? 0u : cb, rb ? (w[kk + H] & amask) : w[kk + H], K);
                 }
-                sa = qm == 8 ? ca : sa;
-                sb = qm == 16 ? cb : sb;
+                sa = qm == H ? ca : sa;
+                sb = qm == UW ? cb : sb;
             }
-            // the piece of the value crossing the unit end: A pushed through B's 32 bytes, then B
-            // (A does not count when that value starts in B's half); the raw CRC of the unit's
-            // first 4 qm bytes: A's snapshot, or all of A pushed through 4 (qm - 8) bytes, then B's
-            const uint32_t pa = kmul(ca, S.KQ + 128 * 8);
-            const uint32_t ps = kmul(ca, S.KQ + 128 * (qm > 8 ? qm - 8 : 0));
-            const uint32_t c = qa >= 8 ? cb : (pa ^ cb);
-            const uint32_t snap = qm <= 8 ? sa : (ps ^ sb);
+            // the piece of the value crossing the unit end: A pushed through B's bytes, then B
+            // (A does not count when that value starts in B's half); the raw CRC of the first
+            // 4 qm bytes: A's snapshot, or all of A pushed through 4 (qm - H) bytes, then B's
+            const uint32_t pa = kmul(ca, S.KQ + 128 * H);
+            const uint32_t ps = kmul(ca, S.KQ + 128 * (qm > H ? qm - H : 0));
+            const uint32_t c = qa >= H ? cb : (pa ^ cb);
+            const uint32_t snap = qm <= H ? sa : (ps ^ sb);
             KVR_STAMP(9);
             uint32_t v = 0, f = 1;               // segment start f: no inflow from the previous unit
             if (vx) {
@@ -733,7 +754,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                 else if (lane == 0 && vx_carry) v = c ^ kmul(c_state, S.KT);   // carried register across unit 0
                 else { v = c; f = 0; }
             }
-            // segmented scan: state at the end of unit l = f ? v : state(l-1) * x^(8*64) ^ v
+            // segmented scan: state at the end of unit l = f ? v : state(l-1) * x^(8*SC) ^ v
 #define KVR_SCAN_ROW(CTRL, D, KTAB)                                          \
             {                                                                \
                 const uint32_t ov = dpp<CTRL>(v), of = dpp<CTRL>(f);         \
@@ -772,13 +793,14 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     rp = crc1(rp, (wm >> (8 * b)) & 255u, K);
                     cf = crc1(cf, 0u, K);
                 }
-                if (m_slot < pool_cap) pool[m_slot].crc32 = ~(cf ^ rp);
+                const uint64_t ms = slot_of(m_ref, m_abs);
+                if (ms < pool_cap) pool[ms].crc32 = ~(cf ^ rp);
             }
             if (out) {                           // the value running past the tile: hand over its register
                 n_carry = 1;
-                n_state = rl32(v, 63);
+                c_state = rl32(v, 63);
                 n_ve = out_ve;
-                n_idx = out_slot;
+                n_ref = slot_of(out_ref, out_abs);
             }
         }
 
@@ -786,20 +808,22 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         // ---- bookkeeping ------------------------------------------------------------------
         if (in_stripe) {
             if (lane == 0) {
-                tres[sg.tile0 + k].pool_off = nrec ? pool_base : 0ull;
-                tres[sg.tile0 + k].count = nrec;
+                TileRes tr;
+                tr.pool_off = nrec ? b1 : 0ull;
+                tr.pool_off2 = b2;
+                tr.count = nrec;
+                tr.count1 = c1 < nrec ? c1 : nrec;
+                tres[sg.tile0 + k] = tr;
             }
             total += nrec;
             if (walk) entry = tile_exit;
         }
         carry = n_carry;
-        c_state = n_state;
-        c_vb = n_vb; c_ve = n_ve; c_idx = n_idx;
+        c_vb = n_vb; c_ve = n_ve; c_slot = n_ref;
         if (err_pos != NONE) stop = 1;
         else if (walk && tile_exit == ERRP) {   // defensive: a broken chain must have reported
             stop = 1; err_pos = entry; err_kind = KVR_E_VAL;
         }
-        wsync();
         KVR_STAMP(4);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain an unused prefetch before exit
@@ -810,8 +834,9 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     // tiles of the stripe that were never reached (error stop / pass-through) hold no tuples
     const uint32_t kfirst = k < sd.t_end ? k : sd.t_end;
     for (uint32_t kk = kfirst + lane; kk < sd.t_end; kk += 64) {
-        tres[sg.tile0 + kk].pool_off = 0;
-        tres[sg.tile0 + kk].count = 0;
+        TileRes tr;
+        tr.pool_off = 0; tr.pool_off2 = 0; tr.count = 0; tr.count1 = 0;
+        tres[sg.tile0 + kk] = tr;
     }
     if (lane == 0) {
         StripeRes r;
