@@ -36,6 +36,7 @@
  * and its address is a single v_perm_b32 of the register byte and the lane's constant.
  */
 #include "kvr_device.h"
+#include <type_traits>
 
 namespace kvr {
 
@@ -572,47 +573,61 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         uint32_t c1 = N32;
         uint32_t nrec = 0, err_rec = N32;    // records emitted; index of the tile's first error
         if (walk) {
+            // positions are tile-relative, in 32 bits unless the segment runs more than 2 GiB past
+            // the tile (then a 64-bit copy of the hop loop runs): the bounds checks stay scalar
+            const bool huge = rem > 0x7FFFFFFFll;
             int64_t p = (int64_t)entry - lo;
             bool broke = false;              // the chain broke at the last record walked
             if (KVR_ABLATE & 4) p = vhi_r;
 #pragma unroll 1
             while (p < vhi_r && !broke && err_rec == N32) {
-                // exact hops; lane j keeps record nrec + j
+                // exact hops; lane j keeps record nrec + j (per-lane selects)
                 uint32_t nb = 0, kmx = 0;
                 int32_t myrec = -1;
                 uint32_t my_op = 0, my_klen = 0, my_vlen = 0;
+                auto hops = [&](auto q) -> decltype(q) {
+                    using T = decltype(q);
+                    using U = std::make_unsigned_t<T>;
+                    const T remT = (T)rem, vhiT = (T)vhi_r;
 #pragma unroll 1
-                while (p < vhi_r && nb < 64u) {
-                    uint32_t op;
-                    uint64_t klen;
-                    if (p + 8 <= TILE) {
-                        const uint64_t x = tu64((int)p);
-                        op = (uint32_t)x & 255u;
-                        klen = (x >> 8) & 0xFFFFFFFFull;
-                    } else {
-                        op = uni32(ts.b8(p));
-                        klen = rem - p >= 5 ? uni32(ts.u32(p + 1)) : 0u;
+                    while (q < vhiT && nb < 64u) {
+                        uint32_t op, klen;
+                        if (q + 8 <= TILE) {
+                            const uint64_t x = tu64((int)q);
+                            op = (uint32_t)x & 255u;
+                            klen = (uint32_t)(x >> 8);
+                        } else {                     // the header crosses the tile end
+                            op = uni32(ts.b8(q));
+                            klen = remT - q >= 5 ? uni32(ts.u32(q + 1)) : 0u;
+                        }
+                        const bool me = lane == (int)nb;
+                        myrec = me ? (int32_t)q : myrec;
+                        my_op = me ? op : my_op;
+                        my_klen = me ? klen : my_klen;
+                        ++nb;
+                        if (op > 1u || remT - q < 5 || (U)klen > (U)(remT - q - 5)) { broke = true; break; }
+                        kmx = klen > kmx ? klen : kmx;
+                        const T e = q + 5 + (T)klen;
+                        if (op == 1u) { q = e; continue; }
+                        if (remT - e < 4) { broke = true; break; }
+                        const uint32_t vlen = e + 8 <= TILE ? (uint32_t)tu64((int)e) : uni32(ts.u32(e));
+                        my_vlen = lane == (int)nb - 1 ? vlen : my_vlen;
+                        const T vb = e + 4;
+                        if ((U)vlen > (U)(remT - vb)) { broke = true; break; }
+                        const T e2 = vb + (T)vlen;
+                        // a value longer than SMALL that crosses a unit boundary: fold it into every
+                        // unit's view (one inside a single unit is CRC'd by its record's lane)
+                        if (vlen > (uint32_t)SMALL && (vb >> SC_LOG) != ((e2 - 1) >> SC_LOG)) {
+                            const uint64_t idx = nrec + nb - 1;
+                            if (vb < TILE) consider((int32_t)vb, (uint64_t)(lo + e2), idx, false, false);
+                            else { n_carry = 2; n_vb = (uint64_t)(lo + vb); n_ve = (uint64_t)(lo + e2); n_ref = idx; n_abs = false; }
+                        }
+                        q = e2;
                     }
-                    if (lane == (int)nb) { myrec = (int32_t)p; my_op = op; my_klen = (uint32_t)klen; }
-                    ++nb;
-                    const int64_t e = p + 5 + (int64_t)klen;
-                    if (op > 1u || rem - p < 5 || e > rem) { broke = true; break; }
-                    kmx = (uint32_t)klen > kmx ? (uint32_t)klen : kmx;
-                    if (op == 1u) { p = e; continue; }
-                    if (rem - e < 4) { broke = true; break; }
-                    const uint32_t vlen = e + 8 <= TILE ? (uint32_t)tu64((int)e) : uni32(ts.u32(e));
-                    if (lane == (int)nb - 1) my_vlen = vlen;
-                    const int64_t vb = e + 4, e2 = vb + (int64_t)vlen;
-                    if (e2 > rem) { broke = true; break; }
-                    // a value longer than SMALL that crosses a unit boundary: fold it into every
-                    // unit's view (one inside a single unit is CRC'd by its record's lane)
-                    if (vlen > (uint32_t)SMALL && (vb >> SC_LOG) != ((e2 - 1) >> SC_LOG)) {
-                        const uint64_t idx = nrec + nb - 1;
-                        if (vb < TILE) consider((int32_t)vb, (uint64_t)(lo + e2), idx, false, false);
-                        else { n_carry = 2; n_vb = (uint64_t)(lo + vb); n_ve = (uint64_t)(lo + e2); n_ref = idx; n_abs = false; }
-                    }
-                    p = e2;
-                }
+                    return q;
+                };
+                if (huge) p = hops((int64_t)p);
+                else p = hops((int32_t)p);
                 KVR_STAMP(1);
                 // pool slots of the batch (one run: a fresh chunk holds any tile's rest)
                 if (nb > chunk_left) {
