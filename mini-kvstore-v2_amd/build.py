@@ -92,9 +92,34 @@ def build_ablate(masks=(0, 1, 2, 3, 7)):
     return out
 
 
+# experimental k_replay variants (tools/ablate.py <cfg> 0 <name>): timing only, not shipped
+VARIANTS = {
+    "rt768": ["-DKVR_RT=768"],
+}
+
+
+def build_variants(names=None):
+    out = os.path.join(LIB, "variants")
+    os.makedirs(out, exist_ok=True)
+    deps = _deps(*[f for f in os.listdir(CSRC) if f.endswith((".hip", ".h"))])
+    procs = []
+    for n in names or VARIANTS:
+        so = os.path.join(out, f"libkvreplay_{n}.so")
+        if _newer(so, deps):
+            procs.append(subprocess.Popen([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+                                           *VARIANTS[n], "-Wno-unused-result", "-o", so,
+                                           os.path.join(CSRC, "kvr_api.hip")]))
+    for p in procs:
+        if p.wait() != 0:
+            raise RuntimeError("variant build failed")
+    return out
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
     if "--prof" in sys.argv:
         print("built", build_prof())
     if "--ablate" in sys.argv:
         print("built", build_ablate())
+    if "--variants" in sys.argv:
+        print("built", build_variants())

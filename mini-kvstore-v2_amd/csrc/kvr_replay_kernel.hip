@@ -40,7 +40,14 @@
 
 namespace kvr {
 
-constexpr int RT = 768;                   // threads per workgroup: 12 stripes, one per wave
+// threads per workgroup: 16 stripes, one per wave.  The 32 tile registers leave room for four waves
+// per SIMD (126 VGPRs) when the next tile is loaded into the same registers once the current one is
+// done with (no separate prefetch buffer); that occupancy hides the load better than a full-tile
+// register prefetch at three waves (RT=768: 7% slower on cfg2)
+#ifndef KVR_RT
+#define KVR_RT 1024
+#endif
+constexpr int RT = KVR_RT;
 constexpr int WPB = RT / 64;              // stripes (waves) per workgroup
 constexpr int UW = SC / 4;                // dwords of a lane's unit
 constexpr int SC_LOG = 7;
@@ -114,13 +121,29 @@ __device__ __forceinline__ uint32_t tget(const Crc &k, uint32_t x, uint32_t sel)
 }
 // the register after the two bytes sitting in x's low half (x = register ^ data)
 // (both lookups are issued before either is used: the empty asm keeps the scheduler from
-// serialising them, which would cost a third LDS round trip per word)
+// serialising them, which would cost a third LDS round trip per word; it is not volatile, so
+// independent chains still interleave around it)
 __device__ __forceinline__ uint32_t crc2(const Crc &k, uint32_t x) {
     uint32_t t0 = tget(k, x, SEL_T1_B0), t1 = tget(k, x, SEL_T0_B1);
-    asm volatile("" : "+v"(t0), "+v"(t1));
+    asm("" : "+v"(t0), "+v"(t1));
     return (x >> 16) ^ t0 ^ t1;
 }
 __device__ __forceinline__ uint32_t crc4(uint32_t c, uint32_t w, const Crc &k) { return crc2(k, crc2(k, c ^ w)); }
+// two independent chains stepped together: their four lookups share one LDS round trip
+__device__ __forceinline__ void crc2x2(const Crc &k, uint32_t &xa, uint32_t &xb) {
+    uint32_t a0 = tget(k, xa, SEL_T1_B0), a1 = tget(k, xa, SEL_T0_B1);
+    uint32_t b0 = tget(k, xb, SEL_T1_B0), b1 = tget(k, xb, SEL_T0_B1);
+    asm("" : "+v"(a0), "+v"(a1), "+v"(b0), "+v"(b1));
+    xa = (xa >> 16) ^ a0 ^ a1;
+    xb = (xb >> 16) ^ b0 ^ b1;
+}
+__device__ __forceinline__ void crc4x2(uint32_t &ca, uint32_t wa, uint32_t &cb, uint32_t wb, const Crc &k) {
+    uint32_t xa = ca ^ wa, xb = cb ^ wb;
+    crc2x2(k, xa, xb);
+    crc2x2(k, xa, xb);
+    ca = xa;
+    cb = xb;
+}
 __device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
     const uint32_t x = c ^ b;
     return (x >> 8) ^ tget(k, x, SEL_T0_B0);
@@ -130,7 +153,7 @@ __device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
 // 16 entries sit in 16 banks and equal indices broadcast: conflict free).  The eight lookups
 // are independent: the empty asm makes the scheduler issue them all before the first use.
 __device__ __forceinline__ uint32_t xor8(uint32_t *t) {
-    asm volatile("" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]), "+v"(t[7]));
+    asm("" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]), "+v"(t[7]));
     return ((t[0] ^ t[1]) ^ (t[2] ^ t[3])) ^ ((t[4] ^ t[5]) ^ (t[6] ^ t[7]));
 }
 __device__ __forceinline__ uint32_t kmul(uint32_t v, const uint32_t *K) {
@@ -487,9 +510,8 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     uint32_t carry = 0, c_state = 0;              // 1: a long value crosses the tile start (c_state: its register);
     uint64_t c_vb = 0, c_ve = 0, c_slot = 0;      // 2: pending (its value starts in a later tile)
 
-    uint32_t nxt[UW];   // this lane's unit of the next tile (prefetch)
-    load_unit(abase, d0, len, sd.t_begin, lane, nxt);
-    bool loaded = true;
+    uint32_t w[UW];     // this lane's unit of the tile (the next tile's load is issued as soon as the
+    bool loaded = false;   // CRC phase is done with these registers, see the end of the loop body)
     uint32_t k = sd.t_begin;
 #ifdef KVR_PROF
     unsigned long long t_last = __builtin_amdgcn_s_memtime();
@@ -501,14 +523,10 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         const bool in_stripe = k < sd.t_end;
         if (stop || (!in_stripe && !carry) || k >= sg.n_tiles) break;
         if (!loaded) {
-            load_unit(abase, d0, len, k, lane, nxt);
+            load_unit(abase, d0, len, k, lane, w);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        uint32_t w[UW];                  // this tile's unit
-#pragma unroll
-        for (int i = 0; i < UW; ++i) w[i] = nxt[i];
-        loaded = (k + 1 < sg.n_tiles) && (k + 1 < sd.t_end || carry);
-        if (loaded) load_unit(abase, d0, len, k + 1, lane, nxt);
+        loaded = false;
 
         const int64_t lo = (int64_t)k * TILE - d0;      // segment position of tile byte 0
         const uint64_t vlo = lo < 0 ? 0ull : (uint64_t)lo;
@@ -738,10 +756,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             uint32_t ca = 0, cb = 0, sa = 0, sb = 0, wm = 0;
             if (!__ballot(m != 0 || qa >= 0)) {
 #pragma unroll
-                for (int kk = 0; kk < H; ++kk) {
-                    ca = crc4(ca, w[kk], K);
-                    cb = crc4(cb, w[kk + H], K);
-                }
+                for (int kk = 0; kk < H; ++kk) crc4x2(ca, w[kk], cb, w[kk + H], K);
             } else {
 #pragma unroll
                 for (int kk = 0; kk < H; ++kk) {
@@ -749,8 +764,9 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     sb = kk + H == qm ? cb : sb;
                     wm = kk == qm ? w[kk] : (kk + H == qm ? w[kk + H] : wm);
                     const bool ra = kk == qa, rb = kk + H == qa;
-                    ca = crc4(ra ? 0u : ca, ra ? (w[kk] & amask) : w[kk], K);
-                    cb = crc4(rb ? 0u : cb, rb ? (w[kk + H] & amask) : w[kk + H], K);
+                    ca = ra ? 0u : ca;
+                    cb = rb ? 0u : cb;
+                    crc4x2(ca, ra ? (w[kk] & amask) : w[kk], cb, rb ? (w[kk + H] & amask) : w[kk + H], K);
                 }
                 sa = qm == H ? ca : sa;
                 sb = qm == UW ? cb : sb;
@@ -819,6 +835,11 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             }
         }
 
+        // the tile's registers are dead from here on: the next tile's load overlaps the rest
+        if (err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry)) {
+            load_unit(abase, d0, len, k + 1, lane, w);
+            loaded = true;
+        }
         KVR_STAMP(3);
         // ---- bookkeeping ------------------------------------------------------------------
         if (in_stripe) {

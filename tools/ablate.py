@@ -23,10 +23,14 @@ if nseg_o:
     nseg = nseg_o
 spec = K.GenSpec(seed=0x6B767265706C6179 + int(cfg[3:]), seg_bytes=seg_bytes, **kw)
 P, U32, U64, SZ = C.c_void_p, C.c_uint32, C.c_uint64, C.c_size_t
-masks = [int(sys.argv[3])] if len(sys.argv) > 3 else sorted(
-    int(f[len("libkvreplay_a"):-3]) for f in os.listdir(ABL) if f.startswith("libkvreplay_a"))
+VAR = os.path.join(ROOT, "mini-kvstore-v2_amd", "lib", "variants")
+if len(sys.argv) > 3:   # a mask (lib/ablate) or a variant name (lib/variants, build.py VARIANTS)
+    masks = [int(sys.argv[3]) if sys.argv[3].isdigit() else sys.argv[3]]
+else:
+    masks = sorted(int(f[len("libkvreplay_a"):-3]) for f in os.listdir(ABL) if f.startswith("libkvreplay_a"))
 for mask in masks:
-    lib = C.CDLL(os.path.join(ABL, f"libkvreplay_a{mask}.so"))   # the only kvreplay library in this process
+    path = os.path.join(ABL, f"libkvreplay_a{mask}.so") if isinstance(mask, int) else os.path.join(VAR, f"libkvreplay_{mask}.so")
+    lib = C.CDLL(path)   # the only kvreplay library in this process
     lib.kvr_ctx_create.argtypes = [C.c_int, C.POINTER(P)]
     lib.kvr_replay.argtypes = [P, C.POINTER(K.Segment), SZ, U32, P, SZ, P, SZ, C.POINTER(SZ), C.POINTER(K.Error)]
     lib.kvr_last_stats.argtypes = [P, C.POINTER(K.Stats)]
@@ -63,5 +67,5 @@ for mask in masks:
         lib.kvr_last_stats(h, C.byref(st))
         ms.append(st.ms_replay)
     t = min(ms[1:])
-    print(f"{cfg} ablate={mask:2d} (1 records, 2 value CRC, 4 hops): rc={rc} n={n.value}/{nrec} k_replay {t:.3f} ms"
+    print(f"{cfg} ablate={mask!s:>6} (1 records, 2 value CRC, 4 hops): rc={rc} n={n.value}/{nrec} k_replay {t:.3f} ms"
           f"  {tot / t / 1e6:.1f} GB/s", flush=True)
