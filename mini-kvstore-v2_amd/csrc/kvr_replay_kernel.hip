@@ -73,8 +73,8 @@ struct __align__(16) Smem {
 };
 
 #ifndef KVR_ABLATE
-#define KVR_ABLATE 0   // diagnostic builds only: 1 skip records, 2 skip value CRC, 4 skip hops
-#endif
+#define KVR_ABLATE 0   // diagnostic builds only: 1 skip records, 2 skip value CRC, 4 skip hops,
+#endif                 // 8 skip the unit loop, 16 skip scan + finalize, 32 skip long-value folding
 
 #ifdef KVR_PROF
 __device__ unsigned long long g_prof[16];
@@ -152,21 +152,31 @@ __device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
 // register state v times a constant K (nibble tables; every lane reads table i at once, so the
 // 16 entries sit in 16 banks and equal indices broadcast: conflict free).  The eight lookups
 // are independent: the empty asm makes the scheduler issue them all before the first use.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {   // one VALU op
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));   // a ^ b ^ c
+    return r;
+}
 __device__ __forceinline__ uint32_t xor8(uint32_t *t) {
     asm("" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]), "+v"(t[7]));
-    return ((t[0] ^ t[1]) ^ (t[2] ^ t[3])) ^ ((t[4] ^ t[5]) ^ (t[6] ^ t[7]));
+    return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
 }
+// (the nibbles are split into two byte planes first: each index is then one byte extract)
 __device__ __forceinline__ uint32_t kmul(uint32_t v, const uint32_t *K) {
+    uint32_t pl[2] = {v & 0x0F0F0F0Fu, (v >> 4) & 0x0F0F0F0Fu};
+    asm("" : "+v"(pl[0]), "+v"(pl[1]));   // keep the planes (no re-fusion into nibble shifts)
     uint32_t t[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) t[i] = K[i * 16 + ((v >> (4 * i)) & 15u)];
+    for (int i = 0; i < 8; ++i) t[i] = K[i * 16 + ((pl[i & 1] >> (8 * (i >> 1))) & 255u)];
     return xor8(t);
 }
 // v times x^(8*SC*(k+1)), k per lane (column k of KR: bank k mod 32, conflict free)
 __device__ __forceinline__ uint32_t kmulr(uint32_t v, const uint32_t *KR, uint32_t k) {
+    uint32_t pl[2] = {v & 0x0F0F0F0Fu, (v >> 4) & 0x0F0F0F0Fu};
+    asm("" : "+v"(pl[0]), "+v"(pl[1]));   // keep the planes (no re-fusion into nibble shifts)
     uint32_t t[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) t[i] = KR[(i * 16 + ((v >> (4 * i)) & 15u)) * 32 + k];
+    for (int i = 0; i < 8; ++i) t[i] = KR[(i * 16 + ((pl[i & 1] >> (8 * (i >> 1))) & 255u)) * 32 + k];
     return xor8(t);
 }
 
@@ -637,7 +647,8 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                         // unit's view (one inside a single unit is CRC'd by its record's lane)
                         if (vlen > (uint32_t)SMALL && (vb >> SC_LOG) != ((e2 - 1) >> SC_LOG)) {
                             const uint64_t idx = nrec + nb - 1;
-                            if (vb < TILE) consider((int32_t)vb, (uint64_t)(lo + e2), idx, false, false);
+                            if (KVR_ABLATE & 32) any_long = true;
+                            else if (vb < TILE) consider((int32_t)vb, (uint64_t)(lo + e2), idx, false, false);
                             else { n_carry = 2; n_vb = (uint64_t)(lo + vb); n_ve = (uint64_t)(lo + e2); n_ref = idx; n_abs = false; }
                         }
                         q = e2;
@@ -754,7 +765,9 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             const int qa = (vx && a_off >= 0) ? (a_off >> 2) : -1;
             const uint32_t amask = ~0u << (8 * (a_off & 3));
             uint32_t ca = 0, cb = 0, sa = 0, sb = 0, wm = 0;
-            if (!__ballot(m != 0 || qa >= 0)) {
+            if (KVR_ABLATE & 8) {
+                ca = w[0]; cb = w[1];
+            } else if (!__ballot(m != 0 || qa >= 0)) {
 #pragma unroll
                 for (int kk = 0; kk < H; ++kk) crc4x2(ca, w[kk], cb, w[kk + H], K);
             } else {
@@ -794,6 +807,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                 v = ok ? (v ^ t_) : v;                                       \
                 f = ok ? of : f;                                             \
             }
+            if (!(KVR_ABLATE & 16)) {
             KVR_SCAN_ROW(0x111, 1, S.KT)
             KVR_SCAN_ROW(0x112, 2, S.KT + 128)
             KVR_SCAN_ROW(0x114, 4, S.KT + 256)
@@ -812,12 +826,13 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                 const bool ok = lane >= 32 && !f;
                 v = ok ? (v ^ t_) : v;
             }
+            }
             KVR_STAMP(10);
             uint32_t sin = dpp<0x138>(v);        // wave_shr:1: the state at this unit's start
             if (lane == 0) sin = c_state;
             // the value ending in this unit at m: its register is sin * x^(8m) ^ raw[0, m)
             // (the x^(8m) push: a constant table for 4q bytes + r zero bytes)
-            if (m != 0) {
+            if (!(KVR_ABLATE & 16) && m != 0) {
                 const int r = m & 3;
                 uint32_t rp = snap, cf = kmul(sin, S.KQ + 128 * qm);
                 for (int b = 0; b < r; ++b) {

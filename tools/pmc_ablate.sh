@@ -6,7 +6,7 @@ set -o pipefail
 OUT=$(mkdir -p "$1" && cd "$1" && pwd); shift
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd /tmp && export TMPDIR=/tmp
-for m in ${*:-0 1 2 3}; do
+for m in ${*:-0 1 2 3 8 16 32}; do
   timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVES SQ_INSTS_VMEM \
     --output-format csv -d "$OUT/a$m" -o pmc -- python "$R/tools/ablate.py" cfg2 0 $m > "$OUT/a$m.log" 2>&1 || { echo "variant $m failed"; tail -5 "$OUT/a$m.log"; exit 1; }
 done
