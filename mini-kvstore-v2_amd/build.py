@@ -74,7 +74,7 @@ def build_prof():
     return out
 
 
-def build_ablate(masks=(0, 1, 2, 3, 7, 8, 16, 32)):
+def build_ablate(masks=(0, 1, 2, 3, 7, 8, 16, 32, 64)):
     """Diagnostic variants with parts of k_replay switched off (tools/ablate.py); not shipped."""
     out = os.path.join(LIB, "ablate")
     os.makedirs(out, exist_ok=True)

@@ -41,7 +41,7 @@
 namespace kvr {
 
 // threads per workgroup: 16 stripes, one per wave.  The 32 tile registers leave room for four waves
-// per SIMD (126 VGPRs) when the next tile is loaded into the same registers once the current one is
+// per SIMD (under 128 VGPRs) when the next tile is loaded into the same registers once the current one is
 // done with (no separate prefetch buffer); that occupancy hides the load better than a full-tile
 // register prefetch at three waves (RT=768: 7% slower on cfg2)
 #ifndef KVR_RT
@@ -74,7 +74,8 @@ struct __align__(16) Smem {
 
 #ifndef KVR_ABLATE
 #define KVR_ABLATE 0   // diagnostic builds only: 1 skip records, 2 skip value CRC, 4 skip hops,
-#endif                 // 8 skip the unit loop, 16 skip scan + finalize, 32 skip long-value folding
+#endif                 // 8 skip the unit loop, 16 skip scan + finalize, 32 skip long-value folding,
+                       // 64 loads only
 
 #ifdef KVR_PROF
 __device__ unsigned long long g_prof[16];
@@ -537,6 +538,15 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         loaded = false;
+        if (KVR_ABLATE & 64) {   // loads only (FETCH_SIZE calibration on a known byte count)
+            uint32_t x = 0;
+#pragma unroll
+            for (int i = 0; i < UW; ++i) x ^= w[i];
+            if (x == 0x9E3779B9u && lane == 0) atomicOr(&ctr->overflow, 8u);   // keeps the loads alive
+            if (in_stripe) total += 0;
+            carry = 0;
+            continue;
+        }
 
         const int64_t lo = (int64_t)k * TILE - d0;      // segment position of tile byte 0
         const uint64_t vlo = lo < 0 ? 0ull : (uint64_t)lo;
@@ -764,7 +774,10 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             const int qm = m >> 2;
             const int qa = (vx && a_off >= 0) ? (a_off >> 2) : -1;
             const uint32_t amask = ~0u << (8 * (a_off & 3));
-            uint32_t ca = 0, cb = 0, sa = 0, sb = 0, wm = 0;
+            // (one compare per step: q & 15 picks the step, a loop-invariant lane mask the chain)
+            const int qh = qm & (H - 1), qah = qa >= 0 ? (qa & (H - 1)) : -1;
+            const bool mb = qm >= H, ab = qa >= H;
+            uint32_t ca = 0, cb = 0, sn = 0, wm = 0;
             if (KVR_ABLATE & 8) {
                 ca = w[0]; cb = w[1];
             } else if (!__ballot(m != 0 || qa >= 0)) {
@@ -773,16 +786,15 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             } else {
 #pragma unroll
                 for (int kk = 0; kk < H; ++kk) {
-                    sa = kk == qm ? ca : sa;
-                    sb = kk + H == qm ? cb : sb;
-                    wm = kk == qm ? w[kk] : (kk + H == qm ? w[kk + H] : wm);
-                    const bool ra = kk == qa, rb = kk + H == qa;
+                    const bool s_ = kk == qh;
+                    sn = s_ ? (mb ? cb : ca) : sn;
+                    wm = s_ ? (mb ? w[kk + H] : w[kk]) : wm;   // (not re-read from memory: its line has left L2)
+                    const bool r = kk == qah, ra = r && !ab, rb = r && ab;
                     ca = ra ? 0u : ca;
                     cb = rb ? 0u : cb;
                     crc4x2(ca, ra ? (w[kk] & amask) : w[kk], cb, rb ? (w[kk + H] & amask) : w[kk + H], K);
                 }
-                sa = qm == H ? ca : sa;
-                sb = qm == UW ? cb : sb;
+                sn = qm == UW ? cb : sn;
             }
             // the piece of the value crossing the unit end: A pushed through B's bytes, then B
             // (A does not count when that value starts in B's half); the raw CRC of the first
@@ -790,7 +802,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             const uint32_t pa = kmul(ca, S.KQ + 128 * H);
             const uint32_t ps = kmul(ca, S.KQ + 128 * (qm > H ? qm - H : 0));
             const uint32_t c = qa >= H ? cb : (pa ^ cb);
-            const uint32_t snap = qm <= H ? sa : (ps ^ sb);
+            const uint32_t snap = qm < H ? sn : (ps ^ sn);
             KVR_STAMP(9);
             uint32_t v = 0, f = 1;               // segment start f: no inflow from the previous unit
             if (vx) {

@@ -3,7 +3,7 @@
 #   parity tests, the bench line, the rocprofv3 kernel-trace summary of the same bench command,
 #   the per-phase cycle breakdown, ablation timings and PMC counters.  Every GPU step has its
 #   own time limit and the steps are chained, so the first failure ends the batch.
-#   usage: tools/gpu_measure.sh <tag> [tests bench bench3 bench5 prof phases ablate pmc ...]
+#   usage: tools/gpu_measure.sh <tag> [tests bench bench3 bench5 prof phases ablate traffic pmc ...]
 set -o pipefail
 TAG=${1:-run}; shift
 STEPS=${*:-tests bench prof}
@@ -39,6 +39,9 @@ for s in $STEPS; do
         timeout -k 10 120 python -u tools/ablate.py cfg2 0 $m >> "$OUT/ablate_cfg2.txt" 2>&1 || { echo "ablate failed"; tail -20 "$OUT/ablate_cfg2.txt"; exit 1; }
       done
       cat "$OUT/ablate_cfg2.txt" ;;
+    traffic)
+      timeout -k 10 600 python -u tools/pmc_traffic.py > "$OUT/traffic.log" 2>&1 || { echo "traffic failed"; tail -20 "$OUT/traffic.log"; exit 1; }
+      cp gpurun_out/pmc_traffic.json "$OUT/pmc_traffic.json" && tail -1 "$OUT/traffic.log" ;;
     pmc)
       timeout -k 10 900 bash tools/pmc.sh "$OUT/pmc" --no-cpu --steps 2 --warmup 1 > "$OUT/pmc.txt" 2>&1 || { echo "pmc failed"; tail -20 "$OUT/pmc.txt"; exit 1; }
       cat "$OUT/pmc.txt" ;;
