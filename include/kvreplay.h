@@ -144,6 +144,35 @@ uint32_t kvr_crc32(uint32_t crc, const uint8_t *data, size_t len);
  * error.rs:11) for err and the segment's path.  Returns the length written (snprintf rules). */
 int  kvr_format_error(const kvr_error *err, const char *path, char *buf, size_t cap);
 
+/* ---- live-record rewrite (compaction) -------------------------------------------------
+ * The intended KVStore::compact (README.md:283-287: "collect all live keys, write to new
+ * segments, delete old segments"; the reference's compaction.rs:9-29 deletes the files without
+ * rewriting anything).  Replays segs (ascending seg_id, as kvr_replay), keeps every
+ * key's final SET (last writer in (segment, offset) order, engine.rs:137 / :141) and writes those
+ * records, byte for byte (the framing of engine.rs:169-173), in (segment, offset) order into out
+ * as consecutive new segments.  A new segment starts at the first record whose offset in out is
+ * >= k * seg_target (k = 1, 2, ...): segments exceed seg_target by less than one record;
+ * seg_target 0 = one segment.  A reference replay of the new segments rebuilds the same map.
+ *   out (host, or device with KVR_OUT_ON_DEVICE) receives *out_len bytes; seg_ends[j] = end
+ *   offset in out of new segment j, *n_out_segs of them (0 when nothing is live).
+ * Returns KVR_OK, KVR_CORRUPTED (*err: the first replay error, as kvr_replay; nothing written),
+ * KVR_CAPACITY (out_cap < *out_len or seg_cap < *n_out_segs; both set to what is required) or
+ * < 0. */
+typedef struct kvr_compact_stats {
+    double   ms_replay;     /* the replay pipeline (device time)                              */
+    double   ms_fold;       /* last-writer fold, live flags, scans, dense live list           */
+    double   ms_gather;     /* byte gather of the live records                                */
+    uint64_t n_tuples;      /* records replayed                                               */
+    uint64_t n_live;        /* records written                                                */
+    uint64_t bytes_in;      /* segment bytes replayed                                         */
+    uint64_t bytes_out;     /* bytes written                                                  */
+} kvr_compact_stats;
+
+int  kvr_compact(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint32_t flags, uint64_t seg_target,
+                 uint8_t *out, uint64_t out_cap, uint64_t *out_len, uint64_t *seg_ends, size_t seg_cap,
+                 size_t *n_out_segs, kvr_error *err);
+int  kvr_last_compact_stats(const kvr_ctx *ctx, kvr_compact_stats *out);
+
 /* ---- synthetic segment generator (device side; byte-identical to kvh_gen_segment) -------- */
 typedef struct kvr_gen_params {
     uint64_t seed;

@@ -6,7 +6,7 @@
  *   kvh_gen_segment   synthetic segments, framing writer  engine.rs:157-198 (byte-identical to
  *                     kvr_gen_segment_device)
  *   kvh_fold          last-writer-wins index fold         engine.rs:137 (insert), :141 (remove)
- *   kvs_open / kvs_get / kvs_stats / kvs_close
+ *   kvs_open / kvs_get / kvs_stats / kvs_compact / kvs_close
  *                     the crate-public KVStore surface the replay path feeds (lib.rs:2-3,
  *                     engine.rs:24, :200, :232-259); the index has the shape of the reference's
  *                     dead `Index` (src/store/index.rs:7): key -> (segment, offset, length).
@@ -65,6 +65,15 @@ int kvs_get(const kvs_store *s, const uint8_t *key, size_t klen, const uint8_t *
 /* Index entry (index.rs:7 shape): segment id, value offset inside that segment file, length. */
 int kvs_locate(const kvs_store *s, const uint8_t *key, size_t klen, uint64_t *seg_id, uint64_t *val_off, uint64_t *len);
 int kvs_stats_get(const kvs_store *s, kvs_stats *out);
+/* KVStore::compact (engine.rs:262-266 -> compaction.rs:9-29) with the intended semantics of
+ * README.md:283-287 (the reference deletes every segment without rewriting a key):
+ * kvr_compact rewrites the live records into new files segment-<active+1>.dat, ... (segments
+ * of about seg_target bytes, 0 = one file), written and fsync'd before every other
+ * segment-*.dat is removed (compaction.rs:11-23); then a fresh empty active segment is created
+ * (reset_active_segment, engine.rs:209-229) and the index is rebuilt over the new files.  A crash
+ * between the writes and the removals leaves old and new files, whose replay gives the same map.
+ * Returns KVR_OK, KVR_CORRUPTED (*err) or < 0 (KVR_EIO: a file could not be written/removed). */
+int kvs_compact(kvs_store *s, kvr_ctx *ctx, uint64_t seg_target, kvr_error *err);
 /* KVStore::list_keys: up to cap keys as (offset, length) pairs into the returned arena. */
 size_t kvs_num_keys(const kvs_store *s);
 void kvs_close(kvs_store *s);

@@ -16,8 +16,11 @@
 #include <cstring>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "kvr_replay_kernel.hip"
 #include "kvr_kernels.hip"
+#include "kvr_compact.hip"
 
 using namespace kvr;
 
@@ -63,6 +66,12 @@ struct kvr_ctx {
     DevBuf<uint64_t> bsum;
     DevBuf<uint32_t> crc, kmul, initx;
     DevBuf<GenRecDev> gen;
+    // compaction (kvr_compact)
+    DevBuf<kvr_tuple> ctup;
+    DevBuf<uint32_t> ht_rep, ht_best, cslot, cflag, cpos, cfirst;
+    DevBuf<uint64_t> csize, coff, l_src, l_off, ctot, ccuts;
+    DevBuf<uint8_t> cout, ctmp;
+    kvr_compact_stats cstats{};
     LinkResult *h_link = nullptr;
     Counters *h_ctr = nullptr;
     std::vector<SegDesc> h_segs;
@@ -214,6 +223,9 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->pool.release(); c->dense.release(); c->redo.release(); c->link.release(); c->ctr.release();
     c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->bsum.release();
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
+    c->ctup.release(); c->ht_rep.release(); c->ht_best.release(); c->cslot.release(); c->cflag.release();
+    c->cpos.release(); c->cfirst.release(); c->csize.release(); c->coff.release(); c->l_src.release();
+    c->l_off.release(); c->ctot.release(); c->ccuts.release(); c->cout.release(); c->ctmp.release();
     if (c->h_link) (void)hipHostFree(c->h_link);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
@@ -485,6 +497,129 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         return total > cap ? KVR_CAPACITY : KVR_OK;
     }
     return KVR_ENOMEM;
+}
+
+// ---------------------------------------------------------------------------------------
+// live-record rewrite (kvr_compact.hip): replay -> fold -> live list -> gather -> cuts
+// ---------------------------------------------------------------------------------------
+int kvr_compact(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, uint64_t seg_target, uint8_t *out,
+                uint64_t out_cap, uint64_t *out_len, uint64_t *seg_ends, size_t seg_cap, size_t *n_out_segs,
+                kvr_error *err) {
+    if (!c || (!segs && n) || !out_len || !n_out_segs || (out_cap && !out) || (seg_cap && !seg_ends)) return KVR_EINVAL;
+    *out_len = 0;
+    *n_out_segs = 0;
+    memset(&c->cstats, 0, sizeof(c->cstats));
+    if (err) memset(err, 0, sizeof(*err));
+    if (n == 0) return KVR_OK;
+    uint64_t bytes_in = 0;
+    for (size_t i = 0; i < n; ++i) bytes_in += segs[i].len;
+    c->cstats.bytes_in = bytes_in;
+
+    // 1. replay into context-resident tuples; the segment bytes stay in HBM (c->segs)
+    size_t nt = 0;
+    if (c->ctup.ensure(bytes_in / 64 + 1024)) return KVR_ENOMEM;
+    const uint32_t rflags = (flags & KVR_SEGS_ON_DEVICE) | KVR_OUT_ON_DEVICE;
+    int rc = kvr_replay(c, segs, n, rflags, nullptr, 0, c->ctup.p, c->ctup.n, &nt, err);
+    if (rc == KVR_CAPACITY) {
+        if (c->ctup.ensure(nt)) return KVR_ENOMEM;
+        rc = kvr_replay(c, segs, n, rflags, nullptr, 0, c->ctup.p, c->ctup.n, &nt, err);
+    }
+    if (rc != KVR_OK) return rc;
+    c->cstats.ms_replay = c->stats.ms_total;
+    c->cstats.n_tuples = nt;
+    if (nt == 0) return KVR_OK;
+    if (nt >= 0x7FFFFFFFull) return KVR_EINVAL;   // 32-bit tuple indices in the fold table
+    hipStream_t st = c->stream;
+
+    // 2. fold: the key's last tuple, live flags and sizes, scans, dense live list
+    uint64_t slots = 1;
+    while (slots < 2 * (uint64_t)nt) slots <<= 1;
+    if (c->ht_rep.ensure(slots) || c->ht_best.ensure(slots) || c->cslot.ensure(nt) || c->cflag.ensure(nt) ||
+        c->cpos.ensure(nt) || c->csize.ensure(nt) || c->coff.ensure(nt) || c->l_src.ensure(nt) ||
+        c->l_off.ensure(nt + 1) || c->ctot.ensure(2))
+        return KVR_ENOMEM;
+    size_t t1 = 0, t2 = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, c->csize.p, c->coff.p, (int)nt, st));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, c->cflag.p, c->cpos.p, (int)nt, st));
+    if (c->ctmp.ensure(std::max(t1, t2))) return KVR_ENOMEM;
+    const uint32_t g = (uint32_t)((nt + 255) / 256);
+    HIPCHK(hipEventRecord(c->ev[0], st));
+    HIPCHK(hipMemsetAsync(c->ht_rep.p, 0xFF, slots * 4, st));
+    HIPCHK(hipMemsetAsync(c->ht_best.p, 0, slots * 4, st));
+    hipLaunchKernelGGL(k_fold_insert, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p, c->ht_rep.p,
+                       c->ht_best.p, (uint32_t)(slots - 1), c->cslot.p);
+    hipLaunchKernelGGL(k_live, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->ht_best.p, c->cslot.p, c->csize.p,
+                       c->cflag.p);
+    HIPCHK(hipGetLastError());
+    size_t tb = c->ctmp.n;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->csize.p, c->coff.p, (int)nt, st));
+    tb = c->ctmp.n;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->cflag.p, c->cpos.p, (int)nt, st));
+    hipLaunchKernelGGL(k_ctotals, dim3(1), dim3(64), 0, st, c->csize.p, c->coff.p, c->cflag.p, c->cpos.p, (uint64_t)nt,
+                       c->l_off.p, c->ctot.p);
+    HIPCHK(hipGetLastError());
+    uint64_t tot[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(tot, c->ctot.p, sizeof(tot), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint64_t total = tot[0], n_live = tot[1];
+    c->cstats.n_live = n_live;
+    c->cstats.bytes_out = total;
+    const uint64_t n_blocks = (total + CBLK - 1) / CBLK;
+    if (c->cfirst.ensure(n_blocks)) return KVR_ENOMEM;
+    hipLaunchKernelGGL(k_scatter, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p, c->csize.p, c->coff.p,
+                       c->cflag.p, c->cpos.p, c->l_src.p, c->l_off.p, c->cfirst.p);
+    HIPCHK(hipGetLastError());
+
+    // 3. new-segment boundaries (cuts at the first record at or after k * seg_target)
+    std::vector<uint64_t> ends;
+    if (total) {
+        if (seg_target && total > seg_target) {
+            const uint64_t n_cuts = (total - 1) / seg_target;
+            if (c->ccuts.ensure(n_cuts)) return KVR_ENOMEM;
+            hipLaunchKernelGGL(k_cuts, dim3((uint32_t)((n_cuts + 255) / 256)), dim3(256), 0, st, c->l_off.p, c->ctot.p,
+                               seg_target, n_cuts, c->ccuts.p);
+            HIPCHK(hipGetLastError());
+            std::vector<uint64_t> cuts(n_cuts);
+            HIPCHK(hipMemcpyAsync(cuts.data(), c->ccuts.p, n_cuts * 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            for (uint64_t v : cuts)
+                if (v < total && (ends.empty() || v > ends.back())) ends.push_back(v);
+        }
+        ends.push_back(total);
+    }
+    HIPCHK(hipEventRecord(c->ev[1], st));
+    *out_len = total;
+    *n_out_segs = ends.size();
+    if (total > out_cap || ends.size() > seg_cap) {
+        HIPCHK(hipStreamSynchronize(st));
+        return KVR_CAPACITY;
+    }
+    for (size_t j = 0; j < ends.size(); ++j) seg_ends[j] = ends[j];
+    if (!total) return KVR_OK;
+
+    // 4. gather (straight into a device output when it is 8-B aligned, else through staging)
+    uint8_t *d_out = out;
+    const bool direct = (flags & KVR_OUT_ON_DEVICE) && !(reinterpret_cast<uintptr_t>(out) & 7u);
+    if (!direct) {
+        if (c->cout.ensure(total + 8)) return KVR_ENOMEM;
+        d_out = c->cout.p;
+    }
+    hipLaunchKernelGGL(k_gather, dim3((uint32_t)((n_blocks + CT_GATHER / 64 - 1) / (CT_GATHER / 64))), dim3(CT_GATHER), 0,
+                       st, c->l_src.p, c->l_off.p, c->cfirst.p, c->ctot.p, n_blocks, d_out);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[2], st));
+    if (!direct)
+        HIPCHK(hipMemcpyAsync(out, d_out, total, (flags & KVR_OUT_ON_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    c->cstats.ms_fold = ev_ms(c->ev[0], c->ev[1]);
+    c->cstats.ms_gather = ev_ms(c->ev[1], c->ev[2]);
+    return KVR_OK;
+}
+
+int kvr_last_compact_stats(const kvr_ctx *c, kvr_compact_stats *out) {
+    if (!c || !out) return KVR_EINVAL;
+    *out = c->cstats;
+    return KVR_OK;
 }
 
 // diagnostic build only (-DKVR_PROF): per-phase cycle sums of k_replay's tile loop

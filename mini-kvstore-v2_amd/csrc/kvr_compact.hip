@@ -1,0 +1,207 @@
+/*
+ * kvr_compact.hip — the live-record rewrite (BASELINE config 4).
+ *
+ * What the reference's compaction is meant to do (README.md:283-287: "collect all live keys,
+ * write to new segments, delete old segments"); its compaction.rs:9-29 only deletes the files
+ * (SURVEY R3).  Parity target: a reference replay (engine.rs:79-154) of the new segments
+ * reproduces the pre-compaction map (tests/store_integration.rs:22-31, now across a reopen).
+ *
+ * Input: the replay tuples of the store (kvr_replay, in (segment, offset) order) and the
+ * segment bytes in HBM.  Device pipeline, one stream:
+ *   k_fold_insert   every tuple into an open-addressing table keyed by its key bytes
+ *                   (key_tag = CRC-32 of the key as the hash): atomicCAS claims an empty slot
+ *                   for the key's first tuple, atomicMax keeps the key's LAST tuple index — the
+ *                   last-writer-wins fold of engine.rs:137 / :141 as an associative max
+ *   k_live          a tuple is live iff it is a SET and its key's last tuple: size 9 + k + v
+ *   (scan)          exclusive sums of sizes (output offsets) and live flags (dense index)
+ *   k_scatter       dense live list (source address, output offset) and, for every 512-B
+ *                   output block, the live record holding its first byte
+ *   k_gather        one wave per 512-B output block: 8 B per lane, the lane's record found by
+ *                   a 6-step binary search over the wave's record ends (DPP/bpermute), the
+ *                   bytes copied verbatim (the framing of engine.rs:169-173 is the record's own)
+ *   k_cuts          new-segment boundaries: a segment starts at the first live record whose
+ *                   output offset is >= k * seg_target
+ * Bytes moved (the roofline): live bytes read + live bytes written + 32 B per
+ * tuple of the fold; HBM-bound.
+ */
+#ifndef KVR_COMPACT_HIP
+#define KVR_COMPACT_HIP
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kvr_device.h"
+
+namespace kvr {
+
+constexpr uint32_t HT_EMPTY = 0xFFFFFFFFu;
+constexpr int CBLK = 512;            // output bytes per gather wave (8 B per lane)
+constexpr int CBLK_LOG = 9;
+static_assert(CBLK == 1 << CBLK_LOG, "block size");
+constexpr int CT_GATHER = 256;       // threads per gather workgroup (4 blocks)
+
+__device__ __forceinline__ uint32_t ht_mix(uint32_t h) {   // the key_tag is a CRC: spread it
+    h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
+    return h;
+}
+
+__device__ __forceinline__ const uint8_t *key_ptr(const SegDesc *segs, const kvr_tuple &t) {
+    return segs[t.seg_idx].base + t.rec_off + 5;   // [op][klen u32][key] (engine.rs:169-171)
+}
+
+// key bytes equal (the tags and lengths are compared first)
+__device__ bool key_eq(const SegDesc *segs, const kvr_tuple &a, const kvr_tuple &b) {
+    if (a.key_tag != b.key_tag || a.key_len != b.key_len) return false;
+    const uint8_t *pa = key_ptr(segs, a), *pb = key_ptr(segs, b);
+    for (uint32_t i = 0; i < a.key_len; ++i)
+        if (pa[i] != pb[i]) return false;
+    return true;
+}
+
+// the table: rep[h] = the key's first tuple (HT_EMPTY: free), best[h] = 1 + the key's last
+// tuple (0: none); mask + 1 slots, at least 2 n
+__global__ void k_fold_insert(const kvr_tuple *__restrict__ tup, uint64_t n, const SegDesc *__restrict__ segs,
+                              uint32_t *__restrict__ rep, uint32_t *__restrict__ best, uint32_t mask,
+                              uint32_t *__restrict__ slot) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const kvr_tuple t = tup[i];
+    uint32_t h = ht_mix(t.key_tag) & mask;
+    for (uint32_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+        uint32_t r = __hip_atomic_load(&rep[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (r == HT_EMPTY) {
+            r = atomicCAS(&rep[h], HT_EMPTY, (uint32_t)i);
+            if (r == HT_EMPTY) r = (uint32_t)i;   // claimed: this tuple represents the key
+        }
+        if (r == (uint32_t)i || key_eq(segs, tup[r], t)) {
+            atomicMax(&best[h], (uint32_t)i + 1u);
+            slot[i] = h;
+            return;
+        }
+    }
+    slot[i] = HT_EMPTY;   // unreachable: the table has at least n empty slots
+}
+
+// live flag and output size of every tuple
+__global__ void k_live(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ best,
+                       const uint32_t *__restrict__ slot, uint64_t *__restrict__ size, uint32_t *__restrict__ flag) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const kvr_tuple t = tup[i];
+    const uint32_t s = slot[i];
+    const bool live = t.op == 0 && s != HT_EMPTY && best[s] == (uint32_t)i + 1u;
+    size[i] = live ? 9ull + t.key_len + t.val_len : 0ull;   // SET framing, engine.rs:169-173
+    flag[i] = live ? 1u : 0u;
+}
+
+// totals: live bytes, live records, and the end sentinel of the dense offsets
+__global__ void k_ctotals(const uint64_t *__restrict__ size, const uint64_t *__restrict__ off,
+                          const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos, uint64_t n,
+                          uint64_t *__restrict__ l_off, uint64_t *__restrict__ totals) {
+    if (threadIdx.x || blockIdx.x) return;
+    const uint64_t bytes = n ? off[n - 1] + size[n - 1] : 0;
+    const uint64_t live = n ? (uint64_t)pos[n - 1] + flag[n - 1] : 0;
+    l_off[live] = bytes;
+    totals[0] = bytes;
+    totals[1] = live;
+}
+
+// dense live list + the first live record of every output block
+__global__ void k_scatter(const kvr_tuple *__restrict__ tup, uint64_t n, const SegDesc *__restrict__ segs,
+                          const uint64_t *__restrict__ size, const uint64_t *__restrict__ off,
+                          const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
+                          uint64_t *__restrict__ l_src, uint64_t *__restrict__ l_off, uint32_t *__restrict__ first) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !flag[i]) return;
+    const kvr_tuple t = tup[i];
+    const uint32_t j = pos[i];
+    const uint64_t s = off[i], e = s + size[i];
+    l_src[j] = reinterpret_cast<uint64_t>(segs[t.seg_idx].base + t.rec_off);
+    l_off[j] = s;
+    for (uint64_t b = (s + CBLK - 1) >> CBLK_LOG; (b << CBLK_LOG) < e; ++b) first[b] = j;
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, l, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// one wave per 512-B output block; lane l writes output bytes [b*512 + 8l, + 8)
+__global__ void __launch_bounds__(CT_GATHER) k_gather(const uint64_t *__restrict__ l_src, const uint64_t *__restrict__ l_off,
+                                                      const uint32_t *__restrict__ first, const uint64_t *__restrict__ totals,
+                                                      uint64_t n_blocks, uint8_t *__restrict__ out) {
+    const uint64_t b = (uint64_t)blockIdx.x * (CT_GATHER / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (b >= n_blocks) return;   // wave-uniform
+    const uint64_t total = totals[0];
+    const uint32_t n_live = (uint32_t)totals[1];
+    const uint32_t j0 = first[b];
+    // lane l: the end of live record j0 + l (records are >= 10 B: at most 52 start in a block)
+    const uint32_t jl = j0 + (uint32_t)lane;
+    const uint64_t e = jl < n_live ? l_off[jl + 1] : ~0ull;
+    const uint64_t x = (b << CBLK_LOG) + 8u * (uint32_t)lane;
+    int c = 0;   // live records of the wave ending at or before x
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1) {
+        const uint64_t ev = shfl64(e, c + step - 1);
+        if (ev <= x) c += step;
+    }
+    const uint64_t ej = shfl64(e, c);
+    if (x >= total) return;
+    uint32_t j = j0 + (uint32_t)c;
+    uint64_t sj = l_off[j];
+    uint64_t src = l_src[j] + (x - sj);
+    uint32_t lo, hi;
+    if (ej - x >= 8) {   // the lane's 8 bytes lie in one record: aligned dword reads + funnel shifts
+        const uint32_t *a = reinterpret_cast<const uint32_t *>(src & ~3ull);
+        const uint32_t sh = (uint32_t)src & 3u;
+        const uint32_t w0 = a[0], w1 = a[1], w2 = sh ? a[2] : 0u;   // a[2] holds byte src + 7 when sh != 0
+        lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    } else {             // the lane's bytes span records: byte by byte
+        uint64_t ejj = ej;
+        src = l_src[j];   // record base (bytes are indexed by output offset - record start)
+        uint8_t by[8];
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t xq = x + q;
+            if (xq >= total) { by[q] = 0; continue; }
+            while (xq >= ejj) {
+                ++j;
+                sj = ejj;
+                src = l_src[j];
+                ejj = l_off[j + 1];
+            }
+            by[q] = reinterpret_cast<const uint8_t *>(src)[xq - sj];
+        }
+        lo = by[0] | (by[1] << 8) | (by[2] << 16) | ((uint32_t)by[3] << 24);
+        hi = by[4] | (by[5] << 8) | (by[6] << 16) | ((uint32_t)by[7] << 24);
+    }
+    if (x + 8 <= total) {
+        uint2 v;
+        v.x = lo;
+        v.y = hi;
+        *reinterpret_cast<uint2 *>(out + x) = v;   // out is 8-B aligned (the host stages otherwise)
+    } else {
+        const uint64_t m = total - x;
+        for (uint64_t q = 0; q < m; ++q) out[x + q] = (uint8_t)((q < 4 ? lo >> (8 * q) : hi >> (8 * (q - 4))) & 255u);
+    }
+}
+
+// cut k (k = 1 .. n_cuts): the output offset of the first live record at or after k * target
+__global__ void k_cuts(const uint64_t *__restrict__ l_off, const uint64_t *__restrict__ totals, uint64_t target,
+                       uint64_t n_cuts, uint64_t *__restrict__ cuts) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_cuts) return;
+    const uint64_t want = (k + 1) * target;
+    uint64_t lo = 0, hi = totals[1];   // lower_bound over l_off[0, n_live)
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (l_off[mid] < want) lo = mid + 1;
+        else hi = mid;
+    }
+    cuts[k] = l_off[lo];   // l_off[n_live] = total
+}
+
+}  // namespace kvr
+
+#endif

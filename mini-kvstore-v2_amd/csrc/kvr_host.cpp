@@ -222,6 +222,62 @@ static int read_file(const std::string &path, std::vector<uint8_t> &out, int *os
     return 0;
 }
 
+// replay the store's resident segments on ctx's GPU and fold the index (engine.rs:53-57, :137, :141)
+static int build_index(kvs_store *s, kvr_ctx *ctx, kvr_error *err, char *msg, size_t msg_cap,
+                       const std::vector<std::string> *paths) {
+    const size_t n = s->ids.size();
+    s->index.clear();
+    s->total_bytes = 0;
+    std::vector<kvr_segment> segs(n);
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        segs[i] = kvr_segment{s->ids[i], s->bytes[i].data(), s->bytes[i].size()};
+        total += s->bytes[i].size();
+    }
+    std::vector<kvr_tuple> tuples(std::max<size_t>(16, total / 64));
+    size_t nt = 0;
+    kvr_error e{};
+    int rc = n ? kvr_replay(ctx, segs.data(), n, 0, nullptr, 0, tuples.data(), tuples.size(), &nt, &e) : KVR_OK;
+    if (rc == KVR_CAPACITY) {
+        tuples.resize(nt);
+        rc = kvr_replay(ctx, segs.data(), n, 0, nullptr, 0, tuples.data(), tuples.size(), &nt, &e);
+    }
+    if (rc == KVR_CORRUPTED) {
+        if (err) *err = e;
+        if (msg && paths) kvr_format_error(&e, (*paths)[e.seg_idx].c_str(), msg, msg_cap);
+        return rc;
+    }
+    if (rc != KVR_OK) return rc;
+    s->index.reserve(nt / 2 + 16);
+    for (size_t i = 0; i < nt; ++i) {   // last-writer-wins fold (engine.rs:137, :141)
+        const kvr_tuple &t = tuples[i];
+        const KeyRef k{segs[t.seg_idx].bytes + t.rec_off + 5, t.key_len, t.key_tag};
+        if (t.op == 0) s->index[k] = kvs_store::Ent{t.seg_idx, t.rec_off + 9 + t.key_len, t.val_len};
+        else s->index.erase(k);
+    }
+    for (const auto &kv : s->index) s->total_bytes += kv.second.len;
+    return KVR_OK;
+}
+
+static bool is_segment_name(const char *name) {   // compaction.rs:41-43
+    const size_t n = strlen(name);
+    return n >= 12 && memcmp(name, "segment-", 8) == 0 && memcmp(name + n - 4, ".dat", 4) == 0;
+}
+
+static int write_file_sync(const std::string &path, const uint8_t *p, size_t n) {
+    const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) return -1;
+    size_t o = 0;
+    while (o < n) {
+        const ssize_t w = write(fd, p + o, n - o);
+        if (w < 0) { if (errno == EINTR) continue; close(fd); return -1; }
+        o += (size_t)w;
+    }
+    const int rc = fsync(fd);
+    close(fd);
+    return rc;
+}
+
 int kvs_open(const char *dir, kvr_ctx *ctx, kvs_store **out, kvr_error *err, char *msg, size_t msg_cap) {
     if (!dir || !ctx || !out) return KVR_EINVAL;
     *out = nullptr;
@@ -252,35 +308,9 @@ int kvs_open(const char *dir, kvr_ctx *ctx, kvs_store **out, kvr_error *err, cha
             return KVR_CORRUPTED;
         }
     }
-    std::vector<kvr_segment> segs(n);
-    uint64_t total = 0;
-    for (size_t i = 0; i < n; ++i) {
-        segs[i] = kvr_segment{ids[i], s->bytes[i].data(), s->bytes[i].size()};
-        total += s->bytes[i].size();
-    }
-    std::vector<kvr_tuple> tuples(std::max<size_t>(16, total / 64));
-    size_t nt = 0;
-    kvr_error e{};
-    rc = kvr_replay(ctx, segs.data(), n, 0, nullptr, 0, tuples.data(), tuples.size(), &nt, &e);
-    if (rc == KVR_CAPACITY) {
-        tuples.resize(nt);
-        rc = kvr_replay(ctx, segs.data(), n, 0, nullptr, 0, tuples.data(), tuples.size(), &nt, &e);
-    }
-    if (rc == KVR_CORRUPTED) {
-        if (err) *err = e;
-        if (msg) kvr_format_error(&e, paths[e.seg_idx].c_str(), msg, msg_cap);
-        delete s;
-        return rc;
-    }
+    std::vector<std::string> *pp = &paths;
+    rc = build_index(s, ctx, err, msg, msg_cap, pp);
     if (rc != KVR_OK) { delete s; return rc; }
-    s->index.reserve(nt / 2 + 16);
-    for (size_t i = 0; i < nt; ++i) {   // last-writer-wins fold (engine.rs:137, :141)
-        const kvr_tuple &t = tuples[i];
-        const KeyRef k{segs[t.seg_idx].bytes + t.rec_off + 5, t.key_len, t.key_tag};
-        if (t.op == 0) s->index[k] = kvs_store::Ent{t.seg_idx, t.rec_off + 9 + t.key_len, t.val_len};
-        else s->index.erase(k);
-    }
-    for (const auto &kv : s->index) s->total_bytes += kv.second.len;
     // engine.rs:59-68: next id = max + 1, create the (empty) active segment for appends
     s->active_id = (n ? ids[n - 1] : 0) + 1;
     const std::string ap = std::string(dir) + "/segment-" + std::to_string(s->active_id) + ".dat";
@@ -332,6 +362,71 @@ int kvs_stats_get(const kvs_store *s, kvs_stats *out) {
 }
 
 size_t kvs_num_keys(const kvs_store *s) { return s ? s->index.size() : 0; }
+
+int kvs_compact(kvs_store *s, kvr_ctx *ctx, uint64_t seg_target, kvr_error *err) {
+    if (!s || !ctx) return KVR_EINVAL;
+    if (err) memset(err, 0, sizeof(*err));
+    const size_t n = s->ids.size();
+    std::vector<kvr_segment> segs(n);
+    uint64_t bytes_in = 0;
+    for (size_t i = 0; i < n; ++i) {
+        segs[i] = kvr_segment{s->ids[i], s->bytes[i].data(), s->bytes[i].size()};
+        bytes_in += s->bytes[i].size();
+    }
+    // 1. the live records, re-framed into new segments, on the GPU
+    std::vector<uint8_t> out(std::max<uint64_t>(bytes_in, 1));
+    std::vector<uint64_t> ends(seg_target ? bytes_in / seg_target + 2 : 1);
+    uint64_t out_len = 0;
+    size_t n_new = 0;
+    int rc = KVR_OK;
+    if (n) {
+        rc = kvr_compact(ctx, segs.data(), n, 0, seg_target, out.data(), out.size(), &out_len, ends.data(),
+                         ends.size(), &n_new, err);
+        if (rc == KVR_CAPACITY) {
+            out.resize(out_len);
+            ends.resize(n_new);
+            rc = kvr_compact(ctx, segs.data(), n, 0, seg_target, out.data(), out.size(), &out_len, ends.data(),
+                             ends.size(), &n_new, err);
+        }
+        if (rc != KVR_OK) return rc;
+    }
+    // 2. new files first (ids after the active segment), durable before anything is removed
+    std::vector<uint64_t> new_ids(n_new);
+    std::vector<std::vector<uint8_t>> new_bytes(n_new);
+    std::vector<std::string> new_names(n_new);
+    uint64_t prev = 0;
+    for (size_t j = 0; j < n_new; ++j) {
+        new_ids[j] = s->active_id + 1 + j;
+        new_names[j] = "segment-" + std::to_string(new_ids[j]) + ".dat";
+        new_bytes[j].assign(out.begin() + (ptrdiff_t)prev, out.begin() + (ptrdiff_t)ends[j]);
+        if (write_file_sync(s->dir + "/" + new_names[j], new_bytes[j].data(), new_bytes[j].size()) != 0) return KVR_EIO;
+        prev = ends[j];
+    }
+    // 3. every other segment-*.dat goes (compaction.rs:11-23; NotFound is not an error)
+    if (DIR *d = opendir(s->dir.c_str())) {
+        std::vector<std::string> victims;
+        while (struct dirent *e = readdir(d)) {
+            if (!is_segment_name(e->d_name)) continue;
+            if (std::find(new_names.begin(), new_names.end(), std::string(e->d_name)) != new_names.end()) continue;
+            victims.push_back(s->dir + "/" + e->d_name);
+        }
+        closedir(d);
+        for (const auto &v : victims)
+            if (unlink(v.c_str()) != 0 && errno != ENOENT) return KVR_EIO;
+    } else {
+        return KVR_EIO;
+    }
+    // 4. reset_active_segment (engine.rs:209-229): the next id, an empty file
+    s->active_id = s->active_id + n_new + 1;
+    const std::string ap = s->dir + "/segment-" + std::to_string(s->active_id) + ".dat";
+    const int fd = open(ap.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
+    if (fd < 0) return KVR_EIO;
+    close(fd);
+    // 5. the store now reads the new files; the index is rebuilt over them (same map)
+    s->ids = new_ids;
+    s->bytes = std::move(new_bytes);
+    return build_index(s, ctx, err, nullptr, 0, nullptr);
+}
 
 void kvs_close(kvs_store *s) { delete s; }
 

@@ -61,6 +61,12 @@ class StoreStats(C.Structure):
                 ("active_segment_id", C.c_uint64), ("oldest_segment_id", C.c_uint64)]
 
 
+class CompactStats(C.Structure):
+    _fields_ = [("ms_replay", C.c_double), ("ms_fold", C.c_double), ("ms_gather", C.c_double),
+                ("n_tuples", C.c_uint64), ("n_live", C.c_uint64), ("bytes_in", C.c_uint64),
+                ("bytes_out", C.c_uint64)]
+
+
 # ---- library loading ---------------------------------------------------------------------------
 _rep = None
 _host = None
@@ -88,6 +94,9 @@ def _load():
     rep.kvr_ctx_set_tiles_per_stripe.argtypes = [P, U32]
     rep.kvr_replay.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
     rep.kvr_last_stats.argtypes = [P, C.POINTER(Stats)]
+    rep.kvr_compact.argtypes = [P, C.POINTER(Segment), SZ, U32, U64, P, U64, C.POINTER(U64), P, SZ, C.POINTER(SZ),
+                                C.POINTER(Error)]
+    rep.kvr_last_compact_stats.argtypes = [P, C.POINTER(CompactStats)]
     rep.kvr_strerror.argtypes = [I]
     rep.kvr_strerror.restype = C.c_char_p
     rep.kvr_crc32.argtypes = [U32, P, SZ]
@@ -106,6 +115,7 @@ def _load():
     host.kvs_stats_get.argtypes = [P, C.POINTER(StoreStats)]
     host.kvs_num_keys.argtypes = [P]
     host.kvs_num_keys.restype = SZ
+    host.kvs_compact.argtypes = [P, P, U64, C.POINTER(Error)]
     host.kvs_close.argtypes = [P]
     host.kvs_close.restype = None
     _rep, _host = rep, host
@@ -224,6 +234,20 @@ class ReplayResult:
     stats: Stats
 
 
+class CompactResult:
+    def __init__(self, status, data, seg_ends, out_len, n_segs, error, stats):
+        self.status, self.data, self.seg_ends, self.out_len, self.n_segs = status, data, seg_ends, out_len, n_segs
+        self.error, self.stats = error, stats
+
+    def segments(self):
+        """The new segment files' bytes (host output)."""
+        out, s = [], 0
+        for e in self.seg_ends:
+            out.append(self.data[s:e])
+            s = e
+        return out
+
+
 class Context:
     """One kvr_ctx on one HIP device."""
 
@@ -308,6 +332,50 @@ class Context:
         tuples = out_arr[: n_out.value] if out_arr is not None and rc == OK else None
         return ReplayResult(rc, tuples, n_out.value, err if rc == CORRUPTED else None, self.last_stats())
 
+    def _segments(self, segments, seg_ids, on_device):
+        keep, n = [], len(segments)
+        segs = (Segment * max(n, 1))()
+        total = 0
+        for i, s in enumerate(segments):
+            sid = seg_ids[i] if seg_ids is not None else i
+            if on_device:
+                ptr, ln = s
+            else:
+                a = np.frombuffer(s, dtype=np.uint8) if isinstance(s, (bytes, bytearray)) else np.ascontiguousarray(s)
+                keep.append(a)
+                ptr, ln = (a.ctypes.data if a.size else None), a.size
+            segs[i] = Segment(sid, ptr, ln)
+            total += ln
+        return segs, keep, total
+
+    def compact(self, segments, seg_target=0, seg_ids=None, on_device=False, out_ptr=None, out_cap=0):
+        """Live-record rewrite (kvr_compact).  Returns CompactResult: data (bytes, host output)
+        unless out_ptr (device memory of out_cap bytes) is given; seg_ends = end offsets of the
+        new segments in the output."""
+        segs, keep, total = self._segments(segments, seg_ids, on_device)
+        flags = SEGS_ON_DEVICE if on_device else 0
+        out_arr = None
+        if out_ptr is not None:
+            flags |= OUT_ON_DEVICE
+            outp, cap = out_ptr, out_cap
+        else:
+            cap = max(total, 1)
+            out_arr = np.zeros(cap, dtype=np.uint8)
+            outp = out_arr.ctypes.data
+        n_ends = (total // seg_target + 2) if seg_target else 1
+        ends = np.zeros(n_ends, dtype=np.uint64)
+        out_len, n_segs = C.c_uint64(), C.c_size_t()
+        err = Error()
+        rc = self._rep.kvr_compact(self.h, segs, len(segments), flags, seg_target, outp, cap, C.byref(out_len),
+                                   ends.ctypes.data, ends.size, C.byref(n_segs), C.byref(err))
+        if rc < 0:
+            raise NativeError(f"kvr_compact: {self._rep.kvr_strerror(rc).decode()} ({rc})")
+        st = CompactStats()
+        self._rep.kvr_last_compact_stats(self.h, C.byref(st))
+        data = out_arr[: out_len.value].tobytes() if out_arr is not None and rc == OK else None
+        return CompactResult(rc, data, [int(x) for x in ends[: n_segs.value]] if rc == OK else [], out_len.value,
+                             n_segs.value, err if rc == CORRUPTED else None, st)
+
     def gen_segment_device(self, spec: GenSpec, seg_no: int, d_buf: int, cap: int, d_expected=None,
                            exp_cap=0):
         p = spec.c()
@@ -372,6 +440,16 @@ class KVStore:
         s = StoreStats()
         self._host.kvs_stats_get(self._h, C.byref(s))
         return s
+
+    def compact(self, seg_target: int = 0):
+        """KVStore::compact with the intended semantics (README.md:283-287): live records are
+        rewritten into new segment files, the old ones removed, the index rebuilt over them."""
+        err = Error()
+        rc = self._host.kvs_compact(self._h, self._ctx.h, seg_target, C.byref(err))
+        if rc == CORRUPTED:
+            raise CorruptedData(err.kind, err.seg_idx, err.rec_off, err.aux)
+        if rc != OK:
+            raise NativeError(f"kvs_compact: {rc}")
 
     def close(self):
         if self._h:

@@ -241,6 +241,58 @@ size_t oracle_fold_live(const oracle_seg *segs, const kvr_tuple *t, size_t n, ui
 }
 
 /* ------------------------------------------------------------------------------------------
+ * oracle_compact — the intended KVStore::compact (README.md:283-287: "collect all live keys,
+ * write to new segments, delete old segments"; the reference's compaction.rs:9-29 deletes the
+ * files without rewriting a key).  Replay (engine.rs:79-154), keep each key's final
+ * SET (oracle_fold_live: engine.rs:137 / :141), copy those records byte for byte in tuple order
+ * (a record's own bytes are its engine.rs:169-173 framing).  A new segment starts at the first
+ * record whose output offset is >= k * seg_target, k = 1, 2, ...; seg_target 0 = one segment.
+ * seg_ends[j] = end offset of segment j.  Returns KVR_OK, KVR_CORRUPTED (*err), KVR_CAPACITY
+ * (*out_len, *n_out_segs = required) or KVR_ENOMEM.
+ * ---------------------------------------------------------------------------------------- */
+int oracle_compact(const oracle_seg *segs, size_t n_segs, uint64_t seg_target, uint8_t *out, uint64_t out_cap,
+                   uint64_t *out_len, uint64_t *seg_ends, size_t seg_cap, size_t *n_out_segs, kvr_error *err) {
+    *out_len = 0;
+    *n_out_segs = 0;
+    uint64_t total_in = 0;
+    for (size_t i = 0; i < n_segs; ++i) total_in += segs[i].len;
+    size_t cap = (size_t)(total_in / 5 + 16), nt = 0;
+    kvr_tuple *t = (kvr_tuple *)malloc(cap * sizeof(kvr_tuple));
+    uint8_t *live = (uint8_t *)malloc(cap + 1);
+    if (!t || !live) { free(t); free(live); return KVR_ENOMEM; }
+    int rc = oracle_replay(segs, n_segs, NULL, 0, t, cap, &nt, err);
+    if (rc != KVR_OK) { free(t); free(live); return rc; }
+    oracle_fold_live(segs, t, nt, live, NULL);
+    /* output offsets of the live records, then the cuts */
+    uint64_t total = 0;
+    for (size_t i = 0; i < nt; ++i)
+        if (live[i]) total += 9ull + t[i].key_len + t[i].val_len;
+    size_t nseg = 0;
+    uint64_t next_cut = seg_target, pos = 0;
+    int over = total > out_cap;
+    for (size_t i = 0; i < nt; ++i) {
+        if (!live[i]) continue;
+        const uint64_t sz = 9ull + t[i].key_len + t[i].val_len;
+        if (seg_target && pos >= next_cut && pos > 0) {      /* this record starts a new segment */
+            if (nseg < seg_cap) seg_ends[nseg] = pos;
+            ++nseg;
+            while (next_cut <= pos) next_cut += seg_target;  /* every k with k * T <= pos is served */
+        }
+        if (!over) memcpy(out + pos, segs[t[i].seg_idx].bytes + t[i].rec_off, sz);
+        pos += sz;
+    }
+    if (total) {
+        if (nseg < seg_cap) seg_ends[nseg] = total;
+        ++nseg;
+    }
+    free(t);
+    free(live);
+    *out_len = total;
+    *n_out_segs = nseg;
+    return (over || nseg > seg_cap) ? KVR_CAPACITY : KVR_OK;
+}
+
+/* ------------------------------------------------------------------------------------------
  * oracle_replay_faithful — the CPU baseline: the reference's replay cost model, single thread.
  * Reads through an 8 KiB buffered reader (engine.rs:83; large reads bypass the buffer as
  * std's BufReader does), allocates the key and the value per record (engine.rs:106, :129),

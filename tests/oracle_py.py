@@ -36,6 +36,9 @@ def lib():
                                     C.POINTER(C.c_size_t), C.POINTER(Error)]
         L.oracle_fold_live.argtypes = [C.POINTER(OSeg), C.c_void_p, C.c_size_t, C.c_void_p, C.POINTER(C.c_uint64)]
         L.oracle_fold_live.restype = C.c_size_t
+        L.oracle_compact.argtypes = [C.POINTER(OSeg), C.c_size_t, C.c_uint64, C.c_void_p, C.c_uint64,
+                                     C.POINTER(C.c_uint64), C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t),
+                                     C.POINTER(Error)]
         L.oracle_replay_faithful.argtypes = [C.POINTER(OSeg), C.c_size_t, C.POINTER(C.c_uint64),
                                              C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                              C.POINTER(Error)]
@@ -103,3 +106,27 @@ def replay_faithful(segments):
     rc = lib().oracle_replay_faithful(segs, len(arrs), C.byref(nk), C.byref(tb), C.byref(nr), C.byref(dg),
                                       C.byref(err))
     return rc, nk.value, tb.value, nr.value, dg.value, err
+
+
+def compact(segments, seg_target=0, seg_ids=None):
+    """The intended compaction (oracle_compact). -> (rc, bytes, [segment end offsets], Error)"""
+    arrs, segs = _segs(segments, seg_ids)
+    n, ns = C.c_uint64(), C.c_size_t()
+    err = Error()
+    rc = lib().oracle_compact(segs, len(arrs), seg_target, None, 0, C.byref(n), None, 0, C.byref(ns), C.byref(err))
+    if rc != 2:   # KVR_CAPACITY is the sizing answer
+        return rc, b"", [], err
+    out = np.zeros(max(n.value, 1), dtype=np.uint8)
+    ends = np.zeros(max(ns.value, 1), dtype=np.uint64)
+    rc = lib().oracle_compact(segs, len(arrs), seg_target, out.ctypes.data, out.size, C.byref(n), ends.ctypes.data,
+                              ends.size, C.byref(ns), C.byref(err))
+    return rc, out[: n.value].tobytes(), [int(x) for x in ends[: ns.value]], err
+
+
+def split_segments(data, ends):
+    """The new segment files of a compaction output."""
+    out, s = [], 0
+    for e in ends:
+        out.append(data[s:e])
+        s = e
+    return out
