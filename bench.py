@@ -9,6 +9,10 @@ verify + ordered tuples left in HBM.  Weak scaling: rank r replays its own 64 se
 only for the barrier and the max-over-ranks timing).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5]
+  python bench.py --mode compact     the compaction live-record rewrite on
+                                     cfg4's per-GPU shard (50 % DEL): one step = one kvr_compact
+                                     (replay + last-writer fold + gather of the live records into
+                                     new segments), input and output resident in HBM; 1 GPU
 """
 import argparse
 import json
@@ -40,11 +44,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="cfg2", choices=list(CONFIGS))
+    ap.add_argument("--config", default=None, choices=list(CONFIGS))
+    ap.add_argument("--mode", default="replay", choices=["replay", "compact"])
     ap.add_argument("--segments", type=int, default=0, help="override segments per GPU")
     ap.add_argument("--cpu-segs", type=int, default=16, help="CPU baseline sample (segments)")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
+    if args.config is None:
+        args.config = "cfg4" if args.mode == "compact" else "cfg2"
 
     import numpy as np
     import torch
@@ -87,6 +94,8 @@ def main():
     segs = [(data.data_ptr() + o, ln) for (ln, _), o in zip(sizes, offs)]
     seg_total = sum(ln for ln, _ in sizes)
     out = torch.empty((n_rec + 1024) * 32, dtype=torch.uint8, device=dev)
+    if args.mode == "compact":
+        return bench_compact(args, ctx, segs, seg_nos, seg_total, n_rec, desc, nseg, seg_bytes, world)
 
     def step():
         r = ctx.replay(segs, seg_ids=seg_nos, expected=(manifest.data_ptr(), n_rec), expected_on_device=True,
@@ -182,6 +191,62 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_compact(args, ctx, segs, seg_nos, seg_total, n_rec, desc, nseg, seg_bytes, world):
+    """kvr_compact over the rank's shard, in and out of HBM.  Per step: the replay pipeline, the
+    fold (hash insert, live flags, scans, dense list) and the gather of the live records."""
+    import numpy as np
+    import torch
+    import kvreplay as K
+    if world > 1:
+        raise SystemExit("--mode compact runs on one GPU: a sharded store needs the cross-rank fold "
+                         "(DESIGN.md §9), not a per-shard one")
+    target = 64 << 20
+    out = torch.empty(seg_total + 4096, dtype=torch.uint8, device="cuda")
+
+    def step():
+        r = ctx.compact(segs, target, seg_ids=seg_nos, on_device=True, out_ptr=out.data_ptr(), out_cap=out.numel())
+        if r.status != 0:
+            raise RuntimeError(f"compact failed: status {r.status}")
+        return r
+
+    for _ in range(args.warmup):
+        r = step()
+    # self-check (size-independent): the new segments replay cleanly to exactly the live records
+    starts = [0] + r.seg_ends[:-1]
+    new = [(out.data_ptr() + a, b - a) for a, b in zip(starts, r.seg_ends)]
+    rr = ctx.replay(new, on_device=True)
+    assert rr.status == 0 and rr.n == r.stats.n_live, (rr.status, rr.n, r.stats.n_live)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st = []
+    for _ in range(args.steps):
+        r = step()
+        st.append((r.stats.ms_replay, r.stats.ms_fold, r.stats.ms_gather))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ms_rep, ms_fold, ms_gat = (float(np.mean([x[i] for x in st])) for i in range(3))
+    live_bytes, n_live = r.stats.bytes_out, r.stats.n_live
+    gather_bytes = 2 * live_bytes                       # live records read once + written once
+    achieved = gather_bytes / (ms_gat / 1e3) / 1e9
+    res = {
+        "metric": "device-resident compaction live-record rewrite GiB/s (segment bytes in)",
+        "value": round(seg_total * args.steps / dt / 2 ** 30, 3), "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (device generator, seeded)",
+        "config": {"workload": f"{args.config}: {desc}, device-resident, compaction into ~64 MiB segments",
+                   "segments_per_gpu": nseg, "segment_bytes": seg_bytes, "bytes_per_gpu": seg_total,
+                   "records_per_gpu": n_rec, "live_records": n_live, "live_bytes": live_bytes,
+                   "new_segments": len(r.seg_ends), "parallelism": "1 GPU"},
+        "ms_replay": round(ms_rep, 4), "ms_fold": round(ms_fold, 4), "ms_gather": round(ms_gat, 4),
+        "roofline": {"bound": "hbm", "kernel": "k_gather", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                     "alg_bytes_per_launch": gather_bytes},
+    }
+    print(json.dumps(res))
+    ctx.close()
 
 
 if __name__ == "__main__":

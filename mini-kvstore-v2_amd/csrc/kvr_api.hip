@@ -558,61 +558,61 @@ int kvr_compact(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, u
     hipLaunchKernelGGL(k_ctotals, dim3(1), dim3(64), 0, st, c->csize.p, c->coff.p, c->cflag.p, c->cpos.p, (uint64_t)nt,
                        c->l_off.p, c->ctot.p);
     HIPCHK(hipGetLastError());
-    uint64_t tot[2] = {0, 0};
-    HIPCHK(hipMemcpyAsync(tot, c->ctot.p, sizeof(tot), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    const uint64_t total = tot[0], n_live = tot[1];
-    c->cstats.n_live = n_live;
-    c->cstats.bytes_out = total;
-    const uint64_t n_blocks = (total + CBLK - 1) / CBLK;
-    if (c->cfirst.ensure(n_blocks)) return KVR_ENOMEM;
+    // the live bytes are at most the segment bytes: size everything by that bound, so the rest of
+    // the pipeline runs without a host round trip (the kernels read the true sizes on device)
+    const uint64_t max_blocks = (bytes_in + CBLK - 1) / CBLK;
+    const uint64_t max_cuts = seg_target ? bytes_in / seg_target + 1 : 1;
+    if (c->cfirst.ensure(max_blocks) || c->ccuts.ensure(max_cuts)) return KVR_ENOMEM;
     hipLaunchKernelGGL(k_scatter, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p, c->csize.p, c->coff.p,
                        c->cflag.p, c->cpos.p, c->l_src.p, c->l_off.p, c->cfirst.p);
     HIPCHK(hipGetLastError());
-
-    // 3. new-segment boundaries (cuts at the first record at or after k * seg_target)
-    std::vector<uint64_t> ends;
-    if (total) {
-        if (seg_target && total > seg_target) {
-            const uint64_t n_cuts = (total - 1) / seg_target;
-            if (c->ccuts.ensure(n_cuts)) return KVR_ENOMEM;
-            hipLaunchKernelGGL(k_cuts, dim3((uint32_t)((n_cuts + 255) / 256)), dim3(256), 0, st, c->l_off.p, c->ctot.p,
-                               seg_target, n_cuts, c->ccuts.p);
-            HIPCHK(hipGetLastError());
-            std::vector<uint64_t> cuts(n_cuts);
-            HIPCHK(hipMemcpyAsync(cuts.data(), c->ccuts.p, n_cuts * 8, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipStreamSynchronize(st));
-            for (uint64_t v : cuts)
-                if (v < total && (ends.empty() || v > ends.back())) ends.push_back(v);
-        }
-        ends.push_back(total);
+    if (seg_target) {
+        hipLaunchKernelGGL(k_cuts, dim3((uint32_t)std::min<uint64_t>((max_cuts + 255) / 256, 1024)), dim3(256), 0, st,
+                           c->l_off.p, c->ctot.p, seg_target, c->ccuts.p);
+        HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(c->ev[1], st));
-    *out_len = total;
-    *n_out_segs = ends.size();
-    if (total > out_cap || ends.size() > seg_cap) {
-        HIPCHK(hipStreamSynchronize(st));
-        return KVR_CAPACITY;
-    }
-    for (size_t j = 0; j < ends.size(); ++j) seg_ends[j] = ends[j];
-    if (!total) return KVR_OK;
-
-    // 4. gather (straight into a device output when it is 8-B aligned, else through staging)
-    uint8_t *d_out = out;
+    // gather straight into a device output when it is 8-B aligned, else through staging
     const bool direct = (flags & KVR_OUT_ON_DEVICE) && !(reinterpret_cast<uintptr_t>(out) & 7u);
+    uint8_t *d_out = out;
+    uint64_t d_cap = out_cap;
     if (!direct) {
-        if (c->cout.ensure(total + 8)) return KVR_ENOMEM;
+        if (c->cout.ensure(bytes_in + 8)) return KVR_ENOMEM;
         d_out = c->cout.p;
+        d_cap = bytes_in;
     }
-    hipLaunchKernelGGL(k_gather, dim3((uint32_t)((n_blocks + CT_GATHER / 64 - 1) / (CT_GATHER / 64))), dim3(CT_GATHER), 0,
-                       st, c->l_src.p, c->l_off.p, c->cfirst.p, c->ctot.p, n_blocks, d_out);
+    const uint32_t gw = (uint32_t)std::min<uint64_t>((max_blocks + CT_GATHER / 64 - 1) / (CT_GATHER / 64),
+                                                     (uint64_t)c->n_cu * 16);
+    hipLaunchKernelGGL(k_gather, dim3(std::max(gw, 1u)), dim3(CT_GATHER), 0, st, c->l_src.p, c->l_off.p, c->cfirst.p,
+                       c->ctot.p, d_out, d_cap);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[2], st));
-    if (!direct)
-        HIPCHK(hipMemcpyAsync(out, d_out, total, (flags & KVR_OUT_ON_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
+    uint64_t tot[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(tot, c->ctot.p, sizeof(tot), hipMemcpyDeviceToHost, st));
+    std::vector<uint64_t> cuts(seg_target ? max_cuts : 0);
+    if (seg_target) HIPCHK(hipMemcpyAsync(cuts.data(), c->ccuts.p, max_cuts * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     c->cstats.ms_fold = ev_ms(c->ev[0], c->ev[1]);
     c->cstats.ms_gather = ev_ms(c->ev[1], c->ev[2]);
+    const uint64_t total = tot[0], n_live = tot[1];
+    c->cstats.n_live = n_live;
+    c->cstats.bytes_out = total;
+    // new-segment boundaries: the distinct cut offsets, then the end
+    std::vector<uint64_t> ends;
+    if (total) {
+        const uint64_t n_cuts = (seg_target && total > seg_target) ? (total - 1) / seg_target : 0;
+        for (uint64_t k = 0; k < n_cuts; ++k)
+            if (cuts[k] < total && (ends.empty() || cuts[k] > ends.back())) ends.push_back(cuts[k]);
+        ends.push_back(total);
+    }
+    *out_len = total;
+    *n_out_segs = ends.size();
+    if (total > out_cap || ends.size() > seg_cap) return KVR_CAPACITY;
+    for (size_t j = 0; j < ends.size(); ++j) seg_ends[j] = ends[j];
+    if (total && !direct) {
+        HIPCHK(hipMemcpyAsync(out, d_out, total, (flags & KVR_OUT_ON_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
     return KVR_OK;
 }
 

@@ -126,80 +126,86 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// one wave per 512-B output block; lane l writes output bytes [b*512 + 8l, + 8)
+// one wave per 512-B output block (grid-stride over the blocks; their number comes from the
+// device totals); lane l writes output bytes [b*512 + 8l, + 8), none at or past cap
 __global__ void __launch_bounds__(CT_GATHER) k_gather(const uint64_t *__restrict__ l_src, const uint64_t *__restrict__ l_off,
                                                       const uint32_t *__restrict__ first, const uint64_t *__restrict__ totals,
-                                                      uint64_t n_blocks, uint8_t *__restrict__ out) {
-    const uint64_t b = (uint64_t)blockIdx.x * (CT_GATHER / 64) + (threadIdx.x >> 6);
+                                                      uint8_t *__restrict__ out, uint64_t cap) {
     const int lane = threadIdx.x & 63;
-    if (b >= n_blocks) return;   // wave-uniform
     const uint64_t total = totals[0];
     const uint32_t n_live = (uint32_t)totals[1];
-    const uint32_t j0 = first[b];
-    // lane l: the end of live record j0 + l (records are >= 10 B: at most 52 start in a block)
-    const uint32_t jl = j0 + (uint32_t)lane;
-    const uint64_t e = jl < n_live ? l_off[jl + 1] : ~0ull;
-    const uint64_t x = (b << CBLK_LOG) + 8u * (uint32_t)lane;
-    int c = 0;   // live records of the wave ending at or before x
+    const uint64_t n_blocks = (total + CBLK - 1) >> CBLK_LOG;
+    const uint64_t lim = total < cap ? total : cap;
+    const uint64_t waves = (uint64_t)gridDim.x * (CT_GATHER / 64);
+    for (uint64_t b = (uint64_t)blockIdx.x * (CT_GATHER / 64) + (threadIdx.x >> 6); b < n_blocks; b += waves) {
+        const uint32_t j0 = first[b];
+        // lane l: the end of live record j0 + l (records are >= 9 B: at most 57 start in a block)
+        const uint32_t jl = j0 + (uint32_t)lane;
+        const uint64_t e = jl < n_live ? l_off[jl + 1] : ~0ull;
+        const uint64_t x = (b << CBLK_LOG) + 8u * (uint32_t)lane;
+        int c = 0;   // live records of the wave ending at or before x
 #pragma unroll
-    for (int step = 32; step >= 1; step >>= 1) {
-        const uint64_t ev = shfl64(e, c + step - 1);
-        if (ev <= x) c += step;
-    }
-    const uint64_t ej = shfl64(e, c);
-    if (x >= total) return;
-    uint32_t j = j0 + (uint32_t)c;
-    uint64_t sj = l_off[j];
-    uint64_t src = l_src[j] + (x - sj);
-    uint32_t lo, hi;
-    if (ej - x >= 8) {   // the lane's 8 bytes lie in one record: aligned dword reads + funnel shifts
-        const uint32_t *a = reinterpret_cast<const uint32_t *>(src & ~3ull);
-        const uint32_t sh = (uint32_t)src & 3u;
-        const uint32_t w0 = a[0], w1 = a[1], w2 = sh ? a[2] : 0u;   // a[2] holds byte src + 7 when sh != 0
-        lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
-        hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-    } else {             // the lane's bytes span records: byte by byte
-        uint64_t ejj = ej;
-        src = l_src[j];   // record base (bytes are indexed by output offset - record start)
-        uint8_t by[8];
-        for (int q = 0; q < 8; ++q) {
-            const uint64_t xq = x + q;
-            if (xq >= total) { by[q] = 0; continue; }
-            while (xq >= ejj) {
-                ++j;
-                sj = ejj;
-                src = l_src[j];
-                ejj = l_off[j + 1];
-            }
-            by[q] = reinterpret_cast<const uint8_t *>(src)[xq - sj];
+        for (int step = 32; step >= 1; step >>= 1) {
+            const uint64_t ev = shfl64(e, c + step - 1);
+            if (ev <= x) c += step;
         }
-        lo = by[0] | (by[1] << 8) | (by[2] << 16) | ((uint32_t)by[3] << 24);
-        hi = by[4] | (by[5] << 8) | (by[6] << 16) | ((uint32_t)by[7] << 24);
-    }
-    if (x + 8 <= total) {
-        uint2 v;
-        v.x = lo;
-        v.y = hi;
-        *reinterpret_cast<uint2 *>(out + x) = v;   // out is 8-B aligned (the host stages otherwise)
-    } else {
-        const uint64_t m = total - x;
-        for (uint64_t q = 0; q < m; ++q) out[x + q] = (uint8_t)((q < 4 ? lo >> (8 * q) : hi >> (8 * (q - 4))) & 255u);
+        const uint64_t ej = shfl64(e, c);
+        if (x >= lim) continue;
+        uint32_t j = j0 + (uint32_t)c;
+        uint64_t sj = l_off[j];
+        uint32_t lo, hi;
+        if (ej - x >= 8) {   // the lane's 8 bytes lie in one record: aligned dword reads + funnel shifts
+            const uint64_t src = l_src[j] + (x - sj);
+            const uint32_t *a = reinterpret_cast<const uint32_t *>(src & ~3ull);
+            const uint32_t sh = (uint32_t)src & 3u;
+            const uint32_t w0 = a[0], w1 = a[1], w2 = sh ? a[2] : 0u;   // a[2] holds byte src + 7 when sh != 0
+            lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        } else {             // the lane's bytes span records: byte by byte
+            uint64_t ejj = ej, src = l_src[j];   // record base: bytes indexed by output offset - record start
+            uint8_t by[8];
+            for (int q = 0; q < 8; ++q) {
+                const uint64_t xq = x + q;
+                if (xq >= total) { by[q] = 0; continue; }
+                while (xq >= ejj) {
+                    ++j;
+                    sj = ejj;
+                    src = l_src[j];
+                    ejj = l_off[j + 1];
+                }
+                by[q] = reinterpret_cast<const uint8_t *>(src)[xq - sj];
+            }
+            lo = by[0] | (by[1] << 8) | (by[2] << 16) | ((uint32_t)by[3] << 24);
+            hi = by[4] | (by[5] << 8) | (by[6] << 16) | ((uint32_t)by[7] << 24);
+        }
+        if (x + 8 <= lim) {
+            uint2 v;
+            v.x = lo;
+            v.y = hi;
+            *reinterpret_cast<uint2 *>(out + x) = v;   // out is 8-B aligned (the host stages otherwise)
+        } else {
+            const uint64_t m = lim - x;
+            for (uint64_t q = 0; q < m; ++q) out[x + q] = (uint8_t)((q < 4 ? lo >> (8 * q) : hi >> (8 * (q - 4))) & 255u);
+        }
     }
 }
 
-// cut k (k = 1 .. n_cuts): the output offset of the first live record at or after k * target
+// cut k (k = 1 .. (total - 1) / target): the output offset of the first live record at or after
+// k * target (grid-stride; the count comes from the device totals, cuts has room for it)
 __global__ void k_cuts(const uint64_t *__restrict__ l_off, const uint64_t *__restrict__ totals, uint64_t target,
-                       uint64_t n_cuts, uint64_t *__restrict__ cuts) {
-    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_cuts) return;
-    const uint64_t want = (k + 1) * target;
-    uint64_t lo = 0, hi = totals[1];   // lower_bound over l_off[0, n_live)
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (l_off[mid] < want) lo = mid + 1;
-        else hi = mid;
+                       uint64_t *__restrict__ cuts) {
+    const uint64_t total = totals[0];
+    const uint64_t n_cuts = total > target ? (total - 1) / target : 0;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_cuts; k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t want = (k + 1) * target;
+        uint64_t lo = 0, hi = totals[1];   // lower_bound over l_off[0, n_live)
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (l_off[mid] < want) lo = mid + 1;
+            else hi = mid;
+        }
+        cuts[k] = l_off[lo];   // l_off[n_live] = total
     }
-    cuts[k] = l_off[lo];   // l_off[n_live] = total
 }
 
 }  // namespace kvr
