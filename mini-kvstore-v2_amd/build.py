@@ -95,6 +95,7 @@ def build_ablate(masks=(0, 1, 2, 3, 7, 8, 16, 32, 64)):
 # experimental k_replay variants (tools/ablate.py <cfg> 0 <name>): timing only, not shipped
 VARIANTS = {
     "rt768": ["-DKVR_RT=768"],
+    "rt512": ["-DKVR_RT=512"],
 }
 
 
