@@ -199,10 +199,9 @@ def bench_compact(args, ctx, segs, seg_nos, seg_total, n_rec, desc, nseg, seg_by
     import numpy as np
     import torch
     import kvreplay as K
-    if world > 1:
-        raise SystemExit("--mode compact runs on one GPU: a sharded store needs the cross-rank fold "
-                         "(DESIGN.md §9), not a per-shard one")
     target = 64 << 20
+    if world > 1:
+        return bench_compact_sharded(args, ctx, segs, seg_nos, seg_total, n_rec, desc, nseg, seg_bytes, world, target)
     out = torch.empty(seg_total + 4096, dtype=torch.uint8, device="cuda")
 
     def step():
@@ -247,6 +246,58 @@ def bench_compact(args, ctx, segs, seg_nos, seg_total, n_rec, desc, nseg, seg_by
     }
     print(json.dumps(res))
     ctx.close()
+
+
+def bench_compact_sharded(args, ctx, segs, seg_nos, seg_total, n_rec, desc, nseg, seg_bytes, world, target):
+    """N ranks, segments round-robin: the global last-writer fold needs the candidate exchange
+    (kvreplay.shard.compact_sharded: two all-to-alls over RCCL); one step = the whole sharded
+    compaction, timed with barriers and the max over ranks."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from kvreplay import shard as SH
+    eng = SH.DeviceCompactEngine(ctx, torch.device("cuda", torch.cuda.current_device()))
+    rank = dist.get_rank()
+
+    def step():
+        return SH.compact_sharded(eng, segs, seg_nos, seg_target=target, on_device=True)
+
+    for _ in range(args.warmup):
+        data, ends = step()
+    n_live = torch.tensor([ctx_live(ctx)], dtype=torch.int64, device="cuda")
+    dist.all_reduce(n_live)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = SH.max_over_ranks(time.perf_counter() - t0)
+    res = {
+        "metric": "device-resident compaction live-record rewrite GiB/s (segment bytes in)",
+        "value": round(seg_total * world * args.steps / dt / 2 ** 30, 3), "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (device generator, seeded)",
+        "config": {"workload": f"{args.config}: {desc}, device-resident input, sharded compaction "
+                               f"(round-robin), each rank's output copied to host",
+                   "segments_per_gpu": nseg, "segment_bytes": seg_bytes, "bytes_per_gpu": seg_total,
+                   "records_per_gpu": n_rec, "live_records_total": int(n_live.item()),
+                   "parallelism": f"shard-segments x{world}, candidate all-to-all (RCCL)"},
+    }
+    if rank == 0:
+        print(json.dumps(res))
+    ctx.close()
+    dist.destroy_process_group()
+
+
+def ctx_live(ctx):
+    import ctypes as C
+    import kvreplay as K
+    st = K.CompactStats()
+    K.native()[0].kvr_last_compact_stats(ctx.h, C.byref(st))
+    return int(st.n_live)
 
 
 if __name__ == "__main__":

@@ -173,6 +173,40 @@ int  kvr_compact(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint32_t 
                  size_t *n_out_segs, kvr_error *err);
 int  kvr_last_compact_stats(const kvr_ctx *ctx, kvr_compact_stats *out);
 
+/* ---- sharded compaction: one rank of a store whose segments are dealt over several GPUs -----
+ * The fold is global (a key's last writer may sit on another rank), so the rewrite runs as
+ * three calls per rank around two all-to-all exchanges that the caller performs on device
+ * buffers (mini-kvstore-v2_amd/kvreplay/shard.py does it over torch.distributed: RCCL on GPUs).
+ *   kvr_compact_stage    replay this rank's segments (segs[i] is global segment gidx[i], the
+ *                        position in the store's sorted list), fold locally and build one
+ *                        candidate per key (its local last record) addressed to owner rank
+ *                        hash(key) mod n_ranks: counts[o] headers and key_bytes[o] key bytes.
+ *   kvr_compact_export   copy the candidates to device buffers: headers grouped by owner, key
+ *                        bytes grouped by owner (each group's key_off is relative to its group).
+ *   kvr_compact_resolve  owner side, over what every rank sent here (headers and keys in sender
+ *                        order; hdr_counts[s] / key_counts[s] per sender): d_win[i] = 1 iff header
+ *                        i is its key's last writer over all ranks (largest global position).
+ *   kvr_compact_finish   d_win = the answers for this rank's own candidates, in export order:
+ *                        a record is live iff it is a SET, its key's local last and the winner;
+ *                        the live records are written out exactly as kvr_compact does.
+ * Every rank's output is disjoint from the others' (one live record per key in the whole store);
+ * together they replay to the pre-compaction map. */
+typedef struct kvr_cand {
+    uint64_t pos;       /* (global segment index << 40) | rec_off                                */
+    uint32_t key_len;
+    uint32_t key_tag;   /* CRC-32 of the key                                                    */
+    uint32_t key_off;   /* offset of the key bytes within the owner group's key bytes            */
+    uint32_t pad;
+} kvr_cand;
+
+int  kvr_compact_stage(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint32_t flags, const uint32_t *gidx,
+                       uint32_t n_ranks, uint64_t *counts, uint64_t *key_bytes, kvr_error *err);
+int  kvr_compact_export(kvr_ctx *ctx, kvr_cand *d_hdr, uint8_t *d_keys);
+int  kvr_compact_resolve(kvr_ctx *ctx, const kvr_cand *d_hdr, const uint8_t *d_keys, const uint64_t *hdr_counts,
+                         const uint64_t *key_counts, uint32_t n_ranks, uint8_t *d_win);
+int  kvr_compact_finish(kvr_ctx *ctx, const uint8_t *d_win, uint32_t flags, uint64_t seg_target, uint8_t *out,
+                        uint64_t out_cap, uint64_t *out_len, uint64_t *seg_ends, size_t seg_cap, size_t *n_out_segs);
+
 /* ---- synthetic segment generator (device side; byte-identical to kvh_gen_segment) -------- */
 typedef struct kvr_gen_params {
     uint64_t seed;

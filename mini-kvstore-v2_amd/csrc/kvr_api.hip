@@ -72,6 +72,16 @@ struct kvr_ctx {
     DevBuf<uint64_t> csize, coff, l_src, l_off, ctot, ccuts;
     DevBuf<uint8_t> cout, ctmp;
     kvr_compact_stats cstats{};
+    size_t c_nt = 0;                       // tuples of the last compaction front half
+    uint32_t c_ranks = 0;                  // sharded compaction state (kvr_compact_stage .. finish)
+    bool c_staged = false;
+    uint64_t c_ncand = 0, c_nkey = 0;
+    DevBuf<uint32_t> c_gidx, c_own, c_sidx;
+    DevBuf<uint64_t> c_val, c_scan, c_gstart;
+    DevBuf<kvr_cand> c_hdr;
+    DevBuf<uint8_t> c_keys;
+    DevBuf<uint32_t> r_rep, r_slot;
+    DevBuf<uint64_t> r_best, r_hk;
     LinkResult *h_link = nullptr;
     Counters *h_ctr = nullptr;
     std::vector<SegDesc> h_segs;
@@ -226,6 +236,9 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->ctup.release(); c->ht_rep.release(); c->ht_best.release(); c->cslot.release(); c->cflag.release();
     c->cpos.release(); c->cfirst.release(); c->csize.release(); c->coff.release(); c->l_src.release();
     c->l_off.release(); c->ctot.release(); c->ccuts.release(); c->cout.release(); c->ctmp.release();
+    c->c_gidx.release(); c->c_own.release(); c->c_sidx.release(); c->c_val.release(); c->c_scan.release();
+    c->c_gstart.release(); c->c_hdr.release(); c->c_keys.release(); c->r_rep.release(); c->r_slot.release();
+    c->r_best.release(); c->r_hk.release();
     if (c->h_link) (void)hipHostFree(c->h_link);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
@@ -502,19 +515,15 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
 // ---------------------------------------------------------------------------------------
 // live-record rewrite (kvr_compact.hip): replay -> fold -> live list -> gather -> cuts
 // ---------------------------------------------------------------------------------------
-int kvr_compact(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, uint64_t seg_target, uint8_t *out,
-                uint64_t out_cap, uint64_t *out_len, uint64_t *seg_ends, size_t seg_cap, size_t *n_out_segs,
-                kvr_error *err) {
-    if (!c || (!segs && n) || !out_len || !n_out_segs || (out_cap && !out) || (seg_cap && !seg_ends)) return KVR_EINVAL;
-    *out_len = 0;
-    *n_out_segs = 0;
+// replay + the local last-writer fold (k_fold_insert): the front half of every compaction
+static int compact_front(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, kvr_error *err, size_t *nt_out) {
+    *nt_out = 0;
     memset(&c->cstats, 0, sizeof(c->cstats));
     if (err) memset(err, 0, sizeof(*err));
-    if (n == 0) return KVR_OK;
     uint64_t bytes_in = 0;
     for (size_t i = 0; i < n; ++i) bytes_in += segs[i].len;
     c->cstats.bytes_in = bytes_in;
-
+    if (n == 0) return KVR_OK;
     // 1. replay into context-resident tuples; the segment bytes stay in HBM (c->segs)
     size_t nt = 0;
     if (c->ctup.ensure(bytes_in / 64 + 1024)) return KVR_ENOMEM;
@@ -527,11 +536,12 @@ int kvr_compact(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, u
     if (rc != KVR_OK) return rc;
     c->cstats.ms_replay = c->stats.ms_total;
     c->cstats.n_tuples = nt;
+    c->c_nt = nt;
+    *nt_out = nt;
     if (nt == 0) return KVR_OK;
     if (nt >= 0x7FFFFFFFull) return KVR_EINVAL;   // 32-bit tuple indices in the fold table
     hipStream_t st = c->stream;
-
-    // 2. fold: the key's last tuple, live flags and sizes, scans, dense live list
+    // 2. the key's last tuple (open addressing over the key bytes)
     uint64_t slots = 1;
     while (slots < 2 * (uint64_t)nt) slots <<= 1;
     if (c->ht_rep.ensure(slots) || c->ht_best.ensure(slots) || c->cslot.ensure(nt) || c->cflag.ensure(nt) ||
@@ -542,15 +552,22 @@ int kvr_compact(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, u
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, c->csize.p, c->coff.p, (int)nt, st));
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, c->cflag.p, c->cpos.p, (int)nt, st));
     if (c->ctmp.ensure(std::max(t1, t2))) return KVR_ENOMEM;
-    const uint32_t g = (uint32_t)((nt + 255) / 256);
     HIPCHK(hipEventRecord(c->ev[0], st));
     HIPCHK(hipMemsetAsync(c->ht_rep.p, 0xFF, slots * 4, st));
     HIPCHK(hipMemsetAsync(c->ht_best.p, 0, slots * 4, st));
-    hipLaunchKernelGGL(k_fold_insert, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p, c->ht_rep.p,
-                       c->ht_best.p, (uint32_t)(slots - 1), c->cslot.p);
-    hipLaunchKernelGGL(k_live, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->ht_best.p, c->cslot.p, c->csize.p,
-                       c->cflag.p);
+    hipLaunchKernelGGL(k_fold_insert, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, st, c->ctup.p, (uint64_t)nt,
+                       c->segs.p, c->ht_rep.p, c->ht_best.p, (uint32_t)(slots - 1), c->cslot.p);
     HIPCHK(hipGetLastError());
+    return KVR_OK;
+}
+
+// sizes and live flags are in csize / cflag: scans, dense live list, cuts, gather, output
+static int compact_back(kvr_ctx *c, uint32_t flags, uint64_t seg_target, uint8_t *out, uint64_t out_cap,
+                        uint64_t *out_len, uint64_t *seg_ends, size_t seg_cap, size_t *n_out_segs) {
+    const size_t nt = c->c_nt;
+    const uint64_t bytes_in = c->cstats.bytes_in;
+    hipStream_t st = c->stream;
+    const uint32_t g = (uint32_t)((nt + 255) / 256);
     size_t tb = c->ctmp.n;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->csize.p, c->coff.p, (int)nt, st));
     tb = c->ctmp.n;
@@ -614,6 +631,119 @@ int kvr_compact(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, u
         HIPCHK(hipStreamSynchronize(st));
     }
     return KVR_OK;
+}
+
+int kvr_compact(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, uint64_t seg_target, uint8_t *out,
+                uint64_t out_cap, uint64_t *out_len, uint64_t *seg_ends, size_t seg_cap, size_t *n_out_segs,
+                kvr_error *err) {
+    if (!c || (!segs && n) || !out_len || !n_out_segs || (out_cap && !out) || (seg_cap && !seg_ends)) return KVR_EINVAL;
+    *out_len = 0;
+    *n_out_segs = 0;
+    size_t nt = 0;
+    const int rc = compact_front(c, segs, n, flags, err, &nt);
+    if (rc != KVR_OK || nt == 0) return rc;
+    hipLaunchKernelGGL(k_live, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, c->stream, c->ctup.p, (uint64_t)nt,
+                       c->ht_best.p, c->cslot.p, c->csize.p, c->cflag.p);
+    HIPCHK(hipGetLastError());
+    return compact_back(c, flags, seg_target, out, out_cap, out_len, seg_ends, seg_cap, n_out_segs);
+}
+
+int kvr_compact_stage(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, const uint32_t *gidx,
+                      uint32_t n_ranks, uint64_t *counts, uint64_t *key_bytes, kvr_error *err) {
+    if (!c || (!segs && n) || (n && !gidx) || n_ranks == 0 || !counts || !key_bytes) return KVR_EINVAL;
+    for (uint32_t o = 0; o < n_ranks; ++o) counts[o] = key_bytes[o] = 0;
+    c->c_ranks = n_ranks;
+    c->c_staged = false;
+    size_t nt = 0;
+    const int rc = compact_front(c, segs, n, flags, err, &nt);
+    if (rc != KVR_OK) return rc;
+    c->c_staged = true;
+    if (nt == 0) return KVR_OK;
+    hipStream_t st = c->stream;
+    const uint32_t g = (uint32_t)((nt + 255) / 256);
+    if (c->c_gidx.ensure(n) || c->c_own.ensure(nt) || c->c_sidx.ensure(nt) || c->c_val.ensure(nt) ||
+        c->c_scan.ensure(nt) || c->c_gstart.ensure(2 * (n_ranks + 1)) || c->c_hdr.ensure(nt) ||
+        c->c_keys.ensure(c->cstats.bytes_in + 8))
+        return KVR_ENOMEM;
+    size_t t3 = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t3, c->c_val.p, c->c_scan.p, (int)nt, st));
+    if (c->ctmp.n < t3 && c->ctmp.ensure(t3)) return KVR_ENOMEM;
+    HIPCHK(hipMemcpyAsync(c->c_gidx.p, gidx, n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(c->c_gstart.p, 0, 2 * (n_ranks + 1) * 8, st));
+    hipLaunchKernelGGL(k_cand, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->ht_best.p, c->cslot.p, n_ranks,
+                       c->c_own.p);
+    for (uint32_t o = 0; o < n_ranks; ++o) {   // one group per owner rank, in owner order
+        hipLaunchKernelGGL(k_cand_val, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->c_own.p, o, c->c_val.p);
+        size_t tb = c->ctmp.n;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->c_val.p, c->c_scan.p, (int)nt, st));
+        hipLaunchKernelGGL(k_cand_total, dim3(1), dim3(64), 0, st, c->c_scan.p, c->c_val.p, (uint64_t)nt, o, n_ranks,
+                           c->c_gstart.p);
+        hipLaunchKernelGGL(k_cand_place, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p, c->c_gidx.p,
+                           c->c_own.p, o, n_ranks, c->c_scan.p, c->c_gstart.p, c->c_hdr.p, c->c_keys.p, c->c_sidx.p);
+        HIPCHK(hipGetLastError());
+    }
+    std::vector<uint64_t> gs(2 * (n_ranks + 1));
+    HIPCHK(hipMemcpyAsync(gs.data(), c->c_gstart.p, gs.size() * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (uint32_t o = 0; o < n_ranks; ++o) {
+        counts[o] = gs[o + 1] - gs[o];
+        key_bytes[o] = gs[n_ranks + 1 + o + 1] - gs[n_ranks + 1 + o];
+    }
+    c->c_ncand = gs[n_ranks];
+    c->c_nkey = gs[2 * n_ranks + 1];
+    return KVR_OK;
+}
+
+int kvr_compact_export(kvr_ctx *c, kvr_cand *d_hdr, uint8_t *d_keys) {
+    if (!c || !c->c_staged) return KVR_EINVAL;
+    hipStream_t st = c->stream;
+    if (c->c_ncand) HIPCHK(hipMemcpyAsync(d_hdr, c->c_hdr.p, c->c_ncand * sizeof(kvr_cand), hipMemcpyDeviceToDevice, st));
+    if (c->c_nkey) HIPCHK(hipMemcpyAsync(d_keys, c->c_keys.p, c->c_nkey, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return KVR_OK;
+}
+
+int kvr_compact_resolve(kvr_ctx *c, const kvr_cand *d_hdr, const uint8_t *d_keys, const uint64_t *hdr_counts,
+                        const uint64_t *key_counts, uint32_t n_ranks, uint8_t *d_win) {
+    if (!c || !hdr_counts || !key_counts || n_ranks == 0) return KVR_EINVAL;
+    std::vector<uint64_t> hk(2 * (n_ranks + 1), 0);   // header starts, then key bases, per sender
+    for (uint32_t s2 = 0; s2 < n_ranks; ++s2) {
+        hk[s2 + 1] = hk[s2] + hdr_counts[s2];
+        hk[n_ranks + 1 + s2 + 1] = hk[n_ranks + 1 + s2] + key_counts[s2];
+    }
+    const uint64_t m = hk[n_ranks];
+    if (m == 0) return KVR_OK;
+    if (m >= 0x7FFFFFFFull) return KVR_EINVAL;
+    uint64_t slots = 1;
+    while (slots < 2 * m) slots <<= 1;
+    hipStream_t st = c->stream;
+    if (c->r_rep.ensure(slots) || c->r_best.ensure(slots) || c->r_slot.ensure(m) || c->r_hk.ensure(hk.size()))
+        return KVR_ENOMEM;
+    HIPCHK(hipMemcpyAsync(c->r_hk.p, hk.data(), hk.size() * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(c->r_rep.p, 0xFF, slots * 4, st));
+    HIPCHK(hipMemsetAsync(c->r_best.p, 0, slots * 8, st));
+    const uint32_t g = (uint32_t)((m + 255) / 256);
+    hipLaunchKernelGGL(k_res_insert, dim3(g), dim3(256), 0, st, d_hdr, m, d_keys, c->r_hk.p, c->r_hk.p + n_ranks + 1,
+                       n_ranks, c->r_rep.p, reinterpret_cast<unsigned long long *>(c->r_best.p), (uint32_t)(slots - 1),
+                       c->r_slot.p);
+    hipLaunchKernelGGL(k_res_flag, dim3(g), dim3(256), 0, st, d_hdr, m,
+                       reinterpret_cast<const unsigned long long *>(c->r_best.p), c->r_slot.p, d_win);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
+    return KVR_OK;
+}
+
+int kvr_compact_finish(kvr_ctx *c, const uint8_t *d_win, uint32_t flags, uint64_t seg_target, uint8_t *out,
+                       uint64_t out_cap, uint64_t *out_len, uint64_t *seg_ends, size_t seg_cap, size_t *n_out_segs) {
+    if (!c || !c->c_staged || !out_len || !n_out_segs || (out_cap && !out) || (seg_cap && !seg_ends)) return KVR_EINVAL;
+    *out_len = 0;
+    *n_out_segs = 0;
+    const size_t nt = c->c_nt;
+    if (nt == 0) return KVR_OK;
+    hipLaunchKernelGGL(k_live_global, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, c->stream, c->ctup.p,
+                       (uint64_t)nt, c->ht_best.p, c->cslot.p, c->c_sidx.p, d_win, c->csize.p, c->cflag.p);
+    HIPCHK(hipGetLastError());
+    return compact_back(c, flags, seg_target, out, out_cap, out_len, seg_ends, seg_cap, n_out_segs);
 }
 
 int kvr_last_compact_stats(const kvr_ctx *c, kvr_compact_stats *out) {

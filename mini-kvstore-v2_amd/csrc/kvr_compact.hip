@@ -208,6 +208,133 @@ __global__ void k_cuts(const uint64_t *__restrict__ l_off, const uint64_t *__res
     }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// sharded compaction (kvr_compact_stage / _resolve / _finish): the global last-writer fold of a
+// store whose segments are dealt over several GPUs.  A candidate is a key's LOCAL last record;
+// it goes to owner rank hash(key) mod n_ranks, which keeps the candidate with the largest
+// global position (global segment index, offset) per key and answers with one flag each.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t NO_OWNER = 0xFFFFFFFFu;
+constexpr uint64_t CPOS_SHIFT = 40;   // global position = (global segment index << 40) | rec_off
+
+__device__ __forceinline__ uint32_t owner_of(uint32_t key_tag, uint32_t n_ranks) {
+    return (ht_mix(key_tag) >> 7) % n_ranks;   // other bits than the table slot's
+}
+
+__global__ void k_cand(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ best,
+                       const uint32_t *__restrict__ slot, uint32_t n_ranks, uint32_t *__restrict__ cown) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = slot[i];
+    cown[i] = (s != HT_EMPTY && best[s] == (uint32_t)i + 1u) ? owner_of(tup[i].key_tag, n_ranks) : NO_OWNER;
+}
+
+// per owner o: (1 << 40) | padded key bytes for its candidates (one exclusive scan gives both
+// the header index and the key offset inside the owner's group)
+__global__ void k_cand_val(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ cown, uint32_t o,
+                           uint64_t *__restrict__ val) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    val[i] = cown[i] == o ? ((1ull << CPOS_SHIFT) | ((tup[i].key_len + 3ull) & ~3ull)) : 0ull;
+}
+
+// gstart[o] / gstart[N + 1 + o]: first header / first key byte of owner o's group
+__global__ void k_cand_total(const uint64_t *__restrict__ scan, const uint64_t *__restrict__ val, uint64_t n, uint32_t o,
+                             uint32_t n_ranks, uint64_t *__restrict__ gstart) {
+    if (threadIdx.x || blockIdx.x) return;
+    const uint64_t t = n ? scan[n - 1] + val[n - 1] : 0;
+    const uint64_t mask = (1ull << CPOS_SHIFT) - 1;
+    gstart[o + 1] = gstart[o] + (t >> CPOS_SHIFT);
+    gstart[n_ranks + 1 + o + 1] = gstart[n_ranks + 1 + o] + (t & mask);
+}
+
+__global__ void k_cand_place(const kvr_tuple *__restrict__ tup, uint64_t n, const SegDesc *__restrict__ segs,
+                             const uint32_t *__restrict__ gidx, const uint32_t *__restrict__ cown, uint32_t o,
+                             uint32_t n_ranks, const uint64_t *__restrict__ scan, const uint64_t *__restrict__ gstart,
+                             kvr_cand *__restrict__ hdr, uint8_t *__restrict__ keys, uint32_t *__restrict__ send_idx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || cown[i] != o) return;
+    const kvr_tuple t = tup[i];
+    const uint64_t mask = (1ull << CPOS_SHIFT) - 1;
+    const uint64_t h = gstart[o] + (scan[i] >> CPOS_SHIFT), koff = scan[i] & mask;
+    kvr_cand c;
+    c.pos = ((uint64_t)gidx[t.seg_idx] << CPOS_SHIFT) | t.rec_off;
+    c.key_len = t.key_len;
+    c.key_tag = t.key_tag;
+    c.key_off = (uint32_t)koff;
+    c.pad = 0;
+    hdr[h] = c;
+    const uint8_t *k = key_ptr(segs, t);
+    uint8_t *d = keys + gstart[n_ranks + 1 + o] + koff;
+    for (uint32_t b = 0; b < t.key_len; ++b) d[b] = k[b];
+    send_idx[i] = (uint32_t)h;
+}
+
+// owner side: the candidates received from every rank (headers and keys in sender order)
+__device__ __forceinline__ const uint8_t *cand_key(const kvr_cand &c, uint64_t i, const uint8_t *keys,
+                                                   const uint64_t *hstart, const uint64_t *kbase, uint32_t n_ranks) {
+    uint32_t s = 0;
+    while (s + 1 < n_ranks && i >= hstart[s + 1]) ++s;   // the sender (a few ranks: linear)
+    return keys + kbase[s] + c.key_off;
+}
+
+__global__ void k_res_insert(const kvr_cand *__restrict__ hdr, uint64_t m, const uint8_t *__restrict__ keys,
+                             const uint64_t *__restrict__ hstart, const uint64_t *__restrict__ kbase, uint32_t n_ranks,
+                             uint32_t *__restrict__ rep, unsigned long long *__restrict__ best, uint32_t mask,
+                             uint32_t *__restrict__ slot) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const kvr_cand c = hdr[i];
+    const uint8_t *k = cand_key(c, i, keys, hstart, kbase, n_ranks);
+    uint32_t h = ht_mix(c.key_tag) & mask;
+    for (uint32_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+        uint32_t r = __hip_atomic_load(&rep[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (r == HT_EMPTY) {
+            r = atomicCAS(&rep[h], HT_EMPTY, (uint32_t)i);
+            if (r == HT_EMPTY) r = (uint32_t)i;
+        }
+        bool same = r == (uint32_t)i;
+        if (!same) {
+            const kvr_cand o = hdr[r];
+            if (o.key_tag == c.key_tag && o.key_len == c.key_len) {
+                const uint8_t *ok = cand_key(o, r, keys, hstart, kbase, n_ranks);
+                same = true;
+                for (uint32_t b = 0; b < c.key_len && same; ++b) same = ok[b] == k[b];
+            }
+        }
+        if (same) {
+            atomicMax(&best[h], (unsigned long long)c.pos);
+            slot[i] = h;
+            return;
+        }
+    }
+    slot[i] = HT_EMPTY;
+}
+
+__global__ void k_res_flag(const kvr_cand *__restrict__ hdr, uint64_t m, const unsigned long long *__restrict__ best,
+                           const uint32_t *__restrict__ slot, uint8_t *__restrict__ win) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t s = slot[i];
+    win[i] = (s != HT_EMPTY && best[s] == (unsigned long long)hdr[i].pos) ? 1 : 0;
+}
+
+// this rank's live records after the exchange: a SET that is its key's local last AND the
+// key's global last (its candidate won at the owner)
+__global__ void k_live_global(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ best,
+                              const uint32_t *__restrict__ slot, const uint32_t *__restrict__ send_idx,
+                              const uint8_t *__restrict__ win, uint64_t *__restrict__ size, uint32_t *__restrict__ flag) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const kvr_tuple t = tup[i];
+    const uint32_t s = slot[i];
+    const bool cand = s != HT_EMPTY && best[s] == (uint32_t)i + 1u;
+    const bool live = t.op == 0 && cand && win[send_idx[i]] != 0;
+    size[i] = live ? 9ull + t.key_len + t.val_len : 0ull;
+    flag[i] = live ? 1u : 0u;
+}
+
 }  // namespace kvr
 
 #endif

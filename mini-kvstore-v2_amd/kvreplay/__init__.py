@@ -61,6 +61,9 @@ class StoreStats(C.Structure):
                 ("active_segment_id", C.c_uint64), ("oldest_segment_id", C.c_uint64)]
 
 
+CAND_BYTES = 24   # sizeof(kvr_cand)
+
+
 class CompactStats(C.Structure):
     _fields_ = [("ms_replay", C.c_double), ("ms_fold", C.c_double), ("ms_gather", C.c_double),
                 ("n_tuples", C.c_uint64), ("n_live", C.c_uint64), ("bytes_in", C.c_uint64),
@@ -97,6 +100,10 @@ def _load():
     rep.kvr_compact.argtypes = [P, C.POINTER(Segment), SZ, U32, U64, P, U64, C.POINTER(U64), P, SZ, C.POINTER(SZ),
                                 C.POINTER(Error)]
     rep.kvr_last_compact_stats.argtypes = [P, C.POINTER(CompactStats)]
+    rep.kvr_compact_stage.argtypes = [P, C.POINTER(Segment), SZ, U32, P, U32, P, P, C.POINTER(Error)]
+    rep.kvr_compact_export.argtypes = [P, P, P]
+    rep.kvr_compact_resolve.argtypes = [P, P, P, P, P, U32, P]
+    rep.kvr_compact_finish.argtypes = [P, P, U32, U64, P, U64, C.POINTER(U64), P, SZ, C.POINTER(SZ)]
     rep.kvr_strerror.argtypes = [I]
     rep.kvr_strerror.restype = C.c_char_p
     rep.kvr_crc32.argtypes = [U32, P, SZ]
@@ -375,6 +382,49 @@ class Context:
         data = out_arr[: out_len.value].tobytes() if out_arr is not None and rc == OK else None
         return CompactResult(rc, data, [int(x) for x in ends[: n_segs.value]] if rc == OK else [], out_len.value,
                              n_segs.value, err if rc == CORRUPTED else None, st)
+
+    # ---- sharded compaction (kvreplay.shard.compact_sharded drives these around the exchange) ----
+    def compact_stage(self, segments, gidx, n_ranks, on_device=False):
+        """Replay + local fold + candidates by owner rank -> (counts[n_ranks], key_bytes[n_ranks])."""
+        segs, keep, total = self._segments(segments, None, on_device)
+        g = np.ascontiguousarray(gidx, dtype=np.uint32)
+        counts = np.zeros(n_ranks, dtype=np.uint64)
+        kb = np.zeros(n_ranks, dtype=np.uint64)
+        err = Error()
+        rc = self._rep.kvr_compact_stage(self.h, segs, len(segments), SEGS_ON_DEVICE if on_device else 0,
+                                         g.ctypes.data if g.size else None, n_ranks, counts.ctypes.data,
+                                         kb.ctypes.data, C.byref(err))
+        if rc == CORRUPTED:
+            raise CorruptedData(err.kind, err.seg_idx, err.rec_off, err.aux)
+        if rc != OK:
+            raise NativeError(f"kvr_compact_stage: {rc}")
+        self._stage_total = total
+        return counts.astype(np.int64), kb.astype(np.int64)
+
+    def compact_export(self, d_hdr: int, d_keys: int):
+        rc = self._rep.kvr_compact_export(self.h, d_hdr, d_keys)
+        if rc != OK:
+            raise NativeError(f"kvr_compact_export: {rc}")
+
+    def compact_resolve(self, d_hdr: int, d_keys: int, hdr_counts, key_counts, d_win: int):
+        hc = np.ascontiguousarray(hdr_counts, dtype=np.uint64)
+        kc = np.ascontiguousarray(key_counts, dtype=np.uint64)
+        rc = self._rep.kvr_compact_resolve(self.h, d_hdr, d_keys, hc.ctypes.data, kc.ctypes.data, hc.size, d_win)
+        if rc != OK:
+            raise NativeError(f"kvr_compact_resolve: {rc}")
+
+    def compact_finish(self, d_win: int, seg_target=0):
+        """This rank's live records (host bytes) and new-segment ends."""
+        cap = max(getattr(self, "_stage_total", 0), 1)
+        out = np.zeros(cap, dtype=np.uint8)
+        n_ends = (cap // seg_target + 2) if seg_target else 1
+        ends = np.zeros(n_ends, dtype=np.uint64)
+        ol, ns = C.c_uint64(), C.c_size_t()
+        rc = self._rep.kvr_compact_finish(self.h, d_win, 0, seg_target, out.ctypes.data, out.size, C.byref(ol),
+                                          ends.ctypes.data, ends.size, C.byref(ns))
+        if rc != OK:
+            raise NativeError(f"kvr_compact_finish: {rc}")
+        return out[: ol.value].tobytes(), [int(x) for x in ends[: ns.value]]
 
     def gen_segment_device(self, spec: GenSpec, seg_no: int, d_buf: int, cap: int, d_expected=None,
                            exp_cap=0):

@@ -10,6 +10,13 @@ segments other shards replayed after i, and engine.rs:56 would have stopped at i
 
 Works with one process driving several contexts (ShardedReplay) or one process per GPU
 (torch.distributed, any backend: gather_shards()).
+
+Compaction of a sharded store (compact_sharded) is the one step with a real exchange: a key's
+last writer may sit on another rank.  Each rank folds its shard locally and sends every key's
+local last record (a candidate: global position + key bytes) to the key's owner rank
+(hash(key) mod N) with an all-to-all; owners keep the largest position per key and answer with
+one flag per candidate through a second all-to-all; each rank then writes out its winners that
+are SETs.  Over RCCL (backend "nccl") the buffers are device tensors.
 """
 from __future__ import annotations
 
@@ -123,3 +130,62 @@ def max_over_ranks(x: float, group=None) -> float:
     t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
+
+
+class DeviceCompactEngine:
+    """kvr_compact_stage / _export / _resolve / _finish on one Context (device buffers)."""
+
+    def __init__(self, ctx: Context, device):
+        self.ctx, self.device = ctx, device
+
+    def stage(self, segments, gidx, n_ranks, on_device=False):
+        import torch
+        counts, kb = self.ctx.compact_stage(segments, gidx, n_ranks, on_device=on_device)
+        from . import CAND_BYTES
+        hdr = torch.empty(max(int(counts.sum()) * CAND_BYTES, 1), dtype=torch.uint8, device=self.device)
+        keys = torch.empty(max(int(kb.sum()), 1), dtype=torch.uint8, device=self.device)
+        self.ctx.compact_export(hdr.data_ptr(), keys.data_ptr())
+        return counts, kb, hdr[: int(counts.sum()) * CAND_BYTES], keys[: int(kb.sum())]
+
+    def resolve(self, hdr, keys, hdr_counts, key_counts):
+        import torch
+        win = torch.zeros(max(int(np.sum(hdr_counts)), 1), dtype=torch.uint8, device=self.device)
+        self.ctx.compact_resolve(hdr.data_ptr() if hdr.numel() else 0, keys.data_ptr() if keys.numel() else 0,
+                                 hdr_counts, key_counts, win.data_ptr())
+        return win[: int(np.sum(hdr_counts))]
+
+    def finish(self, win, seg_target):
+        return self.ctx.compact_finish(win.data_ptr() if win.numel() else 0, seg_target)
+
+
+def _a2a(out, inp, out_splits, in_splits, group):
+    import torch.distributed as dist
+    dist.all_to_all_single(out, inp, [int(x) for x in out_splits], [int(x) for x in in_splits], group=group)
+
+
+def compact_sharded(engine, segments, gidx, seg_target=0, group=None, on_device=False):
+    """This rank's share of the compaction of a sharded store (every rank calls it): returns the
+    live records this rank holds, as new segment bytes and their end offsets.  engine provides
+    stage / resolve / finish (DeviceCompactEngine on GPUs; the CPU tests bring a host one)."""
+    import torch
+    import torch.distributed as dist
+    from . import CAND_BYTES
+    world = dist.get_world_size(group)
+    counts, kb, hdr, keys = engine.stage(segments, gidx, world, on_device=on_device)
+    dev = hdr.device
+    # 1. how much each rank sends each other rank
+    mine = torch.tensor(np.stack([counts, kb], axis=1).reshape(-1), dtype=torch.int64, device=dev)
+    theirs = torch.empty_like(mine)
+    _a2a(theirs, mine, [2] * world, [2] * world, group)
+    th = theirs.cpu().numpy().reshape(world, 2)
+    rc_counts, rc_keys = th[:, 0], th[:, 1]
+    # 2. candidates to their owners (exact sizes: the splits must add up to the tensors)
+    hdr_in = torch.empty(int(rc_counts.sum()) * CAND_BYTES, dtype=torch.uint8, device=dev)
+    keys_in = torch.empty(int(rc_keys.sum()), dtype=torch.uint8, device=dev)
+    _a2a(hdr_in, hdr, rc_counts * CAND_BYTES, counts * CAND_BYTES, group)
+    _a2a(keys_in, keys, rc_keys, kb, group)
+    # 3. owners decide; the answers go back in the senders' order
+    win_in = engine.resolve(hdr_in, keys_in, rc_counts, rc_keys)
+    win_mine = torch.zeros(int(counts.sum()), dtype=torch.uint8, device=dev)
+    _a2a(win_mine, win_in, counts, rc_counts, group)
+    return engine.finish(win_mine, seg_target)

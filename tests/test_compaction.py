@@ -287,3 +287,73 @@ def test_kvstore_compact_then_reopen(gctx, tmp_path):
         st = s.stats()
         assert (st.num_keys, st.total_bytes) == (100, before.total_bytes)
         s.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,target", [(2, 0), (3, 4096)])
+def test_gpu_sharded_compaction(gctx, world, target):
+    """The sharded compaction's device engine (kvr_compact_stage / _resolve / _finish) with the
+    all-to-all exchanges emulated in-process (one context per rank on this one GPU): exports and
+    answers equal the host engine's, and the ranks' outputs are exactly the global winners."""
+    torch = pytest.importorskip("torch")
+    from kvreplay import shard as SH
+    from compact_cpu_engine import CAND, HostCompactEngine
+    spec = K.GenSpec(seed=91, seg_bytes=400_000, val_min=1, val_max=2000, del_permille=400, key_space_log2=9)
+    segs = [K.gen_segment_cpu(spec, s)[0].tobytes() for s in range(7)]
+    ctxs = [gctx] + [K.Context(0) for _ in range(world - 1)]
+    dev = [SH.DeviceCompactEngine(c, "cuda") for c in ctxs]
+    host = [HostCompactEngine() for _ in range(world)]
+    st_d, st_h = [], []
+    for r in range(world):
+        idx = SH.shard_round_robin(len(segs), world, r)
+        st_d.append(dev[r].stage([segs[i] for i in idx], idx, world))
+        st_h.append(host[r].stage([segs[i] for i in idx], idx, world))
+        cd, kd, hd, ksd = st_d[r]
+        ch, kh, hh, ksh = st_h[r]
+        assert np.array_equal(cd, ch) and np.array_equal(kd, kh)
+        assert hd.cpu().numpy().tobytes() == hh.numpy().tobytes()   # kvr_cand headers, in owner order
+        hv, kbd, kbh = hh.numpy().view(CAND), ksd.cpu().numpy(), ksh.numpy()
+        gk = np.concatenate([[0], np.cumsum(kh)])
+        gh = np.concatenate([[0], np.cumsum(ch)])
+        for o in range(world):                                       # key bytes (padding aside)
+            for c in hv[gh[o]: gh[o + 1]]:
+                a = gk[o] + c["key_off"]
+                assert kbd[a: a + c["key_len"]].tobytes() == kbh[a: a + c["key_len"]].tobytes()
+
+    def group(r, o):   # rank r's headers / keys for owner o
+        c, kb, h, k = st_d[r]
+        hs, ks = np.concatenate([[0], np.cumsum(c)]), np.concatenate([[0], np.cumsum(kb)])
+        return h[hs[o] * 24: hs[o + 1] * 24], k[ks[o]: ks[o + 1]], int(c[o]), int(kb[o])
+
+    wins = []
+    for o in range(world):                                           # owners resolve
+        parts = [group(s, o) for s in range(world)]
+        hdr_in = torch.cat([p[0] for p in parts])
+        keys_in = torch.cat([p[1] for p in parts])
+        rc_counts = np.array([p[2] for p in parts], dtype=np.int64)
+        rc_keys = np.array([p[3] for p in parts], dtype=np.int64)
+        w = dev[o].resolve(hdr_in, keys_in, rc_counts, rc_keys)
+        wh = host[o].resolve(hdr_in.cpu(), keys_in.cpu(), rc_counts, rc_keys)
+        assert np.array_equal(w.cpu().numpy(), wh.numpy())
+        wins.append((w, np.concatenate([[0], np.cumsum(rc_counts)])))
+    outs = []
+    for r in range(world):                                           # answers back, finish
+        win_mine = torch.cat([wins[o][0][wins[o][1][r]: wins[o][1][r + 1]] for o in range(world)])
+        outs.append(dev[r].finish(win_mine, target))
+    # expected: the global last record of every key that is a SET, on the rank holding it
+    rc, t, _ = O.replay(segs)
+    last = {}
+    for i, rr in enumerate(t):
+        s = segs[rr["seg_idx"]]
+        last[s[rr["rec_off"] + 5: rr["rec_off"] + 5 + rr["key_len"]]] = i
+    exp = [bytearray() for _ in range(world)]
+    for i in sorted(last.values()):
+        rr = t[i]
+        if rr["op"] == 0:
+            s = segs[rr["seg_idx"]]
+            exp[rr["seg_idx"] % world] += s[rr["rec_off"]: rr["rec_off"] + 9 + rr["key_len"] + rr["val_len"]]
+    for r in range(world):
+        assert outs[r][0] == bytes(exp[r])
+        assert py_compact([outs[r][0]], target)[1] == outs[r][1]     # the cut rule on each rank's output
+    for c in ctxs[1:]:
+        c.close()

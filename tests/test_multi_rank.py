@@ -88,3 +88,60 @@ def test_two_rank_gloo_first_error_is_global_minimum(tmp_path):
     assert st == K.CORRUPTED and rc == K.CORRUPTED
     assert rest.split(")")[0] + ")" == str((e.kind, e.seg_idx, e.rec_off, e.aux))
     assert e.seg_idx == 3
+
+
+# ---- sharded compaction: the one step with a real exchange (kvreplay.shard.compact_sharded) ----
+def _compact_rank_main(rank, world, port, target, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from compact_cpu_engine import HostCompactEngine   # stand-in for DeviceCompactEngine (no GPU here)
+        segs = _segments()
+        idx = SH.shard_round_robin(len(segs), world, rank)
+        data, ends = SH.compact_sharded(HostCompactEngine(), [segs[i] for i in idx], idx, seg_target=target)
+        with open(os.path.join(outdir, f"r{rank}.bin"), "wb") as f:
+            f.write(data)
+        np.save(os.path.join(outdir, f"r{rank}_ends.npy"), np.array(ends, dtype=np.uint64))
+    finally:
+        dist.destroy_process_group()
+
+
+def _expected_split(segs, world):
+    """Per rank: the global last record of every key when it is a SET and lives in that rank's
+    shard, in (segment, offset) order (engine.rs:137/:141 over the whole store)."""
+    rc, t, _ = O.replay(segs)
+    assert rc == 0
+    last = {}
+    for i, r in enumerate(t):
+        s = segs[r["seg_idx"]]
+        last[s[r["rec_off"] + 5: r["rec_off"] + 5 + r["key_len"]]] = i
+    out = [bytearray() for _ in range(world)]
+    for i in sorted(last.values()):
+        r = t[i]
+        if r["op"] == 0:
+            s = segs[r["seg_idx"]]
+            out[r["seg_idx"] % world] += s[r["rec_off"]: r["rec_off"] + 9 + r["key_len"] + r["val_len"]]
+    return [bytes(b) for b in out]
+
+
+@pytest.mark.parametrize("world,target", [(2, 0), (2, 5000), (3, 0)])
+def test_sharded_compaction_gloo(world, target, tmp_path):
+    mp.start_processes(_compact_rank_main, args=(world, _free_port(), target, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    segs = _segments()
+    exp = _expected_split(segs, world)
+    outs = [open(tmp_path / f"r{r}.bin", "rb").read() for r in range(world)]
+    assert outs == exp
+    # every rank's new segments, replayed together, rebuild the store's map
+    new = []
+    for r in range(world):
+        ends = [int(e) for e in np.load(tmp_path / f"r{r}_ends.npy")]
+        new += O.split_segments(outs[r], ends)
+        if target and ends:
+            starts = [0] + ends[:-1]
+            assert all(s // target < (e - 1) // target + 1 for s, e in zip(starts, ends))
+    rc, t, _ = O.replay(new)
+    live, nk, _ = O.fold_live(new, t)
+    rc0, t0, _ = O.replay(segs)
+    live0, nk0, tb0 = O.fold_live(segs, t0)
+    assert nk == nk0 == len(t) and live.all()
