@@ -266,3 +266,27 @@ def test_sharded_replay_matches_single(gctx):
         assert st == rc == 1 and err == (e.kind, e.seg_idx, e.rec_off, e.aux) and err[1] == 2
     finally:
         ctx2.close()
+
+
+def test_segment_over_2gib(gctx):
+    """Maximum sizes: a segment that runs more than 2 GiB past its tiles (the 64-bit copy of the
+    hop loop) holding a value larger than 2 GiB, with ordinary records on both sides, and a
+    second segment after it; plus the same segment cut short inside the big value (KVR_E_VAL)."""
+    big = (1 << 31) + 12345
+    head = b"".join(rec_set(f"k{i}".encode(), bytes([i]) * (i * 37 % 300)) for i in range(200))
+    tail = b"".join(rec_set(f"t{i}".encode(), bytes([255 - i]) * (i * 53 % 900)) for i in range(200)) + rec_del(b"k3")
+    seg = np.empty(len(head) + 9 + 3 + big + len(tail), dtype=np.uint8)
+    o = 0
+    seg[o: o + len(head)] = np.frombuffer(head, np.uint8); o += len(head)
+    hdr = b"\x00" + (3).to_bytes(4, "little") + b"big" + big.to_bytes(4, "little")
+    seg[o: o + len(hdr)] = np.frombuffer(hdr, np.uint8); o += len(hdr)
+    seg[o: o + big] = 0
+    seg[o: o + big: 4099] = 0xA5                     # a sparse pattern (the CRC must see every byte)
+    o += big
+    seg[o: o + len(tail)] = np.frombuffer(tail, np.uint8); o += len(tail)
+    assert o == len(seg)
+    second = rec_set(b"k3", b"again") + rec_set(b"big", b"small now")
+    check_parity(gctx, [seg, second])
+    cut = seg[: len(head) + len(hdr) + big // 2]      # the big value is truncated: engine.rs:130
+    rg = check_parity(gctx, [cut])
+    assert rg.error.kind == KIND["VAL"]
