@@ -3,7 +3,7 @@
 #   parity tests, the bench line, the rocprofv3 kernel-trace summary of the same bench command,
 #   the per-phase cycle breakdown, ablation timings and PMC counters.  Every GPU step has its
 #   own time limit and the steps are chained, so the first failure ends the batch.
-#   usage: tools/gpu_measure.sh <tag> [tests bench bench3 bench5 prof phases ablate traffic pmc ...]
+#   usage: tools/gpu_measure.sh <tag> [tests bench bench3 bench5 prof profc phases ablate traffic pmc ...]
 set -o pipefail
 TAG=${1:-run}; shift
 STEPS=${*:-tests bench prof}
@@ -31,6 +31,10 @@ for s in $STEPS; do
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
         python "$R/bench.py" --no-cpu > "$OUT/prof.log" 2>&1) || { echo "rocprof failed"; tail -20 "$OUT/prof.log"; exit 1; }
       find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \; ;;
+    profc)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profc" -o run -- \
+        python "$R/bench.py" --mode compact --steps 5 --warmup 2 > "$OUT/profc.log" 2>&1) || { echo "rocprof compact failed"; tail -20 "$OUT/profc.log"; exit 1; }
+      find "$OUT/profc" -name '*kernel_stats.csv' -exec cat {} \; ;;
     phases)
       timeout -k 10 240 python -u tools/prof_phases.py cfg2 > "$OUT/phases_cfg2.txt" 2>&1 || { echo "phases failed"; tail -20 "$OUT/phases_cfg2.txt"; exit 1; }
       cat "$OUT/phases_cfg2.txt" ;;
