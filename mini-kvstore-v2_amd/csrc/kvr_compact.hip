@@ -49,13 +49,26 @@ __device__ __forceinline__ const uint8_t *key_ptr(const SegDesc *segs, const kvr
     return segs[t.seg_idx].base + t.rec_off + 5;   // [op][klen u32][key] (engine.rs:169-171)
 }
 
+// n bytes at pa and pb equal: 16-byte chunks of independent (predicated) loads, so a compare costs
+// one memory round trip per 16 bytes instead of one per byte
+__device__ bool bytes_eq(const uint8_t *pa, const uint8_t *pb, uint32_t n) {
+    for (uint32_t i = 0; i < n; i += 16) {
+        const uint32_t m = n - i < 16u ? n - i : 16u;
+        uint32_t diff = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 16; ++q) {
+            const uint32_t x = q < m ? pa[i + q] : 0u, y = q < m ? pb[i + q] : 0u;
+            diff |= x ^ y;
+        }
+        if (diff) return false;
+    }
+    return true;
+}
+
 // key bytes equal (the tags and lengths are compared first)
 __device__ bool key_eq(const SegDesc *segs, const kvr_tuple &a, const kvr_tuple &b) {
     if (a.key_tag != b.key_tag || a.key_len != b.key_len) return false;
-    const uint8_t *pa = key_ptr(segs, a), *pb = key_ptr(segs, b);
-    for (uint32_t i = 0; i < a.key_len; ++i)
-        if (pa[i] != pb[i]) return false;
-    return true;
+    return bytes_eq(key_ptr(segs, a), key_ptr(segs, b), a.key_len);
 }
 
 // the table: rep[h] = the key's first tuple (HT_EMPTY: free), best[h] = 1 + the key's last
@@ -297,11 +310,8 @@ __global__ void k_res_insert(const kvr_cand *__restrict__ hdr, uint64_t m, const
         bool same = r == (uint32_t)i;
         if (!same) {
             const kvr_cand o = hdr[r];
-            if (o.key_tag == c.key_tag && o.key_len == c.key_len) {
-                const uint8_t *ok = cand_key(o, r, keys, hstart, kbase, n_ranks);
-                same = true;
-                for (uint32_t b = 0; b < c.key_len && same; ++b) same = ok[b] == k[b];
-            }
+            if (o.key_tag == c.key_tag && o.key_len == c.key_len)
+                same = bytes_eq(cand_key(o, r, keys, hstart, kbase, n_ranks), k, c.key_len);
         }
         if (same) {
             atomicMax(&best[h], (unsigned long long)c.pos);
