@@ -567,7 +567,39 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         // ---- F + R. framing and records -------------------------------------------------------
         if (in_stripe && search) {   // the stripe's entry: the first plausible record start
             const int o0 = us > (int)vlo_r ? us : (int)vlo_r, o1 = ue < (int)vhi_r ? ue : (int)vhi_r;
-            const int64_t cand = o0 < o1 ? find_cand(ts, o0, o1) : -1;
+            // candidate op bytes (0x00 / 0x01) straight from the registers, kept only when the key
+            // length after them (from the registers too) fits the segment; plausible() (memory
+            // reads) runs on the survivors alone.  cm: bit p = byte p of the lane's unit.
+            const int32_t rc = rem > 0x7FFFFFFFll ? 0x7FFFFFFF : (int32_t)rem;
+            uint32_t cm[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int i = 0; i < UW; ++i) {
+                const uint32_t y = w[i] & 0xFEFEFEFEu;            // bytes 0x00 / 0x01 become 0
+                const uint32_t z = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
+                uint32_t bits = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int o = us + 4 * i + b;
+                    bool ok = ((z >> (8 * b + 7)) & 1u) && o >= o0 && o < o1;
+                    if (i + 1 < UW) {                          // key length: bytes o + 1 .. o + 4
+                        const uint32_t kl = b == 3 ? w[i + 1] : __builtin_amdgcn_alignbyte(w[i + 1], w[i], b + 1);
+                        const int32_t room = rc - o - 5;
+                        ok = ok && room >= 0 && kl <= (uint32_t)room;
+                    }
+                    bits |= ok ? (1u << b) : 0u;
+                }
+                cm[i >> 3] |= bits << (4 * (i & 7));
+            }
+            int64_t cand = -1;
+#pragma unroll 1
+            for (int q = 0; q < 4; ++q) {
+                uint32_t mb = q == 0 ? cm[0] : q == 1 ? cm[1] : q == 2 ? cm[2] : cm[3];
+                while (mb != 0u && cand < 0) {
+                    const int o = us + 32 * q + __builtin_ctz(mb);
+                    if (plausible(ts, o)) cand = o;
+                    mb &= mb - 1u;
+                }
+            }
             uint64_t mn = cand >= 0 ? (uint64_t)(lo + cand) : NONE;
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) {
