@@ -344,33 +344,60 @@ __device__ inline bool key_prefix_ok(const TileSeg &ts, int64_t ok, uint32_t kle
     return true;
 }
 
+// key_prefix_ok over the key bytes held in registers: byte i of the key is byte 5 + i of the
+// little-endian window x[0..5] (x starts at the record).  The same UTF-8 prefix rules as a
+// state machine unrolled over the 16 bytes (need: continuation bytes still due, [clo, chi]: the
+// range of the next one), so no byte waits on the previous one's load.
+__device__ __forceinline__ bool key_prefix_ok_r(const uint32_t (&x)[6], uint32_t klen) {
+    const uint32_t m = klen > 16u ? 16u : klen;
+    uint32_t need = 0, clo = 0x80u, chi = 0xBFu;
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t b = (x[(5 + i) >> 2] >> (8 * ((5 + i) & 3))) & 255u;
+        const bool act = (uint32_t)i < m;
+        const bool lead2 = b >= 0xC2u && b <= 0xDFu, lead3 = b >= 0xE0u && b <= 0xEFu,
+                   lead4 = b >= 0xF0u && b <= 0xF4u;
+        const bool bad_lead = b == 0u || (b >= 0x80u && !lead2 && !lead3 && !lead4);
+        const bool bad_cont = b < clo || b > chi;
+        bad = bad || (act && (need == 0u ? bad_lead : bad_cont));
+        const uint32_t n_need = need != 0u ? need - 1u : (lead2 ? 1u : lead3 ? 2u : lead4 ? 3u : 0u);
+        const uint32_t n_lo = need == 0u && b == 0xE0u ? 0xA0u : need == 0u && b == 0xF0u ? 0x90u : 0x80u;
+        const uint32_t n_hi = need == 0u && b == 0xEDu ? 0x9Fu : need == 0u && b == 0xF4u ? 0x8Fu : 0xBFu;
+        need = n_need; clo = n_lo; chi = n_hi;
+    }
+    return !bad;
+}
+
 __device__ inline bool plausible(const TileSeg &ts, int64_t o) {
     const int64_t rem = (int64_t)ts.len - ts.lo;
+    // the near tests first (header and key bytes sit in the tile's lines): inside a long value
+    // nearly every candidate fails them, before next_rec reads at the far value length.  Inside
+    // the resource the header and 16 key bytes arrive as one window of independent loads.
+    if (o >= 0 && o + 32 <= ts.lim) {
+        const int a = (int)o & ~3;
+        const uint32_t sh = (uint32_t)o & 3u;
+        uint32_t r[7], x[6];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) r[i] = ts.w32a(a + 4 * i);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) x[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
+        const uint32_t op = x[0] & 255u;
+        const uint32_t klen = (x[0] >> 8) | (x[1] << 24);
+        if (op > 1u || rem - o < 5 || (int64_t)klen > rem - o - 5) return false;
+        if (!key_prefix_ok_r(x, klen)) return false;
+    } else {
+        const uint32_t op = ts.b8(o);
+        if (op > 1u || rem - o < 5) return false;
+        const uint32_t klen = ts.u32(o + 1);
+        if ((int64_t)klen > rem - o - 5) return false;
+        if (!key_prefix_ok(ts, o + 5, klen)) return false;
+    }
     const int64_t nx = next_rec(ts, o);
     if (nx < 0) return false;
-    if (!key_prefix_ok(ts, o + 5, ts.u32(o + 1))) return false;
     if (nx == rem) return true;
     if (ts.b8(nx) > 1u || rem - nx < 5) return false;
     return nx + 5 + (int64_t)ts.u32(nx + 1) <= rem;
-}
-
-// first plausible record start in [o0, o1) (tile offsets, inside this lane's unit), or -1
-__device__ __noinline__ int64_t find_cand(const TileSeg ts, int o0, int o1) {
-    #pragma unroll 1
-    for (int q = o0 >> 2; q <= (o1 - 1) >> 2; ++q) {
-        const uint32_t y = ts.w32a(q * 4) & 0xFEFEFEFEu;        // bytes 0x00 / 0x01 become 0
-        uint32_t z = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
-        const int bq = q * 4;
-        if (bq < o0) z &= ~0u << (8 * (o0 - bq));
-        if (bq + 4 > o1) z &= (1u << (8 * (o1 - bq))) - 1u;
-        #pragma unroll 1
-        while (z) {
-            const int o = bq + (__builtin_ctz(z) >> 3);
-            if (plausible(ts, o)) return o;
-            z &= z - 1u;
-        }
-    }
-    return -1;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -590,15 +617,18 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                 }
                 cm[i >> 3] |= bits << (4 * (i & 7));
             }
+            // each round every lane tests its lowest untested survivor, so the lanes' plausible()
+            // calls (dependent loads) run side by side rather than one 32-byte quarter at a time
             int64_t cand = -1;
+            uint32_t m0 = cm[0], m1 = cm[1], m2 = cm[2], m3 = cm[3];
 #pragma unroll 1
-            for (int q = 0; q < 4; ++q) {
-                uint32_t mb = q == 0 ? cm[0] : q == 1 ? cm[1] : q == 2 ? cm[2] : cm[3];
-                while (mb != 0u && cand < 0) {
-                    const int o = us + 32 * q + __builtin_ctz(mb);
-                    if (plausible(ts, o)) cand = o;
-                    mb &= mb - 1u;
-                }
+            while (cand < 0 && (m0 | m1 | m2 | m3) != 0u) {
+                const int q = m0 ? 0 : m1 ? 1 : m2 ? 2 : 3;
+                const uint32_t mb = q == 0 ? m0 : q == 1 ? m1 : q == 2 ? m2 : m3;
+                const uint32_t nb = mb & (mb - 1u);
+                m0 = q == 0 ? nb : m0; m1 = q == 1 ? nb : m1; m2 = q == 2 ? nb : m2; m3 = q == 3 ? nb : m3;
+                const int o = us + 32 * q + __builtin_ctz(mb);
+                if (plausible(ts, o)) cand = o;
             }
             uint64_t mn = cand >= 0 ? (uint64_t)(lo + cand) : NONE;
 #pragma unroll
