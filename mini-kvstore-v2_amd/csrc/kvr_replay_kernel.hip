@@ -594,50 +594,53 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         // ---- F + R. framing and records -------------------------------------------------------
         if (in_stripe && search) {   // the stripe's entry: the first plausible record start
             const int o0 = us > (int)vlo_r ? us : (int)vlo_r, o1 = ue < (int)vhi_r ? ue : (int)vhi_r;
-            // candidate op bytes (0x00 / 0x01) straight from the registers, kept only when the key
-            // length after them (from the registers too) fits the segment; plausible() (memory
-            // reads) runs on the survivors alone.  cm: bit p = byte p of the lane's unit.
+            // candidate op bytes (0x00 / 0x01) straight from the registers, kept only when the top
+            // byte of the key length after them (byte b of the next word) does not exceed the top
+            // byte of the segment bytes left: a necessary condition, word-wide (SWAR).  plausible()
+            // (memory reads, the exact tests) runs on the survivors alone.  cm[g] bit 8 b + j:
+            // byte 4 (8 g + j) + b of the lane's unit.
             const int32_t rc = rem > 0x7FFFFFFFll ? 0x7FFFFFFF : (int32_t)rem;
+            const uint32_t addT = (0x7Fu - ((uint32_t)rc >> 24)) * 0x01010101u;
             uint32_t cm[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
             for (int i = 0; i < UW; ++i) {
                 const uint32_t y = w[i] & 0xFEFEFEFEu;            // bytes 0x00 / 0x01 become 0
-                const uint32_t z = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
-                uint32_t bits = 0;
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const int o = us + 4 * i + b;
-                    bool ok = ((z >> (8 * b + 7)) & 1u) && o >= o0 && o < o1;
-                    if (i + 1 < UW) {                          // key length: bytes o + 1 .. o + 4
-                        const uint32_t kl = b == 3 ? w[i + 1] : __builtin_amdgcn_alignbyte(w[i + 1], w[i], b + 1);
-                        const int32_t room = rc - o - 5;
-                        ok = ok && room >= 0 && kl <= (uint32_t)room;
-                    }
-                    bits |= ok ? (1u << b) : 0u;
+                uint32_t z = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
+                if (i + 1 < UW) {                              // bytes above the bound set their 0x80 bit
+                    const uint32_t x = w[i + 1];
+                    z &= ~((((x & 0x7F7F7F7Fu) + addT) | x));
                 }
-                cm[i >> 3] |= bits << (4 * (i & 7));
+                cm[i >> 3] |= z >> (7 - (i & 7));
             }
-            // each round every lane tests its lowest untested survivor, so the lanes' plausible()
-            // calls (dependent loads) run side by side rather than one 32-byte quarter at a time
-            int64_t cand = -1;
+            KVR_STAMP(11);
+#ifdef KVR_PROF
+            prof_acc[14] += 1000;   // search tiles, x1000
+#endif
+            // each round every lane tests one survivor, so the lanes' plausible() calls (dependent
+            // loads) run side by side; a lane keeps its lowest plausible start, and lanes above the
+            // lowest lane holding one stop (unit positions grow with the lane)
+            int cand = -1;
             uint32_t m0 = cm[0], m1 = cm[1], m2 = cm[2], m3 = cm[3];
 #pragma unroll 1
-            while (cand < 0 && (m0 | m1 | m2 | m3) != 0u) {
-                const int q = m0 ? 0 : m1 ? 1 : m2 ? 2 : 3;
-                const uint32_t mb = q == 0 ? m0 : q == 1 ? m1 : q == 2 ? m2 : m3;
-                const uint32_t nb = mb & (mb - 1u);
-                m0 = q == 0 ? nb : m0; m1 = q == 1 ? nb : m1; m2 = q == 2 ? nb : m2; m3 = q == 3 ? nb : m3;
-                const int o = us + 32 * q + __builtin_ctz(mb);
-                if (plausible(ts, o)) cand = o;
+            for (;;) {
+                const uint64_t fnd = __ballot(cand >= 0);
+                if (fnd != 0ull && lane > (int)__builtin_ctzll(fnd)) { m0 = m1 = m2 = m3 = 0u; }
+                if (__ballot((m0 | m1 | m2 | m3) != 0u) == 0ull) break;
+                if ((m0 | m1 | m2 | m3) != 0u) {
+                    const int q = m0 ? 0 : m1 ? 1 : m2 ? 2 : 3;
+                    const uint32_t mb = q == 0 ? m0 : q == 1 ? m1 : q == 2 ? m2 : m3;
+                    const uint32_t nb = mb & (mb - 1u);
+                    m0 = q == 0 ? nb : m0; m1 = q == 1 ? nb : m1; m2 = q == 2 ? nb : m2; m3 = q == 3 ? nb : m3;
+                    const int t = __builtin_ctz(mb);
+                    const int o = us + 32 * q + 4 * (t & 7) + (t >> 3);
+                    if (o >= o0 && o < o1 && (cand < 0 || o < cand) && plausible(ts, o)) cand = o;
+                }
             }
-            uint64_t mn = cand >= 0 ? (uint64_t)(lo + cand) : NONE;
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) {
-                const uint64_t o = __shfl_xor(mn, d, 64);
-                mn = o < mn ? o : mn;
-            }
-            mn = uni64(mn);
+            KVR_STAMP(12);
+            const uint64_t fnd = __ballot(cand >= 0);
+            const uint64_t mn = fnd == 0ull ? NONE : (uint64_t)(lo + (int64_t)rl32((uint32_t)cand, (int)__builtin_ctzll(fnd)));
             if (mn != NONE) { entry = mn; search = false; stripe_entry = mn; }
+            KVR_STAMP(13);
         }
         const bool walk = in_stripe && !search && entry < vhi;
         uint64_t tile_exit = entry;
