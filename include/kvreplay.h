@@ -136,6 +136,31 @@ int  kvr_replay(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint32_t f
 
 int  kvr_last_stats(const kvr_ctx *ctx, kvr_stats *out);
 
+/* ---- streamed ingest: host segments larger than one transfer ----------
+ * The same loop as kvr_replay (engine.rs:55-57) over host-resident segment bytes, e.g. files
+ * read (engine.rs:80-83) into memory: consecutive segments are grouped into batches of at most
+ * batch_bytes (a larger segment is a batch of its own; 0 = 1 GiB).  While batch b replays, batch
+ * b+1 is copied host -> HBM on a second stream into the other of two device slots, so the PCIe
+ * transfer and the replay overlap.  With KVR_HOST_PINNED the caller's buffers are pinned
+ * (hipHostMalloc / hipHostRegister) and are DMA'd directly; otherwise the library stages them
+ * through two pinned buffers of its own.  Output, errors, expected_crc and return codes are
+ * exactly those of kvr_replay over the same segs (tuples in (segment, offset) order, seg_idx
+ * into segs[]); out is host memory.  kvr_last_stats sums the per-batch device statistics. */
+#define KVR_HOST_PINNED         0x8u  /* kvr_replay_stream: segs[i].bytes are pinned host memory */
+
+typedef struct kvr_stream_stats {
+    double   ms_wall;     /* host wall time of the whole call: transfers + replays + tuple copies */
+    double   ms_device;   /* sum of the batches' device pipelines (kvr_stats.ms_total)            */
+    uint64_t bytes_in;    /* segment bytes                                                        */
+    uint64_t n_records;   /* tuples produced                                                      */
+    uint64_t n_batches;
+} kvr_stream_stats;
+
+int  kvr_replay_stream(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint32_t flags, uint64_t batch_bytes,
+                       const uint32_t *expected_crc, size_t n_expected,
+                       kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err);
+int  kvr_last_stream_stats(const kvr_ctx *ctx, kvr_stream_stats *out);
+
 /* Host helpers. */
 const char *kvr_strerror(int code);
 /* CRC-32/ISO-HDLC, identical to crc32fast::hash (storage.rs:27) when crc == 0. */

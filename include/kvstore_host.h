@@ -44,6 +44,11 @@ int kvh_parse_u64(const char *s, size_t n, uint64_t *out);
  * SET of its key.  Returns the number of live keys (stats().num_keys) and *total_bytes
  * (stats().total_bytes, engine.rs:253-255). */
 uint64_t kvh_fold(const kvr_segment *segs, const kvr_tuple *t, size_t n, uint8_t *live, uint64_t *total_bytes);
+/* The same fold on n_threads host threads (0 = all cores): keys are split by
+ * key_tag into one partition per thread (the last writer of a key is its maximal (segment,
+ * offset) record, so partitions fold independently).  Same results as kvh_fold. */
+uint64_t kvh_fold_parallel(const kvr_segment *segs, const kvr_tuple *t, size_t n, uint32_t n_threads,
+                           uint8_t *live, uint64_t *total_bytes);
 
 typedef struct kvs_store kvs_store;
 

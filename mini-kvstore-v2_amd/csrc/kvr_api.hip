@@ -10,10 +10,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include <hipcub/hipcub.hpp>
@@ -89,6 +91,14 @@ struct kvr_ctx {
     uint64_t pool_hint = 0;
     uint32_t tps_override = 0;
     kvr_stats stats{};
+    // streamed ingest (kvr_replay_stream): two HBM batch slots filled on a copy stream, two pinned
+    // staging slots for pageable callers
+    hipStream_t copy = nullptr;
+    hipEvent_t ev_copy[2] = {};
+    DevBuf<uint8_t> slot[2];
+    uint8_t *h_stage[2] = {};
+    uint64_t h_stage_cap[2] = {};
+    kvr_stream_stats sstats{};
 };
 
 #define HIPCHK(x)                                   \
@@ -239,6 +249,13 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->c_gidx.release(); c->c_own.release(); c->c_sidx.release(); c->c_val.release(); c->c_scan.release();
     c->c_gstart.release(); c->c_hdr.release(); c->c_keys.release(); c->r_rep.release(); c->r_slot.release();
     c->r_best.release(); c->r_hk.release();
+    if (c->copy) (void)hipStreamSynchronize(c->copy);
+    for (int i = 0; i < 2; ++i) {
+        c->slot[i].release();
+        if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
+        if (c->ev_copy[i]) (void)hipEventDestroy(c->ev_copy[i]);
+    }
+    if (c->copy) (void)hipStreamDestroy(c->copy);
     if (c->h_link) (void)hipHostFree(c->h_link);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
@@ -799,6 +816,173 @@ int kvr_gen_segment_device(kvr_ctx *c, const kvr_gen_params *p, uint64_t seg_no,
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipStreamSynchronize(st));
+    return KVR_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// streamed ingest: host segments -> HBM in batches on a copy stream, the
+// transfer of batch b+1 overlapping the replay of batch b (engine.rs:55-57 over host bytes)
+// ---------------------------------------------------------------------------------------
+namespace {
+struct StreamBatch {
+    size_t s0, s1;     // segments [s0, s1)
+    uint64_t bytes;    // padded bytes in the HBM slot
+    uint64_t raw;      // segment bytes
+};
+}  // namespace
+
+// Fill HBM slot k with batch b on the copy stream (runs on a helper thread while the caller's
+// thread replays the previous batch).  Pageable bytes go through pinned staging slot k first,
+// one segment at a time, so the memcpy of segment i+1 overlaps the DMA of segment i.
+static int stream_fill(kvr_ctx *c, const kvr_segment *segs, const StreamBatch &b, int k, uint32_t flags) {
+    HIPCHK(hipSetDevice(c->device));
+    const bool pinned = (flags & KVR_HOST_PINNED) != 0;
+    uint64_t off = 0;
+    for (size_t i = b.s0; i < b.s1; ++i) {
+        const uint64_t len = segs[i].len;
+        if (len) {
+            const uint8_t *src = segs[i].bytes;
+            if (!pinned) {
+                memcpy(c->h_stage[k] + off, src, len);
+                src = c->h_stage[k] + off;
+            }
+            HIPCHK(hipMemcpyAsync(c->slot[k].p + off, src, len, hipMemcpyHostToDevice, c->copy));
+        }
+        off += (len + 255) & ~255ull;
+    }
+    HIPCHK(hipEventRecord(c->ev_copy[k], c->copy));
+    return KVR_OK;
+}
+
+extern "C" {
+
+int kvr_replay_stream(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, uint64_t batch_bytes,
+                      const uint32_t *expected, size_t n_expected, kvr_tuple *out, size_t cap, size_t *n_out,
+                      kvr_error *err) {
+    if (!c || (!segs && n) || !n_out || (cap && !out)) return KVR_EINVAL;
+    if (flags & ~KVR_HOST_PINNED) return KVR_EINVAL;   // host bytes in, host tuples out
+    if (err) memset(err, 0, sizeof(*err));
+    *n_out = 0;
+    memset(&c->sstats, 0, sizeof(c->sstats));
+    memset(&c->stats, 0, sizeof(c->stats));
+    if (n == 0) return KVR_OK;
+    if (n >= 0xFFFFFFFFull) return KVR_EINVAL;
+    for (size_t i = 0; i < n; ++i) {
+        if (i && segs[i].seg_id < segs[i - 1].seg_id) return KVR_EINVAL;   // caller sorts (engine.rs:51)
+        if (segs[i].len && !segs[i].bytes) return KVR_EINVAL;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    if (batch_bytes == 0) batch_bytes = 1ull << 30;
+    // batches: consecutive segments while their padded sizes fit batch_bytes (a larger segment
+    // is a batch of its own)
+    std::vector<StreamBatch> bs;
+    StreamBatch cur{0, 0, 0, 0};
+    uint64_t slot_need = 256;
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t padded = (segs[i].len + 255) & ~255ull;
+        if (cur.s1 > cur.s0 && cur.bytes + padded > batch_bytes) {
+            bs.push_back(cur);
+            cur = StreamBatch{i, i, 0, 0};
+        }
+        cur.s1 = i + 1;
+        cur.bytes += padded;
+        cur.raw += segs[i].len;
+        slot_need = std::max(slot_need, cur.bytes);
+    }
+    bs.push_back(cur);
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->copy) {
+        HIPCHK(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+        for (auto &e : c->ev_copy) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    for (int k = 0; k < 2 && k < (int)bs.size(); ++k) {
+        if (c->slot[k].ensure(slot_need)) return KVR_ENOMEM;
+        if (!(flags & KVR_HOST_PINNED) && c->h_stage_cap[k] < slot_need) {
+            if (c->h_stage[k]) (void)hipHostFree(c->h_stage[k]);
+            c->h_stage[k] = nullptr;
+            c->h_stage_cap[k] = 0;
+            if (hipHostMalloc(reinterpret_cast<void **>(&c->h_stage[k]), slot_need) != hipSuccess) {
+                c->h_stage[k] = nullptr;
+                return KVR_ENOMEM;
+            }
+            c->h_stage_cap[k] = slot_need;
+        }
+    }
+    auto drain = [&](int rc) {
+        (void)hipStreamSynchronize(c->copy);
+        return rc;
+    };
+    int rc = stream_fill(c, segs, bs[0], 0, flags);
+    if (rc != KVR_OK) return drain(rc);
+    kvr_stats tot{};
+    size_t done = 0;   // tuples of the finished batches (counted on past cap: the required size)
+    std::vector<kvr_segment> loc;
+    for (size_t b = 0; b < bs.size(); ++b) {
+        const int k = (int)(b & 1);
+        const StreamBatch &B = bs[b];
+        // the replay of batch b waits for its transfer on the device, not on the host
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_copy[k], 0));
+        int rc_next = KVR_OK;
+        std::thread filler;
+        if (b + 1 < bs.size())   // slot k^1 held batch b-1, whose replay has returned
+            filler = std::thread([&, b, k] { rc_next = stream_fill(c, segs, bs[b + 1], k ^ 1, flags); });
+        loc.resize(B.s1 - B.s0);
+        uint64_t off = 0;
+        for (size_t j = 0; j < loc.size(); ++j) {
+            const kvr_segment &s = segs[B.s0 + j];
+            loc[j] = kvr_segment{s.seg_id, c->slot[k].p + off, s.len};
+            off += (s.len + 255) & ~255ull;
+        }
+        // expected CRCs are per record in tuple order; a batch holds at most raw/5 + 1 records
+        const size_t e0 = std::min(done, n_expected);
+        const size_t ne = expected ? std::min<uint64_t>(n_expected - e0, B.raw / 5 + 1) : 0;
+        const size_t room = done < cap ? cap - done : 0;
+        size_t nb = 0;
+        kvr_error e{};
+        rc = kvr_replay(c, loc.data(), loc.size(), KVR_SEGS_ON_DEVICE, ne ? expected + e0 : nullptr, ne,
+                        room ? out + done : nullptr, room, &nb, &e);
+        if (filler.joinable()) filler.join();
+        tot.ms_total += c->stats.ms_total;
+        tot.ms_replay += c->stats.ms_replay;
+        tot.ms_link += c->stats.ms_link;
+        tot.ms_compact += c->stats.ms_compact;
+        tot.bytes_in += c->stats.bytes_in;
+        tot.n_records += c->stats.n_records;
+        tot.n_crc_fail += c->stats.n_crc_fail;
+        tot.n_stripes += c->stats.n_stripes;
+        tot.n_tiles += c->stats.n_tiles;
+        tot.n_redo += c->stats.n_redo;
+        tot.n_link_passes += c->stats.n_link_passes;
+        if (rc == KVR_CORRUPTED) {   // batches run in (segment, offset) order: this is the first error
+            if (err) {
+                *err = e;
+                err->seg_idx += (uint32_t)B.s0;
+            }
+            return drain(rc);
+        }
+        if (rc != KVR_OK && rc != KVR_CAPACITY) return drain(rc);
+        if (B.s0) {   // seg_idx into the caller's segs[]
+            const size_t m = std::min(nb, room);
+            for (size_t t = 0; t < m; ++t) out[done + t].seg_idx += (uint32_t)B.s0;
+        }
+        done += nb;
+        if (rc_next != KVR_OK) return drain(rc_next);
+    }
+    c->stats = tot;
+    *n_out = done;
+    c->sstats.n_batches = bs.size();
+    c->sstats.bytes_in = tot.bytes_in;
+    c->sstats.n_records = done;
+    c->sstats.ms_device = tot.ms_total;
+    c->sstats.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return done > cap ? KVR_CAPACITY : KVR_OK;
+}
+
+int kvr_last_stream_stats(const kvr_ctx *c, kvr_stream_stats *out) {
+    if (!c || !out) return KVR_EINVAL;
+    *out = c->sstats;
     return KVR_OK;
 }
 

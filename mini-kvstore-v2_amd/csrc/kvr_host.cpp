@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -199,6 +200,82 @@ uint64_t kvh_fold(const kvr_segment *segs, const kvr_tuple *t, size_t n, uint8_t
     }
     if (total_bytes) *total_bytes = tb;
     return nk;
+}
+
+// Parallel fold: the last writer of a key is its maximal (segment, offset)
+// record, so the keys can be split by hash into independent partitions.  Phase 1 counts each
+// chunk's tuples per partition, phase 2 scatters the tuple indices partition-major (chunk order
+// kept, so each partition stays in (segment, offset) order), phase 3 folds every partition into
+// its own open-addressing table (key_tag as the hash, key bytes compared on a tag match).
+uint64_t kvh_fold_parallel(const kvr_segment *segs, const kvr_tuple *t, size_t n, uint32_t n_threads,
+                           uint8_t *live, uint64_t *total_bytes) {
+    if (total_bytes) *total_bytes = 0;
+    if (n == 0) return 0;
+    if (n_threads == 0) n_threads = std::max(1u, std::thread::hardware_concurrency());
+    n_threads = std::min<uint32_t>(n_threads, 256);
+    if (n >= 0xFFFFFFFFull || n_threads == 1) return kvh_fold(segs, t, n, live, total_bytes);
+    const uint32_t P = n_threads;                       // one partition per thread
+    const size_t chunk = (n + P - 1) / P;
+    auto part = [P](uint32_t tag) { return (uint32_t)(((uint64_t)(tag * 0x9E3779B1u) * P) >> 32); };
+    std::vector<uint64_t> cnt((size_t)P * P, 0);         // cnt[chunk * P + partition]
+    std::vector<std::thread> th;
+    auto run = [&](auto fn) {
+        th.clear();
+        for (uint32_t w = 0; w < P; ++w) th.emplace_back(fn, w);
+        for (auto &x : th) x.join();
+    };
+    run([&](uint32_t c) {
+        const size_t a = std::min(n, c * chunk), b = std::min(n, a + chunk);
+        uint64_t *h = &cnt[(size_t)c * P];
+        for (size_t i = a; i < b; ++i) ++h[part(t[i].key_tag)];
+    });
+    std::vector<uint64_t> pstart(P + 1, 0), cur((size_t)P * P);
+    for (uint32_t p = 0; p < P; ++p) {
+        uint64_t s = pstart[p];
+        for (uint32_t c = 0; c < P; ++c) { cur[(size_t)c * P + p] = s; s += cnt[(size_t)c * P + p]; }
+        pstart[p + 1] = s;
+    }
+    std::vector<uint32_t> idx(n);
+    run([&](uint32_t c) {
+        const size_t a = std::min(n, c * chunk), b = std::min(n, a + chunk);
+        uint64_t *o = &cur[(size_t)c * P];
+        for (size_t i = a; i < b; ++i) idx[o[part(t[i].key_tag)]++] = (uint32_t)i;
+    });
+    if (live) memset(live, 0, n);
+    std::vector<uint64_t> nk(P, 0), tb(P, 0);
+    run([&](uint32_t p) {
+        const uint64_t a = pstart[p], b = pstart[p + 1];
+        if (a == b) return;
+        uint64_t cap = 16;
+        while (cap < 2 * (b - a)) cap <<= 1;
+        std::vector<uint32_t> slot(cap, 0xFFFFFFFFu);   // tuple index of the key's latest record
+        const uint64_t mask = cap - 1;
+        for (uint64_t j = a; j < b; ++j) {
+            const uint32_t i = idx[j];
+            const kvr_tuple &x = t[i];
+            const uint8_t *kp = segs[x.seg_idx].bytes + x.rec_off + 5;
+            for (uint64_t h = ((uint64_t)x.key_tag * 0x9E3779B97F4A7C15ull) >> 20;; ++h) {
+                uint32_t &s = slot[h & mask];
+                if (s == 0xFFFFFFFFu) { s = i; break; }
+                const kvr_tuple &y = t[s];
+                if (y.key_tag == x.key_tag && y.key_len == x.key_len &&
+                    memcmp(segs[y.seg_idx].bytes + y.rec_off + 5, kp, x.key_len) == 0) {
+                    s = i;                            // later record wins (engine.rs:137, :141)
+                    break;
+                }
+            }
+        }
+        for (uint32_t s : slot) {
+            if (s == 0xFFFFFFFFu || t[s].op != 0) continue;
+            if (live) live[s] = 1;
+            ++nk[p];
+            tb[p] += t[s].val_len;
+        }
+    });
+    uint64_t k = 0, bytes = 0;
+    for (uint32_t p = 0; p < P; ++p) { k += nk[p]; bytes += tb[p]; }
+    if (total_bytes) *total_bytes = bytes;
+    return k;
 }
 
 static int read_file(const std::string &path, std::vector<uint8_t> &out, int *os_err) {

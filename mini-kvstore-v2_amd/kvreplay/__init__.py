@@ -26,7 +26,7 @@ OK, CORRUPTED, CAPACITY = 0, 1, 2
 EINVAL, EHIP, EIO, ENOMEM = -1, -2, -3, -4
 E_NONE, E_OPEN, E_KEY_LEN, E_KEY, E_UTF8, E_VAL_LEN, E_VAL, E_OPCODE = range(8)
 KIND_NAMES = {0: "NONE", 1: "OPEN", 2: "KEY_LEN", 3: "KEY", 4: "UTF8", 5: "VAL_LEN", 6: "VAL", 7: "OPCODE"}
-SEGS_ON_DEVICE, OUT_ON_DEVICE, EXPECTED_ON_DEVICE = 0x1, 0x2, 0x4
+SEGS_ON_DEVICE, OUT_ON_DEVICE, EXPECTED_ON_DEVICE, HOST_PINNED = 0x1, 0x2, 0x4, 0x8
 TF_VERIFIED, TF_CRC_FAIL = 0x1, 0x2
 
 TUPLE_DTYPE = np.dtype([("rec_off", "<u8"), ("seg_idx", "<u4"), ("key_len", "<u4"), ("val_len", "<u4"),
@@ -48,6 +48,11 @@ class Stats(C.Structure):
                 ("ms_compact", C.c_double), ("bytes_in", C.c_uint64), ("n_records", C.c_uint64),
                 ("n_crc_fail", C.c_uint64), ("n_stripes", C.c_uint32), ("n_tiles", C.c_uint32),
                 ("n_redo", C.c_uint32), ("n_link_passes", C.c_uint32)]
+
+
+class StreamStats(C.Structure):
+    _fields_ = [("ms_wall", C.c_double), ("ms_device", C.c_double), ("bytes_in", C.c_uint64),
+                ("n_records", C.c_uint64), ("n_batches", C.c_uint64)]
 
 
 class GenParams(C.Structure):
@@ -97,6 +102,9 @@ def _load():
     rep.kvr_ctx_set_tiles_per_stripe.argtypes = [P, U32]
     rep.kvr_replay.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
     rep.kvr_last_stats.argtypes = [P, C.POINTER(Stats)]
+    rep.kvr_replay_stream.argtypes = [P, C.POINTER(Segment), SZ, U32, U64, P, SZ, P, SZ, C.POINTER(SZ),
+                                      C.POINTER(Error)]
+    rep.kvr_last_stream_stats.argtypes = [P, C.POINTER(StreamStats)]
     rep.kvr_compact.argtypes = [P, C.POINTER(Segment), SZ, U32, U64, P, U64, C.POINTER(U64), P, SZ, C.POINTER(SZ),
                                 C.POINTER(Error)]
     rep.kvr_last_compact_stats.argtypes = [P, C.POINTER(CompactStats)]
@@ -116,6 +124,8 @@ def _load():
     host.kvh_parse_u64.argtypes = [C.c_char_p, SZ, C.POINTER(U64)]
     host.kvh_fold.argtypes = [C.POINTER(Segment), P, SZ, P, C.POINTER(U64)]
     host.kvh_fold.restype = U64
+    host.kvh_fold_parallel.argtypes = [C.POINTER(Segment), P, SZ, U32, P, C.POINTER(U64)]
+    host.kvh_fold_parallel.restype = U64
     host.kvs_open.argtypes = [C.c_char_p, P, C.POINTER(P), C.POINTER(Error), C.c_char_p, SZ]
     host.kvs_get.argtypes = [P, P, SZ, C.POINTER(P), C.POINTER(SZ)]
     host.kvs_locate.argtypes = [P, P, SZ, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]
@@ -217,9 +227,19 @@ def discover(dirpath: str):
     return [(int(ids[i]), paths[i].decode()) for i in range(n.value)]
 
 
-def fold(segments, tuples):
-    """Native last-writer-wins fold: (live mask, num_keys, total_bytes)."""
+def fold(segments, tuples, threads=None, pinned=False):
+    """Native last-writer-wins fold: (live mask, num_keys, total_bytes).  threads=None runs
+    kvh_fold (one thread), else kvh_fold_parallel on that many threads (0 = all cores).
+    segments are bytes / uint8 arrays, or (ptr, len) host pairs with pinned=True."""
     _, host = _load()
+    if pinned:
+        segs = (Segment * max(len(segments), 1))(*[Segment(i, p, ln) for i, (p, ln) in enumerate(segments)])
+        t = np.ascontiguousarray(tuples, dtype=TUPLE_DTYPE)
+        live = np.zeros(max(len(t), 1), dtype=np.uint8)
+        tb = C.c_uint64()
+        nk = host.kvh_fold_parallel(segs, t.ctypes.data if len(t) else None, len(t), threads or 0,
+                                    live.ctypes.data, C.byref(tb))
+        return live[: len(t)].astype(bool), int(nk), int(tb.value)
     arrs = [np.ascontiguousarray(np.frombuffer(s, dtype=np.uint8) if isinstance(s, (bytes, bytearray)) else s)
             for s in segments]
     segs = (Segment * max(len(arrs), 1))(*[Segment(i, a.ctypes.data if a.size else None, a.size)
@@ -227,7 +247,11 @@ def fold(segments, tuples):
     t = np.ascontiguousarray(tuples, dtype=TUPLE_DTYPE)
     live = np.zeros(max(len(t), 1), dtype=np.uint8)
     tb = C.c_uint64()
-    nk = host.kvh_fold(segs, t.ctypes.data if len(t) else None, len(t), live.ctypes.data, C.byref(tb))
+    if threads is None:
+        nk = host.kvh_fold(segs, t.ctypes.data if len(t) else None, len(t), live.ctypes.data, C.byref(tb))
+    else:
+        nk = host.kvh_fold_parallel(segs, t.ctypes.data if len(t) else None, len(t), threads, live.ctypes.data,
+                                    C.byref(tb))
     return live[: len(t)].astype(bool), int(nk), int(tb.value)
 
 
@@ -338,6 +362,38 @@ class Context:
             raise NativeError(f"kvr_replay: {self._rep.kvr_strerror(rc).decode()} ({rc})")
         tuples = out_arr[: n_out.value] if out_arr is not None and rc == OK else None
         return ReplayResult(rc, tuples, n_out.value, err if rc == CORRUPTED else None, self.last_stats())
+
+    def replay_stream(self, segments, seg_ids=None, expected=None, cap=None, batch_bytes=0, pinned=False):
+        """Streamed ingest (kvr_replay_stream): host segments go to HBM in batches of batch_bytes
+        on a copy stream, overlapping the replay of the previous batch.  segments are bytes /
+        uint8 arrays, or (ptr, len) pairs of pinned host memory with pinned=True.  Returns
+        ReplayResult with the same tuples and errors as replay() on the same segments; the
+        streaming statistics are in .stream_stats."""
+        segs, keep, total = self._segments(segments, seg_ids, pinned)
+        flags = HOST_PINNED if pinned else 0
+        exp_ptr, n_exp = None, 0
+        if expected is not None:
+            e = np.ascontiguousarray(expected, dtype=np.uint32)
+            keep.append(e)
+            exp_ptr, n_exp = (e.ctypes.data if e.size else None), e.size
+        if cap is None:
+            cap = max(1024, total // 24 + len(segments))
+        out_arr = np.zeros(max(cap, 1), dtype=TUPLE_DTYPE)
+        n_out = C.c_size_t()
+        err = Error()
+        rc = self._rep.kvr_replay_stream(self.h, segs, len(segments), flags, batch_bytes, exp_ptr, n_exp,
+                                         out_arr.ctypes.data, cap, C.byref(n_out), C.byref(err))
+        if rc == CAPACITY:
+            return self.replay_stream(segments, seg_ids, expected, cap=n_out.value + 16, batch_bytes=batch_bytes,
+                                      pinned=pinned)
+        if rc < 0:
+            raise NativeError(f"kvr_replay_stream: {self._rep.kvr_strerror(rc).decode()} ({rc})")
+        ss = StreamStats()
+        self._rep.kvr_last_stream_stats(self.h, C.byref(ss))
+        tuples = out_arr[: n_out.value] if rc == OK else None
+        r = ReplayResult(rc, tuples, n_out.value, err if rc == CORRUPTED else None, self.last_stats())
+        r.stream_stats = ss
+        return r
 
     def _segments(self, segments, seg_ids, on_device):
         keep, n = [], len(segments)

@@ -145,6 +145,21 @@ def test_native_fold_matches_oracle_fold():
     assert np.array_equal(live_o, live_n)
 
 
+@pytest.mark.parametrize("threads", [0, 2, 3, 8, 17])
+def test_parallel_fold_matches_oracle_fold(threads):
+    # keys repeat across segments and partitions (2^10 ids, 40 % DEL, a DEL of an absent key)
+    spec = K.GenSpec(seed=99, seg_bytes=120_000, key_space_log2=10, val_min=0, val_max=300, del_permille=400)
+    segs = [K.gen_segment_cpu(spec, s)[0] for s in range(5)]
+    segs.append(np.frombuffer(b"\x01\x05\x00\x00\x00nokey", dtype=np.uint8))
+    rc, t, _ = O.replay(segs)
+    assert rc == 0
+    live_o, nk_o, tb_o = O.fold_live(segs, t)
+    live_p, nk_p, tb_p = K.fold(segs, t, threads=threads)
+    assert (nk_o, tb_o) == (nk_p, tb_p)
+    assert np.array_equal(live_o, live_p)
+    assert K.fold([], t[:0], threads=threads)[1:] == (0, 0)
+
+
 @pytest.mark.parametrize("s,v", [("0", 0), ("001", 1), ("+7", 7), ("18446744073709551615", 2 ** 64 - 1),
                                  ("18446744073709551616", None), ("", None), ("+", None), ("-1", None),
                                  (" 1", None), ("1a", None), ("++1", None)])

@@ -29,7 +29,7 @@ for s in $STEPS; do
       cat "$OUT/bench_cfg5.json" ;;
     prof)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-        python "$R/bench.py" --no-cpu > "$OUT/prof.log" 2>&1) || { echo "rocprof failed"; tail -20 "$OUT/prof.log"; exit 1; }
+        python "$R/bench.py" --no-cpu --no-stream > "$OUT/prof.log" 2>&1) || { echo "rocprof failed"; tail -20 "$OUT/prof.log"; exit 1; }
       find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \; ;;
     profc)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profc" -o run -- \
@@ -47,7 +47,7 @@ for s in $STEPS; do
       timeout -k 10 600 python -u tools/pmc_traffic.py > "$OUT/traffic.log" 2>&1 || { echo "traffic failed"; tail -20 "$OUT/traffic.log"; exit 1; }
       cp gpurun_out/pmc_traffic.json "$OUT/pmc_traffic.json" && tail -1 "$OUT/traffic.log" ;;
     pmc)
-      timeout -k 10 900 bash tools/pmc.sh "$OUT/pmc" --no-cpu --steps 2 --warmup 1 > "$OUT/pmc.txt" 2>&1 || { echo "pmc failed"; tail -20 "$OUT/pmc.txt"; exit 1; }
+      timeout -k 10 900 bash tools/pmc.sh "$OUT/pmc" --no-cpu --no-stream --steps 2 --warmup 1 > "$OUT/pmc.txt" 2>&1 || { echo "pmc failed"; tail -20 "$OUT/pmc.txt"; exit 1; }
       cat "$OUT/pmc.txt" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
