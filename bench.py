@@ -9,6 +9,9 @@ verify + ordered tuples left in HBM.  Weak scaling: rank r replays its own 64 se
 only for the barrier and the max-over-ranks timing).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5]
+  python bench.py --mode etag        batch ETag compute/verify in cfg3's volume-server
+                                     shape: 131072 blobs of 64 KiB (8 GiB) resident in HBM, one step =
+                                     one kvr_etag_batch (CRC-32 per blob + verify against stored ETags)
   python bench.py --mode compact     the compaction live-record rewrite on
                                      cfg4's per-GPU shard (50 % DEL): one step = one kvr_compact
                                      (replay + last-writer fold + gather of the live records into
@@ -45,7 +48,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default=None, choices=list(CONFIGS))
-    ap.add_argument("--mode", default="replay", choices=["replay", "compact"])
+    ap.add_argument("--mode", default="replay", choices=["replay", "compact", "etag"])
     ap.add_argument("--segments", type=int, default=0, help="override segments per GPU")
     ap.add_argument("--cpu-segs", type=int, default=16, help="CPU baseline sample (segments)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -69,6 +72,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.mode == "etag":
+        return bench_etag(args, K, torch, dev, world, rank)
 
     nseg, seg_bytes, kw, desc = CONFIGS[args.config]
     if args.segments:
@@ -338,6 +343,60 @@ def ctx_live(ctx):
     K.native()[0].kvr_last_compact_stats(ctx.h, C.byref(st))
     return int(st.n_live)
 
+
+
+def bench_etag(args, K, torch, dev, world, rank):
+    """kvr_etag_batch over 8 GiB of 64-KiB blobs in HBM (volume-server shape, cfg3), verified
+    against the stored ETags every step; a sample is checked against zlib.crc32 first."""
+    import zlib
+    import numpy as np
+    import torch.distributed as dist
+    n_blob, blob = 131072, 65536
+    ctx = K.Context(dev.index or 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x6B767265 + rank)
+    data = torch.randint(0, 256, (n_blob * blob,), dtype=torch.uint8, device=dev, generator=g)
+    offs = np.arange(n_blob, dtype=np.uint64) * blob
+    lens = np.full(n_blob, blob, dtype=np.uint64)
+    torch.cuda.synchronize()
+    stored, _, _ = ctx.etag_batch(data.data_ptr(), offs, lens, on_device=True, data_len=data.numel())
+    for i in (0, 1, n_blob // 2, n_blob - 1):
+        assert int(stored[i]) == zlib.crc32(data[i * blob:(i + 1) * blob].cpu().numpy().tobytes())
+    ms = []
+    for _ in range(args.warmup):
+        ctx.etag_batch(data.data_ptr(), offs, lens, expected=stored, on_device=True, data_len=data.numel())
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        crc, nf, st = ctx.etag_batch(data.data_ptr(), offs, lens, expected=stored, on_device=True,
+                                     data_len=data.numel())
+        assert nf == 0
+        ms.append((st.ms_chunk, st.ms_join))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        from kvreplay.shard import max_over_ranks
+        dt = max_over_ranks(dt)
+    total = n_blob * blob
+    mc = float(np.mean([a for a, _ in ms]))
+    mj = float(np.mean([b for _, b in ms]))
+    alg = total + 4 * (total // 4096) + 4 * n_blob      # blob bytes once + chunk registers + CRCs
+    res = {"metric": "batch ETag compute+verify GiB/s (SURVEY §8f rank 4)", "value": round(total * world * args.steps / dt / 2 ** 30, 3),
+           "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u8", "data": "synthetic (torch.randint on device, seeded)",
+           "config": {"workload": f"{n_blob} x 64 KiB blobs (8 GiB, volume-server shape) in HBM, CRC-32 + verify",
+                      "blobs_per_gpu": n_blob, "blob_bytes": blob},
+           "blobs_per_s": round(n_blob * world * args.steps / dt, 1),
+           "ms_kernel_chunk": round(mc, 4), "ms_kernel_join": round(mj, 4),
+           "roofline": {"bound": "hbm", "kernel": "k_etag_chunk", "achieved": round(alg / (mc / 1e3) / 1e9, 1),
+                        "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(alg / (mc / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
+                        "traffic": None, "alg_bytes_per_launch": alg}}
+    if rank == 0:
+        print(json.dumps(res))
+    ctx.close()
 
 if __name__ == "__main__":
     main()

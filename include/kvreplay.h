@@ -232,6 +232,30 @@ int  kvr_compact_resolve(kvr_ctx *ctx, const kvr_cand *d_hdr, const uint8_t *d_k
 int  kvr_compact_finish(kvr_ctx *ctx, const uint8_t *d_win, uint32_t flags, uint64_t seg_target, uint8_t *out,
                         uint64_t out_cap, uint64_t *out_len, uint64_t *seg_ends, size_t seg_cap, size_t *n_out_segs);
 
+/* ---- batch ETag compute / verify --------------------------------------
+ * crc_out[i] = crc32fast::hash(data[offs[i] .. offs[i] + lens[i]]) for n blobs of one buffer:
+ * the CRC-32/ISO-HDLC that BlobStorage::put renders as the blob's ETag
+ * (src/volume/storage.rs:27, format!("{:08x}", ...); kvr_etag_format renders it).  data is host
+ * memory, or device memory with KVR_SEGS_ON_DEVICE; crc_out is host memory, or device memory with
+ * KVR_OUT_ON_DEVICE; offs / lens are host arrays.  expected (optional; device memory with
+ * KVR_EXPECTED_ON_DEVICE): the stored ETags to verify against (a scrub); *n_fail (optional) =
+ * blobs whose CRC differs.  Blobs may overlap and sit at any byte offset.  Returns KVR_OK,
+ * KVR_EINVAL (a blob outside [0, data_len)) or < 0. */
+typedef struct kvr_etag_stats {
+    double   ms_chunk;    /* k_etag_chunk: per-4-KiB-chunk CRC registers (the byte pass)      */
+    double   ms_join;     /* k_etag_join: chunk registers -> CRC per blob, verification       */
+    uint64_t bytes;       /* blob bytes hashed                                                 */
+    uint64_t n_blobs;
+    uint64_t n_chunks;
+    uint64_t n_fail;
+} kvr_etag_stats;
+
+int  kvr_etag_batch(kvr_ctx *ctx, const uint8_t *data, uint64_t data_len, const uint64_t *offs, const uint64_t *lens,
+                    size_t n, uint32_t flags, const uint32_t *expected, uint32_t *crc_out, uint64_t *n_fail);
+int  kvr_last_etag_stats(const kvr_ctx *ctx, kvr_etag_stats *out);
+/* out[0..8] = the ETag text "{:08x}" of crc (lowercase hex) and a terminating NUL. */
+void kvr_etag_format(uint32_t crc, char *out);
+
 /* ---- synthetic segment generator (device side; byte-identical to kvh_gen_segment) -------- */
 typedef struct kvr_gen_params {
     uint64_t seed;

@@ -23,6 +23,7 @@
 #include "kvr_replay_kernel.hip"
 #include "kvr_kernels.hip"
 #include "kvr_compact.hip"
+#include "kvr_etag.hip"
 
 using namespace kvr;
 
@@ -99,6 +100,11 @@ struct kvr_ctx {
     uint8_t *h_stage[2] = {};
     uint64_t h_stage_cap[2] = {};
     kvr_stream_stats sstats{};
+    // batch ETag (kvr_etag_batch)
+    DevBuf<uint32_t> e_x, e_cb, e_creg, e_out, e_exp;
+    DevBuf<uint64_t> e_cpre, e_offs, e_lens, e_fail;
+    DevBuf<uint8_t> e_data;
+    kvr_etag_stats estats{};
 };
 
 #define HIPCHK(x)                                   \
@@ -249,6 +255,8 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->c_gidx.release(); c->c_own.release(); c->c_sidx.release(); c->c_val.release(); c->c_scan.release();
     c->c_gstart.release(); c->c_hdr.release(); c->c_keys.release(); c->r_rep.release(); c->r_slot.release();
     c->r_best.release(); c->r_hk.release();
+    c->e_x.release(); c->e_cb.release(); c->e_creg.release(); c->e_out.release(); c->e_exp.release();
+    c->e_cpre.release(); c->e_offs.release(); c->e_lens.release(); c->e_fail.release(); c->e_data.release();
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     for (int i = 0; i < 2; ++i) {
         c->slot[i].release();
@@ -984,6 +992,108 @@ int kvr_last_stream_stats(const kvr_ctx *c, kvr_stream_stats *out) {
     if (!c || !out) return KVR_EINVAL;
     *out = c->sstats;
     return KVR_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// batch ETag compute / verify (kvr_etag.hip; SURVEY §8f rank 4, storage.rs:27)
+// ---------------------------------------------------------------------------------------
+extern "C" {
+
+int kvr_etag_batch(kvr_ctx *c, const uint8_t *data, uint64_t data_len, const uint64_t *offs, const uint64_t *lens,
+                   size_t n, uint32_t flags, const uint32_t *expected, uint32_t *crc_out, uint64_t *n_fail) {
+    if (!c || (n && (!offs || !lens || !crc_out)) || (data_len && !data)) return KVR_EINVAL;
+    if (flags & ~(KVR_SEGS_ON_DEVICE | KVR_OUT_ON_DEVICE | KVR_EXPECTED_ON_DEVICE)) return KVR_EINVAL;
+    memset(&c->estats, 0, sizeof(c->estats));
+    if (n_fail) *n_fail = 0;
+    if (n == 0) return KVR_OK;
+    if (n >= 0xFFFFFFFFull) return KVR_EINVAL;
+    std::vector<uint64_t> cpre(n + 1);
+    uint64_t nch = 0, bytes = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (offs[i] > data_len || lens[i] > data_len - offs[i]) return KVR_EINVAL;   // blob outside data
+        cpre[i] = nch;
+        nch += (lens[i] + ETAG_CH - 1) / ETAG_CH;
+        bytes += lens[i];
+    }
+    cpre[n] = nch;
+    if (nch >= 0xFFFFFFFFull) return KVR_EINVAL;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    if (!c->e_x.p) {   // XT[t] = x^(8t) for t <= CH, XC[l] = x^(8 l CH) for l < 64, x^(8 * 64 CH)
+        std::vector<uint32_t> x(ETAG_NX);
+        x[0] = GF_ONE;
+        for (uint32_t t = 1; t <= ETAG_CH; ++t) x[t] = gf_mul(x[t - 1], 0x00800000u);
+        uint32_t *xc = x.data() + ETAG_CH + 1;
+        xc[0] = GF_ONE;
+        for (int l = 1; l <= 64; ++l) xc[l] = gf_mul(xc[l - 1], x[ETAG_CH]);
+        if (c->e_x.ensure(ETAG_NX)) return KVR_ENOMEM;
+        HIPCHK(hipMemcpyAsync(c->e_x.p, x.data(), ETAG_NX * 4, hipMemcpyHostToDevice, st));
+    }
+    const uint8_t *d_data = data;
+    if (!(flags & KVR_SEGS_ON_DEVICE)) {
+        if (c->e_data.ensure(data_len + 256)) return KVR_ENOMEM;
+        if (data_len) HIPCHK(hipMemcpyAsync(c->e_data.p, data, data_len, hipMemcpyHostToDevice, st));
+        d_data = c->e_data.p;
+    }
+    if (c->e_cpre.ensure(n + 1) || c->e_offs.ensure(n) || c->e_lens.ensure(n) || c->e_cb.ensure(nch) ||
+        c->e_creg.ensure(nch) || c->e_fail.ensure(1))
+        return KVR_ENOMEM;
+    HIPCHK(hipMemcpyAsync(c->e_cpre.p, cpre.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->e_offs.p, offs, n * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->e_lens.p, lens, n * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(c->e_fail.p, 0, 8, st));
+    uint32_t *d_out = crc_out;
+    if (!(flags & KVR_OUT_ON_DEVICE)) {
+        if (c->e_out.ensure(n)) return KVR_ENOMEM;
+        d_out = c->e_out.p;
+    }
+    const uint32_t *d_exp = expected;
+    if (expected && !(flags & KVR_EXPECTED_ON_DEVICE)) {
+        if (c->e_exp.ensure(n)) return KVR_ENOMEM;
+        HIPCHK(hipMemcpyAsync(c->e_exp.p, expected, n * 4, hipMemcpyHostToDevice, st));
+        d_exp = c->e_exp.p;
+    }
+    const uint32_t mgrid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 65536);
+    hipLaunchKernelGGL(k_etag_map, dim3(mgrid), dim3(256), 0, st, c->e_cpre.p, (uint64_t)n, c->e_cb.p);
+    HIPCHK(hipEventRecord(c->ev[0], st));
+    if (nch) {
+        const uint64_t g = (nch + ETAG_WPB - 1) / ETAG_WPB;
+        hipLaunchKernelGGL(k_etag_chunk, dim3((uint32_t)g), dim3(64 * ETAG_WPB), 0, st, d_data, data_len, c->e_offs.p,
+                           c->e_lens.p, c->e_cpre.p, c->e_cb.p, nch, c->crc.p, c->e_x.p, c->e_creg.p);
+    }
+    HIPCHK(hipEventRecord(c->ev[1], st));
+    hipLaunchKernelGGL(k_etag_join, dim3((uint32_t)((n + ETAG_WPB - 1) / ETAG_WPB)), dim3(64 * ETAG_WPB), 0, st,
+                       c->e_lens.p, c->e_cpre.p, (uint64_t)n, c->e_creg.p, c->e_x.p, d_exp, d_out,
+                       reinterpret_cast<unsigned long long *>(c->e_fail.p));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[2], st));
+    uint64_t fails = 0;
+    HIPCHK(hipMemcpyAsync(&fails, c->e_fail.p, 8, hipMemcpyDeviceToHost, st));
+    if (!(flags & KVR_OUT_ON_DEVICE)) HIPCHK(hipMemcpyAsync(crc_out, d_out, n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    float a = 0.f, b = 0.f;
+    (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
+    (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
+    c->estats.ms_chunk = a;
+    c->estats.ms_join = b;
+    c->estats.bytes = bytes;
+    c->estats.n_blobs = n;
+    c->estats.n_chunks = nch;
+    c->estats.n_fail = expected ? fails : 0;
+    if (n_fail) *n_fail = c->estats.n_fail;
+    return KVR_OK;
+}
+
+int kvr_last_etag_stats(const kvr_ctx *c, kvr_etag_stats *out) {
+    if (!c || !out) return KVR_EINVAL;
+    *out = c->estats;
+    return KVR_OK;
+}
+
+void kvr_etag_format(uint32_t crc, char *out) {
+    if (out) snprintf(out, 9, "%08x", crc);
 }
 
 }  // extern "C"

@@ -55,6 +55,11 @@ class StreamStats(C.Structure):
                 ("n_records", C.c_uint64), ("n_batches", C.c_uint64)]
 
 
+class EtagStats(C.Structure):
+    _fields_ = [("ms_chunk", C.c_double), ("ms_join", C.c_double), ("bytes", C.c_uint64),
+                ("n_blobs", C.c_uint64), ("n_chunks", C.c_uint64), ("n_fail", C.c_uint64)]
+
+
 class GenParams(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("seg_bytes", C.c_uint64), ("key_space_log2", C.c_uint32),
                 ("key_dist", C.c_uint32), ("val_min", C.c_uint32), ("val_max", C.c_uint32),
@@ -105,6 +110,10 @@ def _load():
     rep.kvr_replay_stream.argtypes = [P, C.POINTER(Segment), SZ, U32, U64, P, SZ, P, SZ, C.POINTER(SZ),
                                       C.POINTER(Error)]
     rep.kvr_last_stream_stats.argtypes = [P, C.POINTER(StreamStats)]
+    rep.kvr_etag_batch.argtypes = [P, P, U64, P, P, SZ, U32, P, P, C.POINTER(U64)]
+    rep.kvr_last_etag_stats.argtypes = [P, C.POINTER(EtagStats)]
+    rep.kvr_etag_format.argtypes = [U32, C.c_char_p]
+    rep.kvr_etag_format.restype = None
     rep.kvr_compact.argtypes = [P, C.POINTER(Segment), SZ, U32, U64, P, U64, C.POINTER(U64), P, SZ, C.POINTER(SZ),
                                 C.POINTER(Error)]
     rep.kvr_last_compact_stats.argtypes = [P, C.POINTER(CompactStats)]
@@ -171,6 +180,14 @@ def crc32(data: bytes, crc: int = 0) -> int:
     rep, _ = _load()
     a = np.frombuffer(bytes(data), dtype=np.uint8)
     return int(rep.kvr_crc32(crc, a.ctypes.data if a.size else None, a.size))
+
+
+def etag_format(crc: int) -> str:
+    """The ETag text BlobStorage::put returns: format!("{:08x}", crc) (storage.rs:27)."""
+    rep, _ = _load()
+    buf = C.create_string_buffer(9)
+    rep.kvr_etag_format(crc, buf)
+    return buf.value.decode()
 
 
 # ---- generator ---------------------------------------------------------------------------------
@@ -394,6 +411,35 @@ class Context:
         r = ReplayResult(rc, tuples, n_out.value, err if rc == CORRUPTED else None, self.last_stats())
         r.stream_stats = ss
         return r
+
+    def etag_batch(self, data, offs, lens, expected=None, on_device=False, data_len=None):
+        """Batch ETag (kvr_etag_batch): CRC-32 of data[offs[i]:offs[i]+lens[i]] for every i.
+        data is bytes / a uint8 array, or a device pointer with on_device=True (then data_len).
+        Returns (crc uint32 array, n_fail, EtagStats)."""
+        if on_device:
+            dptr, dlen = data, data_len
+            keep = None
+        else:
+            keep = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else \
+                np.ascontiguousarray(data, dtype=np.uint8)
+            dptr, dlen = (keep.ctypes.data if keep.size else None), keep.size
+        o = np.ascontiguousarray(offs, dtype=np.uint64)
+        ln = np.ascontiguousarray(lens, dtype=np.uint64)
+        n = len(o)
+        out = np.zeros(max(n, 1), dtype=np.uint32)
+        ep = None
+        if expected is not None:
+            e = np.ascontiguousarray(expected, dtype=np.uint32)
+            ep = e.ctypes.data
+        nf = C.c_uint64()
+        rc = self._rep.kvr_etag_batch(self.h, dptr, dlen, o.ctypes.data if n else None, ln.ctypes.data if n else None,
+                                      n, SEGS_ON_DEVICE if on_device else 0, ep, out.ctypes.data, C.byref(nf))
+        if rc != OK:
+            raise NativeError(f"kvr_etag_batch: {self._rep.kvr_strerror(rc).decode()} ({rc})")
+        st = EtagStats()
+        self._rep.kvr_last_etag_stats(self.h, C.byref(st))
+        del keep
+        return out[:n], int(nf.value), st
 
     def _segments(self, segments, seg_ids, on_device):
         keep, n = [], len(segments)

@@ -27,6 +27,13 @@ for s in $STEPS; do
     bench5)
       timeout -k 10 300 python -u bench.py --config cfg5 --segments 16 --no-cpu > "$OUT/bench_cfg5.json" 2> "$OUT/bench_cfg5.err" || { echo "bench cfg5 failed"; tail -20 "$OUT/bench_cfg5.err"; exit 1; }
       cat "$OUT/bench_cfg5.json" ;;
+    etag)
+      timeout -k 10 300 python -u bench.py --mode etag > "$OUT/bench_etag.json" 2> "$OUT/bench_etag.err" || { echo "bench etag failed"; tail -20 "$OUT/bench_etag.err"; exit 1; }
+      cat "$OUT/bench_etag.json" ;;
+    profe)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profe" -o run -- \
+        python "$R/bench.py" --mode etag > "$OUT/profe.log" 2>&1) || { echo "rocprof etag failed"; tail -20 "$OUT/profe.log"; exit 1; }
+      find "$OUT/profe" -name '*kernel_stats.csv' -exec cat {} \; ;;
     prof)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
         python "$R/bench.py" --no-cpu --no-stream > "$OUT/prof.log" 2>&1) || { echo "rocprof failed"; tail -20 "$OUT/prof.log"; exit 1; }
