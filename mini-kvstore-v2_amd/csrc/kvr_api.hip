@@ -105,6 +105,7 @@ struct kvr_ctx {
     DevBuf<uint64_t> e_cpre, e_offs, e_lens, e_fail;
     DevBuf<uint8_t> e_data;
     kvr_etag_stats estats{};
+    uint32_t e_wg_per_cu = 0;
 };
 
 #define HIPCHK(x)                                   \
@@ -1028,8 +1029,15 @@ int kvr_etag_batch(kvr_ctx *c, const uint8_t *data, uint64_t data_len, const uin
         uint32_t *xc = x.data() + ETAG_CH + 1;
         xc[0] = GF_ONE;
         for (int l = 1; l <= 64; ++l) xc[l] = gf_mul(xc[l - 1], x[ETAG_CH]);
-        if (c->e_x.ensure(ETAG_NX)) return KVR_ENOMEM;
-        HIPCHK(hipMemcpyAsync(c->e_x.p, x.data(), ETAG_NX * 4, hipMemcpyHostToDevice, st));
+        // KL: per lane, nibble tables of the full-chunk lane shift x^(8 (CH - 64 (lane + 1)))
+        x.resize(ETAG_NX + ETAG_NKL);
+        for (uint32_t l = 0; l < 64; ++l)
+            for (uint32_t i = 0; i < 8; ++i)
+                for (uint32_t nb = 0; nb < 16; ++nb)
+                    x[ETAG_NX + l * 128 + i * 16 + nb] = gf_mul(nb << (4 * i), x[ETAG_CH - 64 * (l + 1)]);
+        if (c->e_x.ensure(x.size())) return KVR_ENOMEM;
+        HIPCHK(hipMemcpyAsync(c->e_x.p, x.data(), x.size() * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));   // x is a local
     }
     const uint8_t *d_data = data;
     if (!(flags & KVR_SEGS_ON_DEVICE)) {
@@ -1059,7 +1067,14 @@ int kvr_etag_batch(kvr_ctx *c, const uint8_t *data, uint64_t data_len, const uin
     hipLaunchKernelGGL(k_etag_map, dim3(mgrid), dim3(256), 0, st, c->e_cpre.p, (uint64_t)n, c->e_cb.p);
     HIPCHK(hipEventRecord(c->ev[0], st));
     if (nch) {
-        const uint64_t g = (nch + ETAG_WPB - 1) / ETAG_WPB;
+        const uint64_t per = (uint64_t)ETAG_WPB * ETAG_NC;
+        if (!c->e_wg_per_cu) {   // persistent grid: exactly the resident workgroups
+            int occ = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_etag_chunk, 64 * ETAG_WPB, 0) != hipSuccess || occ < 1)
+                occ = 1;
+            c->e_wg_per_cu = (uint32_t)occ;
+        }
+        const uint64_t g = std::min<uint64_t>((nch + per - 1) / per, (uint64_t)c->n_cu * c->e_wg_per_cu);
         hipLaunchKernelGGL(k_etag_chunk, dim3((uint32_t)g), dim3(64 * ETAG_WPB), 0, st, d_data, data_len, c->e_offs.p,
                            c->e_lens.p, c->e_cpre.p, c->e_cb.p, nch, c->crc.p, c->e_x.p, c->e_creg.p);
     }

@@ -3,10 +3,12 @@
  * blobs in one launch, the value BlobStorage::put renders as its ETag
  * (src/volume/storage.rs:27: format!("{:08x}", crc32fast::hash(data))).
  *
- * A blob is cut into 4-KiB chunks; one wave per chunk, one 64-B unit per lane:
+ * A blob is cut into 4-KiB chunks, one 64-B unit per lane; a persistent wave takes 4 chunks per
+ * round and runs their CRC chains interleaved:
  *   lane register  u_l = CRC register over the lane's bytes (slice-by-4 from LDS), starting at
  *                  0xFFFFFFFF for lane 0 of a blob's first chunk and at 0 everywhere else
- *   chunk register r_j = XOR_l u_l * x^(8 * bytes after lane l in the chunk)   (wave XOR reduce)
+ *   chunk register r_j = XOR_l u_l * x^(8 * bytes after lane l in the chunk)   (wave XOR reduce;
+ *                  the per-lane multiply by nibble tables in LDS for full chunks)
  * and one wave per blob then joins its chunks (k_etag_join):
  *   register R = (XOR_{k} r_{nch-2-k} * x^(8 k CH)) * x^(8 lastlen)  ^  r_{nch-1}
  *   crc        = R ^ 0xFFFFFFFF
@@ -19,7 +21,9 @@ namespace kvr {
 
 constexpr uint32_t ETAG_CH = 4096;           // chunk bytes (64 lanes x 64 B)
 constexpr uint32_t ETAG_WPB = 4;             // waves per workgroup
-constexpr uint32_t ETAG_NX = ETAG_CH + 1 + 64 + 1;   // XT[0..CH], XC[0..63], X(64 CH)
+constexpr uint32_t ETAG_NC = 4;              // chunks per wave and round (interleaved CRC chains)
+constexpr uint32_t ETAG_NX = ETAG_CH + 1 + 64 + 1;   // XT[0..CH], XC[0..63], X(64 CH); then KL
+constexpr uint32_t ETAG_NKL = 64 * 128;             // KL[lane][i][n]: nibble tables of XT[CH - 64 (lane+1)]
 
 // chunk -> blob map: blob v owns chunks [cpre[v], cpre[v+1])
 __global__ void k_etag_map(const uint64_t *__restrict__ cpre, uint64_t n, uint32_t *__restrict__ chunk_blob) {
@@ -36,6 +40,43 @@ __device__ inline uint32_t crc_byte(const uint32_t *T, uint32_t c, uint32_t b) {
     return (c >> 8) ^ T[(c ^ b) & 255u];
 }
 
+// a * K_lane by nibble tables: K[i * 16 + n] = (n << 4i) * K_lane  (8 lookups, no bit loop)
+__device__ inline uint32_t kmul_nib(const uint32_t *K, uint32_t a) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r ^= K[i * 16 + ((a >> (4 * i)) & 15u)];
+    return r;
+}
+
+// One chunk through the general path: any alignment, partial units, bounds-checked loads.
+__device__ inline uint32_t etag_unit_general(const uint32_t *T, const uint8_t *data, uint64_t data_len, uint64_t start,
+                                             uint32_t clen, uint32_t lane, uint32_t reg, const uint32_t *xt) {
+    const uint32_t u0 = lane * 64u;
+    if (u0 >= clen) return 0u;
+    const uint32_t ul = min(64u, clen - u0);
+    const uint32_t after = clen - (u0 + ul);
+    const uint8_t *p = data + start + u0;
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3u);
+    const uint64_t rel = start + u0;
+    uint32_t k = 0;
+    if (mis == 0) {
+        for (; k + 4 <= ul; k += 4) reg = crc_word4(T, reg, *reinterpret_cast<const uint32_t *>(p + k));
+    } else if (rel >= mis && rel - mis + ((ul + mis + 3u) & ~3u) <= data_len) {
+        // dwords from the aligned-down window while it stays inside the buffer
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(p - mis);
+        uint32_t lo = q[0];
+        for (uint32_t i = 1; k + 4 <= ul; ++i, k += 4) {
+            const uint32_t hi = q[i];
+            reg = crc_word4(T, reg, __builtin_amdgcn_alignbyte(hi, lo, mis));
+            lo = hi;
+        }
+    }
+    for (; k < ul; ++k) reg = crc_byte(T, reg, p[k]);
+    return after ? gf_mul(reg, xt[after]) : reg;
+}
+
+// Persistent: as many workgroups as are resident (occupancy query); each wave takes ETAG_NC chunks per round and runs
+// their CRC chains interleaved (independent LDS lookup chains hide each other's latency).
 __global__ __launch_bounds__(64 * ETAG_WPB) void k_etag_chunk(const uint8_t *__restrict__ data, uint64_t data_len,
                                                              const uint64_t *__restrict__ offs,
                                                              const uint64_t *__restrict__ lens,
@@ -44,62 +85,72 @@ __global__ __launch_bounds__(64 * ETAG_WPB) void k_etag_chunk(const uint8_t *__r
                                                              const uint32_t *__restrict__ crc_tab,
                                                              const uint32_t *__restrict__ xt,
                                                              uint32_t *__restrict__ creg) {
-    __shared__ uint32_t T[1024];   // slice-by-4: T[t * 256 + b] = byte b pushed through t zero bytes
+    __shared__ uint32_t T[1024];          // slice-by-4: T[t * 256 + b] = byte b pushed through t zero bytes
+    __shared__ uint32_t KL[64 * 128];     // per lane: nibble tables of x^(8 (4096 - 64 (lane + 1)))
     for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) T[i] = crc_tab[i];
+    for (uint32_t i = threadIdx.x; i < 64 * 128; i += blockDim.x) KL[i] = xt[ETAG_NX + i];
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t c = blockIdx.x * (uint64_t)ETAG_WPB + (threadIdx.x >> 6);
-    if (c >= n_chunks) return;
-    const uint32_t v = chunk_blob[c];
-    const uint64_t j = c - cpre[v];
-    const uint64_t len = lens[v];
-    const uint64_t start = offs[v] + j * ETAG_CH;
-    const uint32_t clen = (uint32_t)min<uint64_t>(ETAG_CH, len - j * ETAG_CH);
-    const uint32_t u0 = lane * 64u;
-    uint32_t reg = (j == 0 && lane == 0) ? 0xFFFFFFFFu : 0u;
-    uint32_t after = 0;
-    if (u0 < clen) {
-        const uint32_t ul = min(64u, clen - u0);
-        after = clen - (u0 + ul);
-        const uint8_t *p = data + start + u0;
-        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-        if (ul == 64 && (a & 15u) == 0) {           // aligned full unit: 4 x 16-B loads
-            const uint4 *q = reinterpret_cast<const uint4 *>(p);
-            uint4 w[4];
+    const uint32_t *K = KL + lane * 128;
+    const uint64_t waves = (uint64_t)gridDim.x * ETAG_WPB;
+    for (uint64_t base = (blockIdx.x * (uint64_t)ETAG_WPB + (threadIdx.x >> 6)) * ETAG_NC; base < n_chunks;
+         base += waves * ETAG_NC) {
+        uint64_t start[ETAG_NC];
+        uint32_t clen[ETAG_NC], reg[ETAG_NC];
+        bool fast = true;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) w[i] = q[i];
+        for (int k = 0; k < ETAG_NC; ++k) {
+            const uint64_t c = base + k;
+            if (c < n_chunks) {
+                const uint32_t v = chunk_blob[c];
+                const uint64_t j = c - cpre[v];
+                start[k] = offs[v] + j * ETAG_CH;
+                clen[k] = (uint32_t)min<uint64_t>(ETAG_CH, lens[v] - j * ETAG_CH);
+                reg[k] = (j == 0 && lane == 0) ? 0xFFFFFFFFu : 0u;
+                fast = fast && clen[k] == ETAG_CH && ((reinterpret_cast<uintptr_t>(data) + start[k]) & 15u) == 0;
+            } else {
+                start[k] = 0;
+                clen[k] = 0;
+                reg[k] = 0;
+                fast = false;
+            }
+        }
+        if (fast) {   // ETAG_NC full aligned chunks: 4 x 16-B loads per lane and chunk, chains interleaved
+            uint4 w[ETAG_NC][4];
+#pragma unroll
+            for (int k = 0; k < ETAG_NC; ++k) {
+                const uint4 *q = reinterpret_cast<const uint4 *>(data + start[k] + lane * 64u);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[k][i] = q[i];
+            }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                reg = crc_word4(T, reg, w[i].x);
-                reg = crc_word4(T, reg, w[i].y);
-                reg = crc_word4(T, reg, w[i].z);
-                reg = crc_word4(T, reg, w[i].w);
+#pragma unroll
+                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].x);
+#pragma unroll
+                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].y);
+#pragma unroll
+                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].z);
+#pragma unroll
+                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].w);
+            }
+            if (lane != 63) {
+#pragma unroll
+                for (int k = 0; k < ETAG_NC; ++k) reg[k] = kmul_nib(K, reg[k]);
             }
         } else {
-            // unaligned or partial unit: dwords from the aligned-down window while it stays inside
-            // the buffer, then bytes
-            const uint32_t mis = (uint32_t)(a & 3u);
-            const uint64_t rel = (uint64_t)(p - data);
-            uint32_t k = 0;
-            if (mis == 0) {
-                for (; k + 4 <= ul; k += 4) reg = crc_word4(T, reg, *reinterpret_cast<const uint32_t *>(p + k));
-            } else if (rel - mis + ((ul + mis + 3u) & ~3u) <= data_len && rel >= mis) {
-                const uint32_t *q = reinterpret_cast<const uint32_t *>(p - mis);
-                uint32_t lo = q[0];
-                for (uint32_t i = 1; k + 4 <= ul; ++i, k += 4) {
-                    const uint32_t hi = q[i];
-                    reg = crc_word4(T, reg, __builtin_amdgcn_alignbyte(hi, lo, mis));
-                    lo = hi;
-                }
-            }
-            for (; k < ul; ++k) reg = crc_byte(T, reg, p[k]);
+#pragma unroll 1
+            for (int k = 0; k < ETAG_NC; ++k)
+                if (clen[k]) reg[k] = etag_unit_general(T, data, data_len, start[k], clen[k], lane, reg[k], xt);
         }
-        if (after) reg = gf_mul(reg, xt[after]);
-    }
-    // wave XOR reduction
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) reg ^= __shfl_xor(reg, o, 64);
-    if (lane == 0) creg[c] = reg;
+        for (int k = 0; k < ETAG_NC; ++k) {
+            uint32_t r = reg[k];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) r ^= __shfl_xor(r, o, 64);
+            if (lane == 0 && base + k < n_chunks) creg[base + k] = r;
+        }
+    }
 }
 
 // one wave per blob: join the chunk registers, finish the CRC, verify against expected
