@@ -121,8 +121,8 @@ void kvr_ctx_destroy(kvr_ctx *ctx);
  * restores the context's own stream. */
 int  kvr_ctx_set_stream(kvr_ctx *ctx, void *hip_stream);
 int  kvr_ctx_device(const kvr_ctx *ctx);
-/* Tiles (16 KiB each) per stripe, the unit of speculation; 0 = automatic (about 8 stripes per
- * compute unit).  Larger stripes mean fewer speculated entries, smaller ones more parallelism. */
+/* Tiles (8 KiB each) per stripe, the unit of speculation; 0 = automatic (one stripe per resident
+ * wave).  Larger stripes mean fewer speculated entries, smaller ones more parallelism. */
 int  kvr_ctx_set_tiles_per_stripe(kvr_ctx *ctx, uint32_t tiles);
 
 /* Replay n_segs segments (ascending seg_id) -> tuples in (segment, offset) order.

@@ -344,8 +344,10 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         total_tiles += g.n_tiles;
     }
     if (total_tiles >= 0xFFFFFFFFull) return KVR_EINVAL;
-    // one stripe per wave, two rounds of resident waves (k_replay: WPB stripes per workgroup)
-    const uint64_t target = (uint64_t)c->n_cu * (uint64_t)c->wg_per_cu * WPB * 2;
+    // one stripe per resident wave, one round (k_replay: WPB stripes per workgroup).  Measured
+    // (tools/tps_sweep.py): one round beats two by 5 % on cfg2 and 14 % on cfg5, and stripe counts
+    // between whole rounds leave a ragged tail
+    const uint64_t target = (uint64_t)c->n_cu * (uint64_t)c->wg_per_cu * WPB;
     const uint64_t tps = c->tps_override ? c->tps_override : std::max<uint64_t>(1, (total_tiles + target - 1) / target);
     c->h_stripes.clear();
     for (size_t i = 0; i < n; ++i) {
