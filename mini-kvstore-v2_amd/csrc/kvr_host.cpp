@@ -248,28 +248,35 @@ uint64_t kvh_fold_parallel(const kvr_segment *segs, const kvr_tuple *t, size_t n
         if (a == b) return;
         uint64_t cap = 16;
         while (cap < 2 * (b - a)) cap <<= 1;
-        std::vector<uint32_t> slot(cap, 0xFFFFFFFFu);   // tuple index of the key's latest record
+        // slot = key_tag << 32 | tuple index of the key's latest record: probes compare tags in
+        // the table and touch the tuple and the key bytes only on a tag match
+        constexpr uint64_t EMPTY = ~0ull;
+        std::vector<uint64_t> slot(cap, EMPTY);
         const uint64_t mask = cap - 1;
         for (uint64_t j = a; j < b; ++j) {
             const uint32_t i = idx[j];
             const kvr_tuple &x = t[i];
-            const uint8_t *kp = segs[x.seg_idx].bytes + x.rec_off + 5;
+            const uint64_t tag = (uint64_t)x.key_tag << 32;
             for (uint64_t h = ((uint64_t)x.key_tag * 0x9E3779B97F4A7C15ull) >> 20;; ++h) {
-                uint32_t &s = slot[h & mask];
-                if (s == 0xFFFFFFFFu) { s = i; break; }
-                const kvr_tuple &y = t[s];
-                if (y.key_tag == x.key_tag && y.key_len == x.key_len &&
-                    memcmp(segs[y.seg_idx].bytes + y.rec_off + 5, kp, x.key_len) == 0) {
-                    s = i;                            // later record wins (engine.rs:137, :141)
+                uint64_t &s = slot[h & mask];
+                if (s == EMPTY) { s = tag | i; break; }
+                if ((s & 0xFFFFFFFF00000000ull) != tag) continue;
+                const kvr_tuple &y = t[(uint32_t)s];
+                if (y.key_len == x.key_len &&
+                    memcmp(segs[y.seg_idx].bytes + y.rec_off + 5, segs[x.seg_idx].bytes + x.rec_off + 5,
+                           x.key_len) == 0) {
+                    s = tag | i;                      // later record wins (engine.rs:137, :141)
                     break;
                 }
             }
         }
-        for (uint32_t s : slot) {
-            if (s == 0xFFFFFFFFu || t[s].op != 0) continue;
-            if (live) live[s] = 1;
+        for (uint64_t s : slot) {
+            if (s == EMPTY) continue;
+            const kvr_tuple &y = t[(uint32_t)s];
+            if (y.op != 0) continue;
+            if (live) live[(uint32_t)s] = 1;
             ++nk[p];
-            tb[p] += t[s].val_len;
+            tb[p] += y.val_len;
         }
     });
     uint64_t k = 0, bytes = 0;
