@@ -136,6 +136,15 @@ int  kvr_replay(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint32_t f
 
 int  kvr_last_stats(const kvr_ctx *ctx, kvr_stats *out);
 
+/* ---- replay + last-writer fold on the device (SURVEY §8b dedup_last_writer) ----------------
+ * kvr_replay, then the fold of engine.rs:137 (insert) / :141 (remove) in HBM (the compaction's
+ * hash table over the key bytes): out receives only each live key's final SET tuple, in
+ * (segment, offset) order — the records the reference's HashMap holds after open — and
+ * *n_out = stats().num_keys (engine.rs:237-259).  Errors as kvr_replay; KVR_CAPACITY with the
+ * required count.  flags: KVR_SEGS_ON_DEVICE, KVR_OUT_ON_DEVICE. */
+int  kvr_replay_live(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint32_t flags,
+                     kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err);
+
 /* ---- streamed ingest: host segments larger than one transfer ----------
  * The same loop as kvr_replay (engine.rs:55-57) over host-resident segment bytes, e.g. files
  * read (engine.rs:80-83) into memory: consecutive segments are grouped into batches of at most

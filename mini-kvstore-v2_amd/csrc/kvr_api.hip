@@ -70,7 +70,7 @@ struct kvr_ctx {
     DevBuf<uint32_t> crc, kmul, initx;
     DevBuf<GenRecDev> gen;
     // compaction (kvr_compact)
-    DevBuf<kvr_tuple> ctup;
+    DevBuf<kvr_tuple> ctup, lout;
     DevBuf<uint32_t> ht_rep, ht_best, cslot, cflag, cpos, cfirst;
     DevBuf<uint64_t> csize, coff, l_src, l_off, ctot, ccuts;
     DevBuf<uint8_t> cout, ctmp;
@@ -250,7 +250,7 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->pool.release(); c->dense.release(); c->redo.release(); c->link.release(); c->ctr.release();
     c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->bsum.release();
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
-    c->ctup.release(); c->ht_rep.release(); c->ht_best.release(); c->cslot.release(); c->cflag.release();
+    c->ctup.release(); c->lout.release(); c->ht_rep.release(); c->ht_best.release(); c->cslot.release(); c->cflag.release();
     c->cpos.release(); c->cfirst.release(); c->csize.release(); c->coff.release(); c->l_src.release();
     c->l_off.release(); c->ctot.release(); c->ccuts.release(); c->cout.release(); c->ctmp.release();
     c->c_gidx.release(); c->c_own.release(); c->c_sidx.release(); c->c_val.release(); c->c_scan.release();
@@ -1111,6 +1111,59 @@ int kvr_last_etag_stats(const kvr_ctx *c, kvr_etag_stats *out) {
 
 void kvr_etag_format(uint32_t crc, char *out) {
     if (out) snprintf(out, 9, "%08x", crc);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// replay + last-writer fold in HBM: only the live index leaves the device (SURVEY §8b
+// dedup_last_writer; engine.rs:137 / :141)
+// ---------------------------------------------------------------------------------------
+namespace {
+__global__ void k_live_tuples(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ flag,
+                              const uint32_t *__restrict__ pos, kvr_tuple *__restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && flag[i]) out[pos[i]] = tup[i];
+}
+}  // namespace
+
+extern "C" {
+
+int kvr_replay_live(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, kvr_tuple *out, size_t cap,
+                    size_t *n_out, kvr_error *err) {
+    if (!c || (!segs && n) || !n_out || (cap && !out)) return KVR_EINVAL;
+    if (flags & ~(KVR_SEGS_ON_DEVICE | KVR_OUT_ON_DEVICE)) return KVR_EINVAL;
+    *n_out = 0;
+    size_t nt = 0;
+    int rc = compact_front(c, segs, n, flags, err, &nt);   // replay + k_fold_insert (kvr_compact.hip)
+    if (rc != KVR_OK || nt == 0) return rc;
+    hipStream_t st = c->stream;
+    const uint32_t g = (uint32_t)((nt + 255) / 256);
+    hipLaunchKernelGGL(k_live, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->ht_best.p, c->cslot.p,
+                       c->csize.p, c->cflag.p);
+    HIPCHK(hipGetLastError());
+    size_t tb = c->ctmp.n;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->cflag.p, c->cpos.p, (int)nt, st));
+    uint32_t last[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(&last[0], c->cpos.p + nt - 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&last[1], c->cflag.p + nt - 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint64_t total = (uint64_t)last[0] + last[1];
+    *n_out = total;
+    c->cstats.n_live = total;
+    if (total > cap) return KVR_CAPACITY;
+    if (total == 0) return KVR_OK;
+    kvr_tuple *d_out = out;
+    if (!(flags & KVR_OUT_ON_DEVICE)) {
+        if (c->lout.ensure(total)) return KVR_ENOMEM;
+        d_out = c->lout.p;
+    }
+    hipLaunchKernelGGL(k_live_tuples, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->cflag.p, c->cpos.p, d_out);
+    HIPCHK(hipGetLastError());
+    if (!(flags & KVR_OUT_ON_DEVICE))
+        HIPCHK(hipMemcpyAsync(out, d_out, total * sizeof(kvr_tuple), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return KVR_OK;
 }
 
 }  // extern "C"

@@ -109,6 +109,7 @@ def _load():
     rep.kvr_last_stats.argtypes = [P, C.POINTER(Stats)]
     rep.kvr_replay_stream.argtypes = [P, C.POINTER(Segment), SZ, U32, U64, P, SZ, P, SZ, C.POINTER(SZ),
                                       C.POINTER(Error)]
+    rep.kvr_replay_live.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
     rep.kvr_last_stream_stats.argtypes = [P, C.POINTER(StreamStats)]
     rep.kvr_etag_batch.argtypes = [P, P, U64, P, P, SZ, U32, P, P, C.POINTER(U64)]
     rep.kvr_last_etag_stats.argtypes = [P, C.POINTER(EtagStats)]
@@ -411,6 +412,30 @@ class Context:
         r = ReplayResult(rc, tuples, n_out.value, err if rc == CORRUPTED else None, self.last_stats())
         r.stream_stats = ss
         return r
+
+    def replay_live(self, segments, seg_ids=None, on_device=False, out_ptr=None, cap=None):
+        """Replay + last-writer fold on the device (kvr_replay_live): only the live keys' final
+        SET tuples, in (segment, offset) order.  Returns ReplayResult (tuples None with out_ptr)."""
+        segs, keep, total = self._segments(segments, seg_ids, on_device)
+        if cap is None:
+            cap = max(1024, total // 24 + len(segments))
+        flags = SEGS_ON_DEVICE if on_device else 0
+        out_arr = None
+        if out_ptr is not None:
+            flags |= OUT_ON_DEVICE
+            outp = out_ptr
+        else:
+            out_arr = np.zeros(max(cap, 1), dtype=TUPLE_DTYPE)
+            outp = out_arr.ctypes.data
+        n_out = C.c_size_t()
+        err = Error()
+        rc = self._rep.kvr_replay_live(self.h, segs, len(segments), flags, outp, cap, C.byref(n_out), C.byref(err))
+        if rc == CAPACITY and out_ptr is None:
+            return self.replay_live(segments, seg_ids, on_device, None, n_out.value + 16)
+        if rc < 0:
+            raise NativeError(f"kvr_replay_live: {self._rep.kvr_strerror(rc).decode()} ({rc})")
+        tuples = out_arr[: n_out.value] if out_arr is not None and rc == OK else None
+        return ReplayResult(rc, tuples, n_out.value, err if rc == CORRUPTED else None, self.last_stats())
 
     def etag_batch(self, data, offs, lens, expected=None, on_device=False, data_len=None):
         """Batch ETag (kvr_etag_batch): CRC-32 of data[offs[i]:offs[i]+lens[i]] for every i.
