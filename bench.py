@@ -215,6 +215,26 @@ def main():
                             "CRC verify + D2H of the tuples to host), best of 2"}
         del pin
 
+    live_idx = None
+    if rank == 0 and world == 1 and not args.no_stream:
+        # the index built on the device (kvr_replay_live: replay + last-writer fold in HBM, only
+        # the live keys' final tuples written), device-resident in and out
+        lo = torch.empty((n_rec + 1024) * 32, dtype=torch.uint8, device=dev)
+        lms = []
+        for i in range(3):
+            torch.cuda.synchronize()
+            t4 = time.perf_counter()
+            rl = ctx.replay_live(segs, seg_ids=seg_nos, on_device=True, out_ptr=lo.data_ptr(), cap=n_rec + 1024)
+            torch.cuda.synchronize()
+            assert rl.status == 0
+            if i:
+                lms.append(time.perf_counter() - t4)
+        live_idx = {"value": round(seg_total / min(lms) / 2 ** 30, 3), "unit": "GiB/s", "live_keys": rl.n,
+                    "ms": round(min(lms) * 1e3, 3),
+                    "sample": "kvr_replay_live on the device-resident shard: replay + last-writer fold in HBM, "
+                              "live tuples out (the index of engine.rs:137/:141), wall time, best of 2"}
+        del lo
+
     traffic = None   # HBM bytes per k_replay launch from PMC (tools/pmc_traffic.py), if measured on this build
     tj = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tj):
@@ -242,6 +262,7 @@ def main():
         "cpu_baseline_parallel": cpu_par,
         "e2e_host": e2e,
         "e2e_stream_pinned": stream,
+        "live_index_device": live_idx,
     }
     if rank == 0:
         print(json.dumps(res))
