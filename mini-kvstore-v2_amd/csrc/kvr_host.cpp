@@ -318,13 +318,15 @@ static int build_index(kvs_store *s, kvr_ctx *ctx, kvr_error *err, char *msg, si
         segs[i] = kvr_segment{s->ids[i], s->bytes[i].data(), s->bytes[i].size()};
         total += s->bytes[i].size();
     }
-    std::vector<kvr_tuple> tuples(std::max<size_t>(16, total / 64));
+    // the replay and the last-writer fold (engine.rs:137, :141) both run on the GPU
+    // (kvr_replay_live): only each live key's final SET comes back
+    std::vector<kvr_tuple> tuples(std::max<size_t>(16, total / 256));
     size_t nt = 0;
     kvr_error e{};
-    int rc = n ? kvr_replay(ctx, segs.data(), n, 0, nullptr, 0, tuples.data(), tuples.size(), &nt, &e) : KVR_OK;
+    int rc = n ? kvr_replay_live(ctx, segs.data(), n, 0, tuples.data(), tuples.size(), &nt, &e) : KVR_OK;
     if (rc == KVR_CAPACITY) {
         tuples.resize(nt);
-        rc = kvr_replay(ctx, segs.data(), n, 0, nullptr, 0, tuples.data(), tuples.size(), &nt, &e);
+        rc = kvr_replay_live(ctx, segs.data(), n, 0, tuples.data(), tuples.size(), &nt, &e);
     }
     if (rc == KVR_CORRUPTED) {
         if (err) *err = e;
@@ -332,12 +334,11 @@ static int build_index(kvs_store *s, kvr_ctx *ctx, kvr_error *err, char *msg, si
         return rc;
     }
     if (rc != KVR_OK) return rc;
-    s->index.reserve(nt / 2 + 16);
-    for (size_t i = 0; i < nt; ++i) {   // last-writer-wins fold (engine.rs:137, :141)
+    s->index.reserve(nt + 16);
+    for (size_t i = 0; i < nt; ++i) {   // one live SET per key, already folded
         const kvr_tuple &t = tuples[i];
         const KeyRef k{segs[t.seg_idx].bytes + t.rec_off + 5, t.key_len, t.key_tag};
-        if (t.op == 0) s->index[k] = kvs_store::Ent{t.seg_idx, t.rec_off + 9 + t.key_len, t.val_len};
-        else s->index.erase(k);
+        s->index[k] = kvs_store::Ent{t.seg_idx, t.rec_off + 9 + t.key_len, t.val_len};
     }
     for (const auto &kv : s->index) s->total_bytes += kv.second.len;
     return KVR_OK;
