@@ -9,6 +9,12 @@ verify + ordered tuples left in HBM.  Weak scaling: rank r replays its own 64 se
 only for the barrier and the max-over-ranks timing).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5]
+                                     --gpus N > 1 without WORLD_SIZE in the environment: the parent
+                                     (which never touches a GPU) launches N ranks with
+                                     torch.distributed.run and exits with their status; under a
+                                     launcher WORLD_SIZE must equal N
+  python bench.py --dry-run          the same launch / barrier / max-over-ranks path on CPU (gloo), a
+                                     sleep standing in for the replay (tests/test_bench_launch.py)
   python bench.py --mode etag        batch ETag compute/verify in cfg3's volume-server
                                      shape: 131072 blobs of 64 KiB (8 GiB) resident in HBM, one step =
                                      one kvr_etag_batch (CRC-32 per blob + verify against stored ETags)
@@ -54,18 +60,26 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stream", action="store_true", help="skip the pinned-host streamed (H2D-inclusive) leg")
     ap.add_argument("--stream-batch", type=int, default=512 << 20, help="kvr_replay_stream batch bytes")
+    ap.add_argument("--dry-run", action="store_true", help="CPU rehearsal of the launch and timing path (gloo)")
     args = ap.parse_args()
     if args.config is None:
         args.config = "cfg4" if args.mode == "compact" else "cfg2"
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: one rank per GPU")
+    if args.dry_run:
+        return dry_run(args, world, rank)
 
     import numpy as np
     import torch
     import torch.distributed as dist
     import kvreplay as K
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -129,8 +143,10 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    per_rank = None
     if world > 1:
         from kvreplay.shard import max_over_ranks
+        per_rank = gather_per_rank(dt, seg_total, args.steps)
         dt = max_over_ranks(dt)
 
     ms_replay = float(np.mean([a for a, _ in k_ms]))
@@ -264,6 +280,8 @@ def main():
         "e2e_stream_pinned": stream,
         "live_index_device": live_idx,
     }
+    if per_rank is not None:
+        res["per_rank"] = per_rank
     if rank == 0:
         print(json.dumps(res))
     ctx.close()
@@ -432,5 +450,64 @@ def bench_etag(args, K, torch, dev, world, rank):
         print(json.dumps(res))
     ctx.close()
 
+def spawn_ranks(n):
+    """One process per GPU: run this script under torch.distributed.run as a child process (this
+    parent has made no HIP call, so nothing is exec'd over an initialised GPU) and exit with its
+    status.  Rendezvous on 127.0.0.1 (the container hostname may not resolve)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def gather_per_rank(dt, bytes_per_rank, steps):
+    """Every rank's own wall time and rate, on rank 0 (None elsewhere)."""
+    import torch.distributed as dist
+    mine = {"rank": dist.get_rank(), "seconds": round(dt, 6),
+            "GiB_s": round(bytes_per_rank * steps / dt / 2 ** 30, 3) if dt > 0 else None}
+    out = [None] * dist.get_world_size() if dist.get_rank() == 0 else None
+    dist.gather_object(mine, out, dst=0)
+    return out
+
+
+def dry_run(args, world, rank):
+    """The launch, barrier and max-over-ranks logic of the replay leg on CPU (gloo): a sleep of
+    (rank + 1) ms stands in for one replay step, so the whole-job time must be the slowest rank's."""
+    import torch.distributed as dist
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+    bytes_per_rank = 1 << 30
+    for _ in range(args.warmup):
+        time.sleep(0.001 * (rank + 1))
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001 * (rank + 1))
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    per_rank = None
+    if world > 1:
+        from kvreplay.shard import max_over_ranks
+        per_rank = gather_per_rank(dt, bytes_per_rank, args.steps)
+        dt = max_over_ranks(dt)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC + " (dry run: no GPU, sleep steps)", "value": round(
+            bytes_per_rank * world * args.steps / dt / 2 ** 30, 3), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "none (dry run)", "config": {"workload": "dry run", "parallelism": f"shard-segments x{world}"},
+            "per_rank": per_rank}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -96,6 +96,10 @@ def build_ablate(masks=(0, 1, 2, 3, 7, 8, 16, 32, 64)):
 VARIANTS = {
     "rt768": ["-DKVR_RT=768"],
     "rt512": ["-DKVR_RT=512"],
+    "v9": ["-DKVR_KERNEL_V9"],
+    "v9a3": ["-DKVR_KERNEL_V9", "-DKVR_ABLATE=3"],
+    "v9a64": ["-DKVR_KERNEL_V9", "-DKVR_ABLATE=64"],
+    "v8": ["-DKVR_KERNEL_V8"],
 }
 
 

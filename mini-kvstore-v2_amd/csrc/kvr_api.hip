@@ -21,11 +21,27 @@
 #include <hipcub/hipcub.hpp>
 
 #include "kvr_replay_kernel.hip"
+#include "kvr_replay8.hip"
+#include "kvr_replay9.hip"
 #include "kvr_kernels.hip"
 #include "kvr_compact.hip"
 #include "kvr_etag.hip"
 
 using namespace kvr;
+
+// the replay kernel: V7 (kvr_replay_kernel.hip, the fastest measured: DESIGN.md §7);
+// -DKVR_KERNEL_V8 / -DKVR_KERNEL_V9 build the experimental kernels (timing only).
+// KR_WPB = stripes per workgroup, KR_TILE = tile bytes.
+#if defined(KVR_KERNEL_V9)
+#define KR_KERNEL v9::k_replay9
+static constexpr int KR_RT = v9::RT, KR_WPB = v9::WPB * v9::QPW, KR_TILE = v9::TILE;
+#elif defined(KVR_KERNEL_V8)
+#define KR_KERNEL v8::k_replay8
+static constexpr int KR_RT = v8::RT, KR_WPB = v8::WPB, KR_TILE = TILE;
+#else
+#define KR_KERNEL k_replay
+static constexpr int KR_RT = RT, KR_WPB = WPB, KR_TILE = TILE;
+#endif
 
 namespace {
 
@@ -219,7 +235,7 @@ int kvr_ctx_create(int device, kvr_ctx **out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->n_cu = prop.multiProcessorCount;
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_replay, RT, 0) == hipSuccess && occ > 0) c->wg_per_cu = occ;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, KR_KERNEL, KR_RT, 0) == hipSuccess && occ > 0) c->wg_per_cu = occ;
     if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return KVR_EHIP; }
     c->stream = c->own;
     for (auto &e : c->ev) if (hipEventCreate(&e) != hipSuccess) { delete c; return KVR_EHIP; }
@@ -339,7 +355,7 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         g.base = dptr[i];
         g.len = segs[i].len;
         g.d0 = (uint32_t)(reinterpret_cast<uintptr_t>(dptr[i]) & 15u);
-        g.n_tiles = g.len ? (uint32_t)((g.len + g.d0 + TILE - 1) / TILE) : 0u;
+        g.n_tiles = g.len ? (uint32_t)((g.len + g.d0 + KR_TILE - 1) / KR_TILE) : 0u;
         g.tile0 = (uint32_t)total_tiles;
         total_tiles += g.n_tiles;
     }
@@ -347,7 +363,7 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
     // one stripe per resident wave, one round (k_replay: WPB stripes per workgroup).  Measured
     // (tools/tps_sweep.py): one round beats two by 5 % on cfg2 and 14 % on cfg5, and stripe counts
     // between whole rounds leave a ragged tail
-    const uint64_t target = (uint64_t)c->n_cu * (uint64_t)c->wg_per_cu * WPB;
+    const uint64_t target = (uint64_t)c->n_cu * (uint64_t)c->wg_per_cu * KR_WPB;
     const uint64_t tps = c->tps_override ? c->tps_override : std::max<uint64_t>(1, (total_tiles + target - 1) / target);
     c->h_stripes.clear();
     for (size_t i = 0; i < n; ++i) {
@@ -409,12 +425,12 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         HIPCHK(hipMemsetAsync(c->ctr.p, 0, sizeof(Counters), st));
         HIPCHK(hipMemsetAsync(c->link.p, 0, sizeof(LinkResult), st));
         HIPCHK(hipEventRecord(c->ev[0], st));
-        hipLaunchKernelGGL(k_replay, dim3((n_stripes + WPB - 1) / WPB), dim3(RT), 0, st, c->segs.p, c->stripes.p, n_stripes,
+        hipLaunchKernelGGL(KR_KERNEL, dim3((n_stripes + KR_WPB - 1) / KR_WPB), dim3(KR_RT), 0, st, c->segs.p, c->stripes.p, n_stripes,
                            c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, c->redo.p, c->link.p, 0, pool_chunk);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[1], st));
         hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
-                           c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p);
+                           c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p, (uint32_t)KR_TILE);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[2], st));
         // compaction is launched right away: it does nothing unless linking succeeded (status 0),
@@ -459,11 +475,11 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
             continue;
         }
         while (c->h_link->status == 3 && guard++ < n_stripes + 4) {
-            hipLaunchKernelGGL(k_replay, dim3((std::max(1u, std::min(c->h_link->n_redo, (uint32_t)c->redo.n)) + WPB - 1) / WPB), dim3(RT),
+            hipLaunchKernelGGL(KR_KERNEL, dim3((std::max(1u, std::min(c->h_link->n_redo, (uint32_t)c->redo.n)) + KR_WPB - 1) / KR_WPB), dim3(KR_RT),
                                0, st, c->segs.p, c->stripes.p, n_stripes, c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p,
                                tb, c->redo.p, c->link.p, 1, pool_chunk);
             hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes,
-                               c->sres.p, c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p);
+                               c->sres.p, c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p, (uint32_t)KR_TILE);
             HIPCHK(hipGetLastError());
             HIPCHK(hipMemcpyAsync(c->h_link, c->link.p, sizeof(LinkResult), hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, st));

@@ -20,13 +20,13 @@ namespace kvr {
 // ---------------------------------------------------------------------------------------
 constexpr int LT = 1024;
 
-__device__ __forceinline__ uint64_t stripe_hi(const StripeDesc &d, const SegDesc &g) {
-    const int64_t h = (int64_t)d.t_end * TILE - (int64_t)g.d0;
+__device__ __forceinline__ uint64_t stripe_hi(const StripeDesc &d, const SegDesc &g, uint32_t tile) {
+    const int64_t h = (int64_t)d.t_end * tile - (int64_t)g.d0;
     return (uint64_t)h > g.len ? g.len : (uint64_t)h;
 }
 
-__device__ __forceinline__ uint64_t stripe_lo(const StripeDesc &d, const SegDesc &g) {
-    const int64_t l = (int64_t)d.t_begin * TILE - (int64_t)g.d0;
+__device__ __forceinline__ uint64_t stripe_lo(const StripeDesc &d, const SegDesc &g, uint32_t tile) {
+    const int64_t l = (int64_t)d.t_begin * tile - (int64_t)g.d0;
     return l < 0 ? 0ull : (uint64_t)l;
 }
 
@@ -34,7 +34,7 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
                                              const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
                                              const StripeRes *__restrict__ sres, RedoEnt *__restrict__ redo,
                                              uint32_t redo_cap, LinkResult *res, uint32_t *seg_bad,
-                                             uint32_t *seg_err) {
+                                             uint32_t *seg_err, uint32_t tile) {
     __shared__ int32_t cm[LT];
     __shared__ uint32_t first_problem, nredo;
     const int tid = threadIdx.x;
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
         if (!first) {
             const uint64_t xp = run >= 0 ? sres[run].exit : NONE;
             if (xp == ERRP) after_err = true;
-            else if (r.entry == NONE) bad = xp < stripe_hi(d, g);
+            else if (r.entry == NONE) bad = xp < stripe_hi(d, g, tile);
             else bad = (r.entry != xp);
         }
         if (bad && !after_err) atomicMin(&seg_bad[d.seg], s);
@@ -104,13 +104,13 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
                 const uint64_t xp = run >= 0 ? sres[run].exit : NONE;
                 bool bad = false;
                 if (xp != ERRP) {
-                    if (r.entry == NONE) bad = xp < stripe_hi(d, g);
+                    if (r.entry == NONE) bad = xp < stripe_hi(d, g, tile);
                     else bad = (r.entry != xp);
                 }
                 const uint32_t se = __hip_atomic_load(&seg_err[d.seg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 // a predecessor exit short of this stripe lands in a pass-through stripe in
                 // between, which is re-walked first; this one waits for the next round
-                if (bad && s < se && xp >= stripe_lo(d, g)) {
+                if (bad && s < se && xp >= stripe_lo(d, g, tile)) {
                     const uint32_t i = atomicAdd(&nredo, 1u);
                     if (i < redo_cap) { redo[i].stripe = s; redo[i].pad = 0; redo[i].entry = xp; }
                 }

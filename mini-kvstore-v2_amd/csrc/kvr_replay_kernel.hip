@@ -258,7 +258,8 @@ __device__ inline uint32_t crc_long(const TileSeg &ts, uint32_t c, int64_t o, ui
 // UTF-8 validation with Rust's Utf8Error semantics (engine.rs:114, String::from_utf8).
 // Returns true if valid, else *vu = valid_up_to and *el = error_len (0 = incomplete).
 // ---------------------------------------------------------------------------------------
-__device__ inline bool utf8_check(const TileSeg &ts, int64_t p, uint64_t n, uint64_t *vu, uint32_t *el) {
+template <class TS>
+__device__ inline bool utf8_check(const TS &ts, int64_t p, uint64_t n, uint64_t *vu, uint32_t *el) {
     uint64_t i = 0;
 #pragma unroll 1
     while (i < n) {
@@ -300,7 +301,8 @@ __device__ inline bool utf8_check(const TileSeg &ts, int64_t p, uint64_t n, uint
 // ---------------------------------------------------------------------------------------
 // End of the record at o (engine.rs framing, exact), or -1 if the framing is broken there:
 // opcode outside {0,1} or a field running past the segment end.  o inside the segment.
-__device__ inline int64_t next_rec(const TileSeg &ts, int64_t o) {
+template <class TS>
+__device__ inline int64_t next_rec(const TS &ts, int64_t o) {
     const int64_t rem = (int64_t)ts.len - ts.lo;          // segment end, tile-relative
     const uint32_t op = ts.b8(o);
     if (op > 1u || rem - o < 5) return -1;
@@ -318,7 +320,8 @@ __device__ inline int64_t next_rec(const TileSeg &ts, int64_t o) {
 // whose "key" is the zero bytes of the true length) fails the NUL test.  Heuristic only: a true
 // record rejected here (a key holding NUL) is found again by the stripe link check and the
 // exact re-walk, so results never depend on it.
-__device__ inline bool key_prefix_ok(const TileSeg &ts, int64_t ok, uint32_t klen) {
+template <class TS>
+__device__ inline bool key_prefix_ok(const TS &ts, int64_t ok, uint32_t klen) {
     const int m = klen > 16u ? 16 : (int)klen;
     int i = 0;
     #pragma unroll 1
@@ -369,7 +372,8 @@ __device__ __forceinline__ bool key_prefix_ok_r(const uint32_t (&x)[6], uint32_t
     return !bad;
 }
 
-__device__ inline bool plausible(const TileSeg &ts, int64_t o) {
+template <class TS>
+__device__ inline bool plausible(const TS &ts, int64_t o) {
     const int64_t rem = (int64_t)ts.len - ts.lo;
     // the near tests first (header and key bytes sit in the tile's lines): inside a long value
     // nearly every candidate fails them, before next_rec reads at the far value length.  Inside
