@@ -170,6 +170,32 @@ int  kvr_replay_stream(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uin
                        kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err);
 int  kvr_last_stream_stats(const kvr_ctx *ctx, kvr_stream_stats *out);
 
+/* ---- several GPUs from one process ---------------------------------------------
+ * The loop of engine.rs:55-57 over N contexts: segment i of the (sorted) list is replayed by
+ * context i mod N, each on its own host thread and stream, no collective; the host merges the
+ * shards.  Output, errors, expected_crc and return codes are exactly those of kvr_replay over the
+ * same segs on one GPU: tuples in (segment, offset) order with seg_idx into segs[], the first
+ * error = the minimum (segment, offset) error over the shards.  devices may repeat an id (several
+ * contexts on one GPU).  Host segments and host output only (flags: 0). */
+typedef struct kvr_mctx kvr_mctx;
+typedef struct kvr_multi_stats {
+    double   ms_wall;         /* host wall time of the call: shard threads + merge                 */
+    double   ms_device_max;   /* the slowest shard's device pipeline (kvr_stats.ms_total)          */
+    uint64_t bytes_in;
+    uint64_t n_records;
+    uint64_t n_crc_fail;
+    uint32_t n_shards;
+    uint32_t pad;
+} kvr_multi_stats;
+
+int  kvr_mctx_create(const int *devices, int n_devices, kvr_mctx **out);
+void kvr_mctx_destroy(kvr_mctx *m);
+int  kvr_mctx_size(const kvr_mctx *m);
+int  kvr_replay_multi(kvr_mctx *m, const kvr_segment *segs, size_t n_segs, uint32_t flags,
+                      const uint32_t *expected_crc, size_t n_expected,
+                      kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err);
+int  kvr_last_multi_stats(const kvr_mctx *m, kvr_multi_stats *out);
+
 /* Host helpers. */
 const char *kvr_strerror(int code);
 /* CRC-32/ISO-HDLC, identical to crc32fast::hash (storage.rs:27) when crc == 0. */

@@ -1183,3 +1183,5 @@ int kvr_replay_live(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flag
 }
 
 }  // extern "C"
+
+#include "kvr_multi.hip"

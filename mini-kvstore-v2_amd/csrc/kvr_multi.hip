@@ -1,0 +1,148 @@
+/*
+ * kvr_multi.hip — several GPUs behind one call, included by kvr_api.hip.
+ *
+ * The store's sorted segment list (engine.rs:51) is dealt round-robin: segment i -> context
+ * i mod N.  Segments are independent parse units (framing never crosses files, engine.rs:80-85),
+ * so every context replays its shard with kvr_replay on its own host thread and stream, with no
+ * collective and no device-to-device traffic; the host gathers the shards.  The merge is exact:
+ *   - tuples: a shard's output is in (its segment, offset) order, so the store's order
+ *     (engine.rs:55-57 applies records segment by segment) is segment i's run taken from shard
+ *     i mod N, for i ascending — an O(n) copy, seg_idx rewritten to the caller's index;
+ *   - errors: the store's first error is the minimum (segment, offset) error over the shards
+ *     (engine.rs:56 stops at the first one; what other shards found after it is never reached);
+ *   - expected CRCs (the caller's manifest in store tuple order) are checked on the merged order.
+ */
+#include <thread>
+
+struct kvr_mctx {
+    std::vector<kvr_ctx *> c;
+    kvr_multi_stats st{};
+};
+
+extern "C" {
+
+int kvr_mctx_create(const int *devices, int n_devices, kvr_mctx **out) {
+    if (!out || n_devices < 1 || !devices) return KVR_EINVAL;
+    *out = nullptr;
+    kvr_mctx *m = new kvr_mctx();
+    for (int i = 0; i < n_devices; ++i) {
+        kvr_ctx *c = nullptr;
+        const int rc = kvr_ctx_create(devices[i], &c);
+        if (rc != KVR_OK) {
+            kvr_mctx_destroy(m);
+            return rc;
+        }
+        m->c.push_back(c);
+    }
+    *out = m;
+    return KVR_OK;
+}
+
+void kvr_mctx_destroy(kvr_mctx *m) {
+    if (!m) return;
+    for (kvr_ctx *c : m->c) kvr_ctx_destroy(c);
+    delete m;
+}
+
+int kvr_mctx_size(const kvr_mctx *m) { return m ? (int)m->c.size() : 0; }
+
+int kvr_last_multi_stats(const kvr_mctx *m, kvr_multi_stats *out) {
+    if (!m || !out) return KVR_EINVAL;
+    *out = m->st;
+    return KVR_OK;
+}
+
+int kvr_replay_multi(kvr_mctx *m, const kvr_segment *segs, size_t n, uint32_t flags, const uint32_t *expected,
+                     size_t n_expected, kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err) {
+    if (!m || m->c.empty() || (!segs && n) || !n_out || (cap && !out)) return KVR_EINVAL;
+    if (flags & (KVR_SEGS_ON_DEVICE | KVR_OUT_ON_DEVICE | KVR_EXPECTED_ON_DEVICE)) return KVR_EINVAL;   // host in, host out
+    if (err) memset(err, 0, sizeof(*err));
+    *n_out = 0;
+    memset(&m->st, 0, sizeof(m->st));
+    for (size_t i = 1; i < n; ++i)
+        if (segs[i].seg_id < segs[i - 1].seg_id) return KVR_EINVAL;   // caller sorts (engine.rs:51)
+    const size_t N = m->c.size();
+    m->st.n_shards = (uint32_t)N;
+    if (n == 0) return KVR_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+
+    std::vector<std::vector<kvr_segment>> sh(N);
+    for (size_t i = 0; i < n; ++i) {
+        sh[i % N].push_back(segs[i]);
+        m->st.bytes_in += segs[i].len;
+    }
+    std::vector<std::vector<kvr_tuple>> tv(N);
+    std::vector<int> rc(N, KVR_OK);
+    std::vector<kvr_error> er(N);
+    std::vector<size_t> nn(N, 0);
+    std::vector<double> dev_ms(N, 0.0);
+    std::vector<std::thread> th;
+    for (size_t r = 0; r < N; ++r) {
+        if (sh[r].empty()) continue;
+        th.emplace_back([&, r]() {
+            uint64_t bytes = 0;
+            for (const kvr_segment &s : sh[r]) bytes += s.len;
+            size_t c = (size_t)(bytes / 256) + 4096 + sh[r].size();
+            tv[r].resize(c);
+            int x = kvr_replay(m->c[r], sh[r].data(), sh[r].size(), 0, nullptr, 0, tv[r].data(), c, &nn[r], &er[r]);
+            if (x == KVR_CAPACITY) {   // rare: denser than one record per 256 B; replay again into the exact size
+                c = nn[r];
+                tv[r].resize(c);
+                x = kvr_replay(m->c[r], sh[r].data(), sh[r].size(), 0, nullptr, 0, tv[r].data(), c, &nn[r], &er[r]);
+            }
+            kvr_stats s;
+            kvr_last_stats(m->c[r], &s);
+            dev_ms[r] = s.ms_total;
+            rc[r] = x;
+        });
+    }
+    for (std::thread &t : th) t.join();
+    for (size_t r = 0; r < N; ++r) {
+        if (rc[r] < 0) return rc[r];
+        m->st.ms_device_max = std::max(m->st.ms_device_max, dev_ms[r]);
+    }
+
+    // the store's first error: minimum (segment, offset) over the shards
+    bool bad = false;
+    kvr_error first{};
+    for (size_t r = 0; r < N; ++r) {
+        if (rc[r] != KVR_CORRUPTED) continue;
+        kvr_error e = er[r];
+        e.seg_idx = (uint32_t)(e.seg_idx * N + r);   // local index j of shard r is global j * N + r
+        if (!bad || e.seg_idx < first.seg_idx || (e.seg_idx == first.seg_idx && e.rec_off < first.rec_off)) first = e;
+        bad = true;
+    }
+    if (bad) {
+        if (err) *err = first;
+        m->st.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return KVR_CORRUPTED;
+    }
+
+    // merge: segment i's run from shard i mod N, in segment order
+    std::vector<size_t> pos(N, 0);
+    size_t o = 0;
+    uint64_t fails = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const size_t r = i % N;
+        const uint32_t j = (uint32_t)(i / N);
+        const std::vector<kvr_tuple> &t = tv[r];
+        size_t &p = pos[r];
+        while (p < nn[r] && t[p].seg_idx == j) {
+            kvr_tuple x = t[p++];
+            x.seg_idx = (uint32_t)i;
+            if (expected && o < n_expected && x.op == 0) {
+                x.flags |= KVR_TF_VERIFIED;
+                if (expected[o] != x.crc32) { x.flags |= KVR_TF_CRC_FAIL; ++fails; }
+            }
+            if (o < cap) out[o] = x;
+            ++o;
+        }
+    }
+    *n_out = o;
+    m->st.n_records = o;
+    m->st.n_crc_fail = fails;
+    m->st.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return o > cap ? KVR_CAPACITY : KVR_OK;
+}
+
+}  // extern "C"

@@ -55,6 +55,12 @@ class StreamStats(C.Structure):
                 ("n_records", C.c_uint64), ("n_batches", C.c_uint64)]
 
 
+class MultiStats(C.Structure):
+    _fields_ = [("ms_wall", C.c_double), ("ms_device_max", C.c_double), ("bytes_in", C.c_uint64),
+                ("n_records", C.c_uint64), ("n_crc_fail", C.c_uint64), ("n_shards", C.c_uint32),
+                ("pad", C.c_uint32)]
+
+
 class EtagStats(C.Structure):
     _fields_ = [("ms_chunk", C.c_double), ("ms_join", C.c_double), ("bytes", C.c_uint64),
                 ("n_blobs", C.c_uint64), ("n_chunks", C.c_uint64), ("n_fail", C.c_uint64)]
@@ -107,6 +113,12 @@ def _load():
     rep.kvr_ctx_set_tiles_per_stripe.argtypes = [P, U32]
     rep.kvr_replay.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
     rep.kvr_last_stats.argtypes = [P, C.POINTER(Stats)]
+    rep.kvr_mctx_create.argtypes = [P, I, C.POINTER(P)]
+    rep.kvr_mctx_destroy.argtypes = [P]
+    rep.kvr_mctx_destroy.restype = None
+    rep.kvr_mctx_size.argtypes = [P]
+    rep.kvr_replay_multi.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
+    rep.kvr_last_multi_stats.argtypes = [P, C.POINTER(MultiStats)]
     rep.kvr_replay_stream.argtypes = [P, C.POINTER(Segment), SZ, U32, U64, P, SZ, P, SZ, C.POINTER(SZ),
                                       C.POINTER(Error)]
     rep.kvr_replay_live.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
@@ -295,6 +307,68 @@ class CompactResult:
             out.append(self.data[s:e])
             s = e
         return out
+
+
+class MultiContext:
+    """kvr_mctx: one context per entry of devices (ids may repeat), segments dealt round-robin,
+    shards replayed concurrently on host threads, merged on the host (kvr_replay_multi)."""
+
+    def __init__(self, devices):
+        rep, _ = _load()
+        self._rep = rep
+        d = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        rc = rep.kvr_mctx_create(d, len(devices), C.byref(h))
+        if rc != OK:
+            raise NativeError(f"kvr_mctx_create({list(devices)}) failed: {rep.kvr_strerror(rc).decode()} ({rc})")
+        self.h, self.devices = h, list(devices)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._rep.kvr_mctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def last_stats(self) -> MultiStats:
+        s = MultiStats()
+        self._rep.kvr_last_multi_stats(self.h, C.byref(s))
+        return s
+
+    def replay(self, segments, seg_ids=None, expected=None, cap=None):
+        """Same contract as Context.replay over host segments; returns ReplayResult (stats:
+        MultiStats)."""
+        keep = []
+        n = len(segments)
+        segs = (Segment * max(n, 1))()
+        total = 0
+        for i, s in enumerate(segments):
+            a = np.frombuffer(s, dtype=np.uint8) if isinstance(s, (bytes, bytearray)) else np.ascontiguousarray(s)
+            keep.append(a)
+            segs[i] = Segment(seg_ids[i] if seg_ids is not None else i, a.ctypes.data if a.size else None, a.size)
+            total += a.size
+        exp_ptr, n_exp = None, 0
+        if expected is not None:
+            e = np.ascontiguousarray(expected, dtype=np.uint32)
+            keep.append(e)
+            exp_ptr, n_exp = (e.ctypes.data if e.size else None), e.size
+        if cap is None:
+            cap = max(1024, total // 24 + n)
+        out_arr = np.zeros(max(cap, 1), dtype=TUPLE_DTYPE)
+        n_out = C.c_size_t()
+        err = Error()
+        rc = self._rep.kvr_replay_multi(self.h, segs, n, 0, exp_ptr, n_exp, out_arr.ctypes.data, cap, C.byref(n_out),
+                                        C.byref(err))
+        if rc == CAPACITY:
+            return self.replay(segments, seg_ids, expected, cap=n_out.value + 16)
+        if rc < 0:
+            raise NativeError(f"kvr_replay_multi: {self._rep.kvr_strerror(rc).decode()} ({rc})")
+        tuples = out_arr[: n_out.value] if rc == OK else None
+        return ReplayResult(rc, tuples, n_out.value, err if rc == CORRUPTED else None, self.last_stats())
 
 
 class Context:

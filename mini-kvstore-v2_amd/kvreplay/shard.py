@@ -96,17 +96,21 @@ class ShardedReplay:
         n = len(segments)
         world = len(self.ctxs)
         exp_parts = _split_expected(segments, expected, world) if expected is not None else [None] * world
-        parts = []
-        for r, ctx in enumerate(self.ctxs):
+        def one(r):
             idx = shard_round_robin(n, world, r)
             if not idx:
-                continue
-            res = ctx.replay([segments[i] for i in idx],
-                             seg_ids=None if seg_ids is None else [seg_ids[i] for i in idx],
-                             expected=exp_parts[r], on_device=on_device)
+                return None
+            res = self.ctxs[r].replay([segments[i] for i in idx],
+                                      seg_ids=None if seg_ids is None else [seg_ids[i] for i in idx],
+                                      expected=exp_parts[r], on_device=on_device)
             e = res.error
             err = (e.kind, e.seg_idx, e.rec_off, e.aux) if (res.status == CORRUPTED and e is not None) else None
-            parts.append(localize(idx, res.status, res.tuples if res.status == OK else None, err))
+            return localize(idx, res.status, res.tuples if res.status == OK else None, err)
+
+        # one host thread per context: the native calls release the GIL, so the GPUs run concurrently
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=world) as ex:
+            parts = [p for p in ex.map(one, range(world)) if p is not None]
         return merge_shards(parts)
 
 
