@@ -73,11 +73,14 @@ def utf8_check(data):
     return bool(ok), int(vu.value), int(el.value)
 
 
-def replay(segments, expected=None, seg_ids=None):
-    """-> (status, tuples ndarray, Error).  Tuples are those walked before the first error."""
+def replay(segments, expected=None, seg_ids=None, cap=None):
+    """-> (status, tuples ndarray, Error).  Tuples are those walked before the first error.
+    cap: tuple capacity (default one per 5 bytes, the densest framing); a run that needs more
+    returns the first cap tuples."""
     arrs, segs = _segs(segments, seg_ids)
     total = sum(a.size for a in arrs)
-    cap = total // 5 + 16
+    if cap is None:
+        cap = total // 5 + 16
     out = np.zeros(cap, dtype=TUPLE_DTYPE)
     n = C.c_size_t()
     err = Error()
@@ -130,3 +133,27 @@ def split_segments(data, ends):
         out.append(data[s:e])
         s = e
     return out
+
+
+def replay_parallel(segments, threads=16, cap_per_byte=256):
+    """The oracle over many large segments, one segment per host thread (the checker for the
+    full-size GPU tests): -> (status, tuples with the store's seg_idx, Error of the first failing
+    segment).  Segments are independent parse units (engine.rs:80-85), so this equals replay()."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(i):
+        a = _as_u8(segments[i])
+        rc, t, e = replay([a], cap=a.size // cap_per_byte + 4096)
+        if rc == 0 and len(t) == a.size // cap_per_byte + 4096:      # capacity hit: exact size
+            rc, t, e = replay([a])
+        t = t.copy()
+        t["seg_idx"] = i
+        e.seg_idx = i
+        return rc, t, e
+
+    with ThreadPoolExecutor(threads) as ex:
+        parts = list(ex.map(one, range(len(segments))))
+    for rc, _, e in parts:
+        if rc != 0:
+            return rc, np.zeros(0, TUPLE_DTYPE), e
+    return 0, np.concatenate([t for _, t, _ in parts]) if parts else np.zeros(0, TUPLE_DTYPE), Error()

@@ -1,0 +1,91 @@
+"""Full-size GPU tests at BASELINE.json's shapes: the segments are generated
+in HBM by the device generator exactly as bench.py does, replayed through the C ABI, and checked
+
+  cfg2  64 x 64 MiB, 1 KiB values          tuple for tuple against the oracle (one segment per host
+  cfg3  8 x 1 GiB, 64 KiB values           thread over the D2H copy of the same bytes) + manifest
+  cfg5  64 x 512 MiB (one GPU's 32 GiB     size-independent properties: records = generator count,
+        shard of the 256 GiB store)        every CRC verified against the manifest with 0 failures,
+                                           stripe re-walks reported; two segments against the oracle
+"""
+import numpy as np
+import pytest
+import torch
+
+import kvreplay as K
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+
+SPECS = {   # bench.py CONFIGS (seed = 0x6B767265706C6179 + config number)
+    "cfg2": (64, 64 << 20, dict(val_min=1024, val_max=1024, key_space_log2=20)),
+    "cfg3": (8, 1 << 30, dict(val_min=65536, val_max=65536, key_space_log2=20)),
+    "cfg5": (64, 512 << 20, dict(val_min=16, val_max=1 << 20, key_space_log2=24, key_dist=1, del_permille=100)),
+}
+
+
+def _generate(ctx, cfg):
+    nseg, seg_bytes, kw = SPECS[cfg]
+    spec = K.GenSpec(seed=0x6B767265706C6179 + int(cfg[3:]), seg_bytes=seg_bytes, **kw)
+    sizes = [K.gen_segment_size(spec, s) for s in range(nseg)]
+    offs, tot = [], 0
+    for ln, _ in sizes:
+        offs.append(tot)
+        tot += (ln + 255) & ~255
+    n_rec = sum(nr for _, nr in sizes)
+    data = torch.empty(tot + 256, dtype=torch.uint8, device="cuda")
+    man = torch.empty(n_rec + 1, dtype=torch.int32, device="cuda")
+    eo = 0
+    for s, ((ln, nr), o) in enumerate(zip(sizes, offs)):
+        ctx.gen_segment_device(spec, s, data.data_ptr() + o, ln, man.data_ptr() + 4 * eo, nr)
+        eo += nr
+    torch.cuda.synchronize()
+    return data, offs, sizes, man, n_rec
+
+
+def _replay_to_host(ctx, data, offs, sizes, man, n_rec):
+    segs = [(data.data_ptr() + o, ln) for (ln, _), o in zip(sizes, offs)]
+    out = torch.empty((n_rec + 1024) * 32, dtype=torch.uint8, device="cuda")
+    r = ctx.replay(segs, expected=(man.data_ptr(), n_rec), expected_on_device=True, on_device=True,
+                   out_ptr=out.data_ptr(), cap=n_rec + 1024)
+    torch.cuda.synchronize()
+    t = out[: r.n * 32].cpu().numpy().view(K.TUPLE_DTYPE) if r.status == 0 else None
+    return r, t
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
+def test_full_size_bit_exact(gctx, cfg):
+    data, offs, sizes, man, n_rec = _generate(gctx, cfg)
+    r, t = _replay_to_host(gctx, data, offs, sizes, man, n_rec)
+    assert r.status == 0 and r.n == n_rec and r.stats.n_crc_fail == 0
+    host = data.cpu().numpy()
+    segs = [host[o: o + ln] for (ln, _), o in zip(sizes, offs)]
+    del data
+    rc, ref, _ = O.replay_parallel(segs, threads=16)
+    assert rc == 0 and len(ref) == n_rec
+    ref["flags"] |= np.where(ref["op"] == 0, K.TF_VERIFIED, 0).astype(np.uint8)   # the manifest matches
+    if not np.array_equal(t, ref):
+        bad = np.nonzero(t != ref)[0][:5]
+        raise AssertionError(f"{cfg}: tuple mismatch at {bad}: gpu={t[bad]} oracle={ref[bad]}")
+
+
+def test_cfg5_shard_properties(gctx):
+    data, offs, sizes, man, n_rec = _generate(gctx, "cfg5")
+    assert sum(ln for ln, _ in sizes) > 31 << 30           # the full 32-GiB shard of one GPU
+    r, t = _replay_to_host(gctx, data, offs, sizes, man, n_rec)
+    assert r.status == 0
+    assert r.n == n_rec                                     # every generated record, no more
+    assert r.stats.n_crc_fail == 0                          # every value CRC = the manifest's ETag
+    assert int(np.count_nonzero(t["flags"] & K.TF_VERIFIED)) == int(np.count_nonzero(t["op"] == 0))
+    assert r.stats.n_redo >= 0 and r.stats.n_stripes > 0
+    # per-segment record counts match the generator, and two whole segments match the oracle
+    counts = np.bincount(t["seg_idx"], minlength=len(sizes))
+    assert [int(c) for c in counts] == [nr for _, nr in sizes]
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    for s in (0, 37):
+        ln, _ = sizes[s]
+        seg = data[offs[s]: offs[s] + ln].cpu().numpy()
+        rc, ref, _ = O.replay([seg])
+        got = t[starts[s]: starts[s + 1]].copy()
+        got["seg_idx"] = 0
+        got["flags"] = 0
+        assert rc == 0 and np.array_equal(got, ref)

@@ -34,7 +34,8 @@ def test_multi_matches_oracle(devices, n_segs):
         r = mc.replay(segs, expected=man)
         rc, ref, _ = O.replay(segs, expected=man)
         assert r.status == rc == 0 and np.array_equal(r.tuples, ref)
-        assert r.stats.n_crc_fail == int(np.count_nonzero(ref["flags"] & K.TF_CRC_FAIL)) > 0
+        fails = int(np.count_nonzero(ref["flags"] & K.TF_CRC_FAIL))
+        assert r.stats.n_crc_fail == fails and (fails > 0 or n_segs < 5)
     finally:
         mc.close()
 
