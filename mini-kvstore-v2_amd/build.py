@@ -57,7 +57,7 @@ def build(force=False, verbose=False):
     orc = os.path.join(ROOT, "oracle", "liboracle.so")
     src = os.path.join(ROOT, "oracle", "replay_ref.c")
     if force or _newer(orc, [src, os.path.join(ROOT, "include", "kvreplay.h")]):
-        _run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-Wall", "-o", orc, src])
+        _run(["gcc", "-O3", "-std=c11", "-fPIC", "-shared", "-Wall", "-o", orc, src])
         if verbose:
             print("built", orc)
     return rep, host, orc

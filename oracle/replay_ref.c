@@ -193,6 +193,91 @@ int oracle_replay(const oracle_seg *segs, size_t n_segs,
 }
 
 /* ------------------------------------------------------------------------------------------
+ * oracle_replay_s16 — the strong CPU baseline (SURVEY §8d ii): oracle_replay's walk and tuples
+ * with a slice-by-16 CRC-32 (16 byte tables, 16 bytes per step), for one thread per segment.
+ * Same results as oracle_replay (tests/test_oracle_golden.py compares them).
+ * ---------------------------------------------------------------------------------------- */
+static uint32_t g_s16[16][256];
+static int g_s16_ready = 0;
+
+static void s16_init(void) {
+    crc_init();
+    for (int i = 0; i < 256; ++i) g_s16[0][i] = g_crc_table[i];
+    for (int t = 1; t < 16; ++t)
+        for (int i = 0; i < 256; ++i) g_s16[t][i] = (g_s16[t - 1][i] >> 8) ^ g_s16[0][g_s16[t - 1][i] & 0xFFu];
+    g_s16_ready = 1;
+}
+
+uint32_t oracle_crc32_s16(uint32_t crc, const uint8_t *p, size_t n) {
+    if (!g_s16_ready) s16_init();
+    uint32_t c = ~crc;
+    while (n >= 16) {
+        const uint32_t a = rd_u32le(p) ^ c, b = rd_u32le(p + 4), d = rd_u32le(p + 8), e = rd_u32le(p + 12);
+        c = g_s16[15][a & 255] ^ g_s16[14][(a >> 8) & 255] ^ g_s16[13][(a >> 16) & 255] ^ g_s16[12][a >> 24] ^
+            g_s16[11][b & 255] ^ g_s16[10][(b >> 8) & 255] ^ g_s16[9][(b >> 16) & 255] ^ g_s16[8][b >> 24] ^
+            g_s16[7][d & 255] ^ g_s16[6][(d >> 8) & 255] ^ g_s16[5][(d >> 16) & 255] ^ g_s16[4][d >> 24] ^
+            g_s16[3][e & 255] ^ g_s16[2][(e >> 8) & 255] ^ g_s16[1][(e >> 16) & 255] ^ g_s16[0][e >> 24];
+        p += 16;
+        n -= 16;
+    }
+    while (n--) c = (c >> 8) ^ g_s16[0][(c ^ *p++) & 0xFFu];
+    return ~c;
+}
+
+int oracle_replay_s16(const oracle_seg *segs, size_t n_segs, kvr_tuple *out, size_t cap, size_t *n_out,
+                      kvr_error *err) {
+    if (!g_s16_ready) s16_init();
+    size_t nt = 0;
+    if (err) memset(err, 0, sizeof(*err));
+    for (size_t si = 0; si < n_segs; ++si) {
+        const uint8_t *b = segs[si].bytes;
+        const uint64_t n = segs[si].len;
+        uint64_t p = 0;
+        while (p < n) {                                                   /* engine.rs:88-91 */
+            const uint8_t op = b[p];
+            kvr_error e = {0, (uint32_t)si, p, 0};
+            if (n - p < 5) { e.kind = KVR_E_KEY_LEN; goto fail; }
+            const uint64_t klen = rd_u32le(b + p + 1);
+            if (n - (p + 5) < klen) { e.kind = KVR_E_KEY; goto fail; }
+            {
+                uint64_t vu; uint32_t el;
+                if (!oracle_utf8_check(b + p + 5, (size_t)klen, &vu, &el)) {
+                    e.kind = KVR_E_UTF8; e.aux = vu | ((uint64_t)el << 32); goto fail;
+                }
+            }
+            kvr_tuple t;
+            memset(&t, 0, sizeof(t));
+            t.rec_off = p; t.seg_idx = (uint32_t)si; t.key_len = (uint32_t)klen; t.op = op;
+            t.key_tag = oracle_crc32_s16(0, b + p + 5, (size_t)klen);
+            uint64_t next;
+            if (op == 0) {
+                const uint64_t q = p + 5 + klen;
+                if (n - q < 4) { e.kind = KVR_E_VAL_LEN; goto fail; }
+                const uint64_t vlen = rd_u32le(b + q);
+                if (n - (q + 4) < vlen) { e.kind = KVR_E_VAL; goto fail; }
+                t.val_len = (uint32_t)vlen;
+                t.crc32 = oracle_crc32_s16(0, b + q + 4, (size_t)vlen);
+                next = q + 4 + vlen;
+            } else if (op == 1) {
+                next = p + 5 + klen;
+            } else {
+                e.kind = KVR_E_OPCODE; e.aux = op; goto fail;
+            }
+            if (out && nt < cap) out[nt] = t;
+            ++nt;
+            p = next;
+            continue;
+        fail:
+            if (err) *err = e;
+            if (n_out) *n_out = nt;
+            return KVR_CORRUPTED;
+        }
+    }
+    if (n_out) *n_out = nt;
+    return (out && nt > cap) ? KVR_CAPACITY : KVR_OK;
+}
+
+/* ------------------------------------------------------------------------------------------
  * Last-writer-wins fold (engine.rs:137 insert / :141 remove, segments in id order :55):
  * live[i] = 1 iff tuple i is a SET and no later tuple (in tuple order) names the same key.
  * Keys are compared by bytes (read at rec_off + 5 of their segment).  Returns live count.
@@ -358,9 +443,21 @@ static void vm_grow(vmap_t *m) {
     free(old);
 }
 
+/* the map the last faithful replay built: KVStore::open hands it to the caller (engine.rs:70-75)
+ * rather than dropping it, so releasing it is not part of the timed replay */
+static vmap_t g_faithful_map = {0};
+
+void oracle_faithful_release(void) {
+    vmap_t *m = &g_faithful_map;
+    for (size_t i = 0; i < m->cap; ++i) if (m->s[i].used == 1) { free(m->s[i].key); free(m->s[i].val); }
+    free(m->s);
+    memset(m, 0, sizeof(*m));
+}
+
 int oracle_replay_faithful(const oracle_seg *segs, size_t n_segs, uint64_t *num_keys,
                            uint64_t *total_bytes, uint64_t *n_records, uint64_t *digest,
                            kvr_error *err) {
+    oracle_faithful_release();
     vmap_t m = {0}; vm_grow(&m);
     bufrd_t *r = (bufrd_t *)malloc(sizeof(bufrd_t));
     uint64_t nrec = 0, crc_acc = 0;
@@ -407,13 +504,16 @@ int oracle_replay_faithful(const oracle_seg *segs, size_t n_segs, uint64_t *num_
             break;
         }
     }
-    uint64_t nk = 0, tb = 0, dg = crc_acc * 0x9E3779B97F4A7C15ull;
+    /* stats() (engine.rs:253-255) and a digest from what the walk already computed: the per-value
+     * CRCs summed during the replay and the live keys' hashes and lengths (no second pass over
+     * the values) */
+    uint64_t nk = m.n, tb = 0, dg = crc_acc * 0x9E3779B97F4A7C15ull;
     for (size_t i = 0; i < m.cap; ++i) if (m.s[i].used == 1) {
-        ++nk; tb += m.s[i].vlen;
-        dg += (uint64_t)oracle_crc32(0, m.s[i].val, m.s[i].vlen) * (m.s[i].h | 1);
-        free(m.s[i].key); free(m.s[i].val);
+        tb += m.s[i].vlen;
+        dg += (uint64_t)m.s[i].vlen * (m.s[i].h | 1);
     }
-    free(m.s); free(r);
+    g_faithful_map = m;
+    free(r);
     if (num_keys) *num_keys = nk;
     if (total_bytes) *total_bytes = tb;
     if (n_records) *n_records = nrec;

@@ -42,6 +42,12 @@ def lib():
         L.oracle_replay_faithful.argtypes = [C.POINTER(OSeg), C.c_size_t, C.POINTER(C.c_uint64),
                                              C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                              C.POINTER(Error)]
+        L.oracle_faithful_release.argtypes = []
+        L.oracle_faithful_release.restype = None
+        L.oracle_crc32_s16.argtypes = [C.c_uint32, C.c_void_p, C.c_size_t]
+        L.oracle_crc32_s16.restype = C.c_uint32
+        L.oracle_replay_s16.argtypes = [C.POINTER(OSeg), C.c_size_t, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t),
+                                        C.POINTER(Error)]
         _lib = L
     return _lib
 
@@ -101,14 +107,40 @@ def fold_live(segments, tuples):
     return live[: len(t)].astype(bool), int(nk), int(tb.value)
 
 
-def replay_faithful(segments):
-    """The reference's cost model (CPU baseline). -> (rc, num_keys, total_bytes, n_records, digest, Error)"""
+def replay_faithful(segments, release=True):
+    """The reference's cost model (CPU baseline). -> (rc, num_keys, total_bytes, n_records, digest, Error).
+    The map it builds stays allocated until faithful_release() (release=True does it at once;
+    bench.py times the replay alone and releases after the clock stops)."""
     arrs, segs = _segs(segments)
     nk, tb, nr, dg = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
     err = Error()
     rc = lib().oracle_replay_faithful(segs, len(arrs), C.byref(nk), C.byref(tb), C.byref(nr), C.byref(dg),
                                       C.byref(err))
+    if release:
+        faithful_release()
     return rc, nk.value, tb.value, nr.value, dg.value, err
+
+
+def faithful_release():
+    lib().oracle_faithful_release()
+
+
+def crc32_s16(data, crc=0):
+    a = _as_u8(data)
+    return int(lib().oracle_crc32_s16(crc, a.ctypes.data if a.size else None, a.size))
+
+
+def replay_s16(segments, cap=None):
+    """oracle_replay with the slice-by-16 CRC (the strong CPU baseline's kernel) -> (status, tuples, Error)"""
+    arrs, segs = _segs(segments)
+    total = sum(a.size for a in arrs)
+    if cap is None:
+        cap = total // 5 + 16
+    out = np.zeros(cap, dtype=TUPLE_DTYPE)
+    n = C.c_size_t()
+    err = Error()
+    rc = lib().oracle_replay_s16(segs, len(arrs), out.ctypes.data, cap, C.byref(n), C.byref(err))
+    return rc, out[: min(n.value, cap)], err
 
 
 def compact(segments, seg_target=0, seg_ids=None):

@@ -199,3 +199,34 @@ def test_faithful_baseline_agrees_with_fold():
     assert (rc, nk, tb, nr) == (0, 2, 7, 5)
     rc, *_ , err = O.replay_faithful([bytes.fromhex("0002000000ff00")])
     assert rc == 1 and err.kind == 4
+
+
+def test_slice16_baseline_matches_oracle(golden):
+    """The strong CPU baseline's kernel (slice-by-16 CRC) gives oracle_replay's tuples and errors."""
+    assert O.crc32_s16(b"123456789") == 0xCBF43926 == int(golden["crc_check"]["crc32"], 16)
+    rng = random.Random(11)
+    for n in list(range(0, 40)) + [255, 4096, 65537]:
+        b = bytes(rng.getrandbits(8) for _ in range(n))
+        assert O.crc32_s16(b) == zlib.crc32(b)
+        k = n // 3
+        assert O.crc32_s16(b[k:], O.crc32_s16(b[:k])) == zlib.crc32(b)
+    for name in ("compaction_example", "persistence"):
+        ids, segs = read_dir(name)
+        rc, t, err = O.replay(segs)
+        rc16, t16, err16 = O.replay_s16(segs)
+        assert rc == rc16 == 0 and np.array_equal(t, t16)
+    for bad in (bytes.fromhex("0002000000ff00"), b"\x00\x01\x00\x00\x00a\x01", b"\x07\x00\x00\x00\x00"):
+        rc, _, err = O.replay([bad])
+        rc16, _, err16 = O.replay_s16([bad])
+        assert rc == rc16 == 1
+        assert (err.kind, err.seg_idx, err.rec_off, err.aux) == (err16.kind, err16.seg_idx, err16.rec_off, err16.aux)
+
+
+def test_faithful_map_release_is_separate():
+    """replay_faithful(release=False) keeps the map (the reference's open() returns it); release frees it."""
+    ids, segs = read_dir("compaction_example")
+    r1 = O.replay_faithful(segs, release=False)
+    O.faithful_release()
+    O.faithful_release()   # idempotent
+    r2 = O.replay_faithful(segs)
+    assert r1[:5] == r2[:5]
