@@ -145,6 +145,62 @@ int  kvr_last_stats(const kvr_ctx *ctx, kvr_stats *out);
 int  kvr_replay_live(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint32_t flags,
                      kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err);
 
+/* ---- the open-time index on the device (engine.rs:24-76, index.rs:5-7) ---------------------
+ * kvr_replay_index = kvr_replay_live plus a hash table over the live keys built in HBM, so the
+ * host receives the reference's HashMap (every live key -> its final SET) as two flat arrays and
+ * folds nothing itself:
+ *   live[0 .. *n_live)     each live key's final SET tuple, in (segment, offset) order — exactly
+ *                          kvr_replay_live's output; *n_live = stats().num_keys
+ *   slots[0 .. *n_slots)   slots[h] = 1 + index into live[] (0 = free); *n_slots =
+ *                          kvr_index_slots(*n_live); a key's home slot is
+ *                          kvr_index_hash(CRC-32 of the key) & (*n_slots - 1), then linear probing.
+ *                          Which free slot an insert took may differ between runs; lookups do not.
+ * flags: KVR_SEGS_ON_DEVICE, KVR_OUT_ON_DEVICE (live and slots are device pointers).
+ * Returns as kvr_replay_live; KVR_CAPACITY when live_cap < *n_live or slot_cap < *n_slots — the
+ * result then stays in the context until its next call, and kvr_index_fetch copies it out. */
+typedef struct kvr_index_stats {
+    double   ms_wall;       /* host wall time of the call                                         */
+    double   ms_replay;     /* the replay pipeline (device)                                       */
+    double   ms_fold;       /* fold rounds, live list and key table (device)                      */
+    uint64_t bytes_in;
+    uint64_t n_tuples;      /* records replayed                                                   */
+    uint64_t n_live;
+    uint64_t n_slots;
+    uint32_t fold_rounds;   /* probe rounds of the fold (1 + rounds for keys sharing a CRC-32)     */
+    uint32_t pad;
+} kvr_index_stats;
+
+int      kvr_replay_index(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint32_t flags,
+                          kvr_tuple *live, size_t live_cap, uint32_t *slots, uint64_t slot_cap,
+                          size_t *n_live, uint64_t *n_slots, kvr_error *err);
+int      kvr_index_fetch(kvr_ctx *ctx, uint32_t flags, kvr_tuple *live, size_t live_cap, uint32_t *slots,
+                         uint64_t slot_cap);
+int      kvr_last_index_stats(const kvr_ctx *ctx, kvr_index_stats *out);
+uint64_t kvr_index_slots(uint64_t n_live);     /* max(16, the power of two >= 2 n_live)            */
+uint32_t kvr_index_hash(uint32_t key_tag);     /* MurmurHash3 fmix32                               */
+/* Host lookup of key (klen bytes) in an index whose keys live in segs[] (host bytes): the index
+ * into live[] of its final SET, or -1 when the key is not live (engine.rs:200 get -> None). */
+int64_t  kvr_index_find(const kvr_tuple *live, const uint32_t *slots, uint64_t n_slots, const kvr_segment *segs,
+                        const uint8_t *key, size_t klen);
+/* The same table built on the host from a live list (the host-fold path): n_slots a power of two
+ * > n_live (kvr_index_slots(n_live) gives the device's size). */
+int      kvr_index_build_host(const kvr_tuple *live, size_t n_live, uint32_t *slots, uint64_t n_slots);
+
+/* ---- ingest: the store's files into HBM while they are being read -------------------------
+ * kvr_ingest_begin reserves HBM for total_bytes of segments (KVR_ENOMEM when they do not fit:
+ * replay them batch-wise with kvr_replay_stream instead).  kvr_ingest_push queues the copy of one
+ * segment (ascending seg_id, as engine.rs:51 orders them) on the context's copy stream and returns:
+ * pinned bytes (kvr_host_alloc) are DMA'd asynchronously and must stay unchanged until
+ * kvr_ingest_index returns.  kvr_ingest_index = kvr_replay_index over the pushed segments once
+ * their copies land (seg_idx = push order).  flags: KVR_OUT_ON_DEVICE. */
+int  kvr_ingest_begin(kvr_ctx *ctx, uint64_t total_bytes, size_t n_segs);
+int  kvr_ingest_push(kvr_ctx *ctx, uint64_t seg_id, const uint8_t *bytes, uint64_t len);
+int  kvr_ingest_index(kvr_ctx *ctx, uint32_t flags, kvr_tuple *live, size_t live_cap, uint32_t *slots,
+                      uint64_t slot_cap, size_t *n_live, uint64_t *n_slots, kvr_error *err);
+/* Pinned (page-locked) host memory for segment bytes: hipHostMalloc / hipHostFree. */
+int  kvr_host_alloc(uint64_t bytes, void **out);
+void kvr_host_free(void *p);
+
 /* ---- streamed ingest: host segments larger than one transfer ----------
  * The same loop as kvr_replay (engine.rs:55-57) over host-resident segment bytes, e.g. files
  * read (engine.rs:80-83) into memory: consecutive segments are grouped into batches of at most

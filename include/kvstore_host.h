@@ -65,6 +65,33 @@ typedef struct kvs_stats {          /* StoreStats, src/store/stats.rs:3-10 */
  * (engine.rs:59-68).  On KVR_CORRUPTED, *err and msg (the exact engine.rs message, without
  * error.rs's "Corrupted data: " prefix) describe the first error. */
 int kvs_open(const char *dir, kvr_ctx *ctx, kvs_store **out, kvr_error *err, char *msg, size_t msg_cap);
+/* kvs_open with options.  The default path: up to 16 reader threads pread the files (8-MiB
+ * pieces, store order) into one pinned arena (kvr_host_alloc); each segment is pushed to HBM
+ * (kvr_ingest_push) as soon as its bytes are in, so reading and PCIe overlap; then
+ * kvr_ingest_index replays, folds and builds the key table on the GPU and only the live tuples
+ * and the table come back.  When the store does not fit in HBM (KVR_ENOMEM) or exceeds the
+ * fold's 2^31-tuple limit (KVR_EINVAL), the host-fold path takes over: kvr_replay_stream in
+ * batches, kvh_fold_parallel, kvr_index_build_host.  Both give the same index.
+ * An unopenable segment k is reported (KVR_E_OPEN) only when segments 0 .. k-1 replay cleanly,
+ * as engine.rs:55-57 opens the files one after the other. */
+#define KVS_OPEN_HOST_FOLD  0x1u   /* force the host-fold path                         */
+#define KVS_OPEN_NO_PIN     0x2u   /* read into pageable memory (no kvr_host_alloc)     */
+#define KVS_PATH_DEVICE_INDEX 1u
+#define KVS_PATH_HOST_FOLD    2u
+typedef struct kvs_open_stats {
+    double   ms_total;       /* the whole kvs_open_ex call                                        */
+    double   ms_alloc;       /* the segments' host arena (pinning)                                 */
+    double   ms_read;        /* reader threads, first piece to last (transfers overlap it)          */
+    double   ms_index;       /* last byte read -> index ready: transfer tail, replay, fold, copies  */
+    uint64_t bytes;          /* segment bytes read                                                 */
+    uint64_t n_segments;
+    uint64_t n_live;         /* stats().num_keys                                                   */
+    uint32_t path;           /* KVS_PATH_DEVICE_INDEX or KVS_PATH_HOST_FOLD (last index build)      */
+    uint32_t read_threads;
+} kvs_open_stats;
+int kvs_open_ex(const char *dir, kvr_ctx *ctx, uint32_t flags, kvs_store **out, kvr_error *err, char *msg,
+                size_t msg_cap);
+int kvs_last_open_stats(const kvs_store *s, kvs_open_stats *out);
 /* KVStore::get (engine.rs:200): 1 and the value bytes if live, 0 if absent. */
 int kvs_get(const kvs_store *s, const uint8_t *key, size_t klen, const uint8_t **val, size_t *vlen);
 /* Index entry (index.rs:7 shape): segment id, value offset inside that segment file, length. */

@@ -87,10 +87,13 @@ struct kvr_ctx {
     DevBuf<GenRecDev> gen;
     // compaction (kvr_compact)
     DevBuf<kvr_tuple> ctup, lout;
-    DevBuf<uint32_t> ht_rep, ht_best, cslot, cflag, cpos, cfirst;
+    DevBuf<FoldEnt> fent;                  // the fold table (k_fold_claim / k_fold_verify)
+    DevBuf<uint32_t> flist, fcnt;          // collision rounds: two tuple lists, their counts
+    DevBuf<uint32_t> cslot, cflag, cpos, cfirst;
     DevBuf<uint64_t> csize, coff, l_src, l_off, ctot, ccuts;
     DevBuf<uint8_t> cout, ctmp;
     kvr_compact_stats cstats{};
+    uint32_t fold_rounds = 0;              // probe rounds of the last fold (1 = no tag collision)
     size_t c_nt = 0;                       // tuples of the last compaction front half
     uint32_t c_ranks = 0;                  // sharded compaction state (kvr_compact_stage .. finish)
     bool c_staged = false;
@@ -122,6 +125,15 @@ struct kvr_ctx {
     DevBuf<uint8_t> e_data;
     kvr_etag_stats estats{};
     uint32_t e_wg_per_cu = 0;
+    // open-time index (kvr_replay_index) and ingest (kvr_ingest_*): the live list stays in lout,
+    // the key table in islots, until the next call
+    DevBuf<uint32_t> islots;
+    uint64_t ix_live = 0, ix_slots = 0;
+    bool ix_valid = false;
+    kvr_index_stats istats{};
+    DevBuf<uint8_t> ing;                   // the store's segment bytes, resident in HBM
+    uint64_t ing_off = 0;
+    std::vector<kvr_segment> ing_segs;     // device pointers into ing, in push order
 };
 
 #define HIPCHK(x)                                   \
@@ -266,7 +278,8 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->pool.release(); c->dense.release(); c->redo.release(); c->link.release(); c->ctr.release();
     c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->bsum.release();
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
-    c->ctup.release(); c->lout.release(); c->ht_rep.release(); c->ht_best.release(); c->cslot.release(); c->cflag.release();
+    c->ctup.release(); c->lout.release(); c->fent.release(); c->flist.release(); c->fcnt.release();
+    c->cslot.release(); c->cflag.release(); c->islots.release(); c->ing.release();
     c->cpos.release(); c->cfirst.release(); c->csize.release(); c->coff.release(); c->l_src.release();
     c->l_off.release(); c->ctot.release(); c->ccuts.release(); c->cout.release(); c->ctmp.release();
     c->c_gidx.release(); c->c_own.release(); c->c_sidx.release(); c->c_val.release(); c->c_scan.release();
@@ -559,14 +572,23 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
 // ---------------------------------------------------------------------------------------
 // live-record rewrite (kvr_compact.hip): replay -> fold -> live list -> gather -> cuts
 // ---------------------------------------------------------------------------------------
-// replay + the local last-writer fold (k_fold_insert): the front half of every compaction
-static int compact_front(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, kvr_error *err, size_t *nt_out) {
+// replay + the local last-writer fold (k_fold_claim / k_fold_verify): the front half of every
+// compaction and of kvr_replay_live / kvr_replay_index.  It reuses the buffers of a staged
+// sharded compaction, so it ends one (kvr_compact_export / _finish then return KVR_EINVAL until
+// the next kvr_compact_stage).  rewrite: also size the buffers of the byte rewrite
+// (compact_back).  cs: the statistics this call fills (the caller's, so a live replay leaves
+// kvr_last_compact_stats alone).
+static int compact_front(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, kvr_error *err, size_t *nt_out,
+                         bool rewrite, kvr_compact_stats *cs) {
     *nt_out = 0;
-    memset(&c->cstats, 0, sizeof(c->cstats));
+    c->c_staged = false;
+    c->c_nt = 0;
+    c->fold_rounds = 0;
+    memset(cs, 0, sizeof(*cs));
     if (err) memset(err, 0, sizeof(*err));
     uint64_t bytes_in = 0;
     for (size_t i = 0; i < n; ++i) bytes_in += segs[i].len;
-    c->cstats.bytes_in = bytes_in;
+    cs->bytes_in = bytes_in;
     if (n == 0) return KVR_OK;
     // 1. replay into context-resident tuples; the segment bytes stay in HBM (c->segs)
     size_t nt = 0;
@@ -578,30 +600,50 @@ static int compact_front(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t
         rc = kvr_replay(c, segs, n, rflags, nullptr, 0, c->ctup.p, c->ctup.n, &nt, err);
     }
     if (rc != KVR_OK) return rc;
-    c->cstats.ms_replay = c->stats.ms_total;
-    c->cstats.n_tuples = nt;
-    c->c_nt = nt;
+    cs->ms_replay = c->stats.ms_total;
+    cs->n_tuples = nt;
     *nt_out = nt;
     if (nt == 0) return KVR_OK;
     if (nt >= 0x7FFFFFFFull) return KVR_EINVAL;   // 32-bit tuple indices in the fold table
+    c->c_nt = nt;
     hipStream_t st = c->stream;
-    // 2. the key's last tuple (open addressing over the key bytes)
+    // 2. the key's last tuple (open addressing over the key bytes, kvr_compact.hip)
     uint64_t slots = 1;
     while (slots < 2 * (uint64_t)nt) slots <<= 1;
-    if (c->ht_rep.ensure(slots) || c->ht_best.ensure(slots) || c->cslot.ensure(nt) || c->cflag.ensure(nt) ||
-        c->cpos.ensure(nt) || c->csize.ensure(nt) || c->coff.ensure(nt) || c->l_src.ensure(nt) ||
-        c->l_off.ensure(nt + 1) || c->ctot.ensure(2))
+    if (c->fent.ensure(slots) || c->cslot.ensure(nt) || c->cflag.ensure(nt) || c->cpos.ensure(nt) ||
+        c->csize.ensure(nt) || c->flist.ensure(2 * nt) || c->fcnt.ensure(1))
+        return KVR_ENOMEM;
+    if (rewrite && (c->coff.ensure(nt) || c->l_src.ensure(nt) || c->l_off.ensure(nt + 1) || c->ctot.ensure(2)))
         return KVR_ENOMEM;
     size_t t1 = 0, t2 = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, c->csize.p, c->coff.p, (int)nt, st));
+    if (rewrite) HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, c->csize.p, c->coff.p, (int)nt, st));
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, c->cflag.p, c->cpos.p, (int)nt, st));
     if (c->ctmp.ensure(std::max(t1, t2))) return KVR_ENOMEM;
     HIPCHK(hipEventRecord(c->ev[0], st));
-    HIPCHK(hipMemsetAsync(c->ht_rep.p, 0xFF, slots * 4, st));
-    HIPCHK(hipMemsetAsync(c->ht_best.p, 0, slots * 4, st));
-    hipLaunchKernelGGL(k_fold_insert, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, st, c->ctup.p, (uint64_t)nt,
-                       c->segs.p, c->ht_rep.p, c->ht_best.p, (uint32_t)(slots - 1), c->cslot.p);
-    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemsetAsync(c->fent.p, 0xFF, slots * sizeof(FoldEnt), st));
+    const uint32_t mask = (uint32_t)(slots - 1);
+    const uint32_t *list = nullptr;   // round 0: every tuple
+    uint64_t m = nt;
+    for (uint32_t r = 0;; ++r) {
+        uint32_t *next = c->flist.p + (uint64_t)(r & 1u) * nt;
+        const uint32_t g = (uint32_t)((m + 255) / 256);
+        HIPCHK(hipMemsetAsync(c->fcnt.p, 0, 4, st));
+        hipLaunchKernelGGL(k_fold_claim, dim3(g), dim3(256), 0, st, c->ctup.p, m, list, c->segs.p, c->fent.p, mask,
+                           c->cslot.p);
+        hipLaunchKernelGGL(k_fold_verify, dim3(g), dim3(256), 0, st, c->ctup.p, m, list, c->segs.p, c->fent.p, mask,
+                           c->cslot.p, next, c->fcnt.p);
+        HIPCHK(hipGetLastError());
+        uint32_t left = 0;
+        HIPCHK(hipMemcpyAsync(&left, c->fcnt.p, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        c->fold_rounds = r + 1;
+        if (left == 0) break;
+        // tuples whose tag another key holds: each round moves every one of them at least one
+        // entry on, so mask + 1 rounds bound the loop (a few in practice)
+        if (r > mask) return KVR_EHIP;
+        list = next;
+        m = left;
+    }
     return KVR_OK;
 }
 
@@ -684,10 +726,10 @@ int kvr_compact(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, u
     *out_len = 0;
     *n_out_segs = 0;
     size_t nt = 0;
-    const int rc = compact_front(c, segs, n, flags, err, &nt);
+    const int rc = compact_front(c, segs, n, flags, err, &nt, true, &c->cstats);
     if (rc != KVR_OK || nt == 0) return rc;
     hipLaunchKernelGGL(k_live, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, c->stream, c->ctup.p, (uint64_t)nt,
-                       c->ht_best.p, c->cslot.p, c->csize.p, c->cflag.p);
+                       c->fent.p, c->cslot.p, c->csize.p, c->cflag.p);
     HIPCHK(hipGetLastError());
     return compact_back(c, flags, seg_target, out, out_cap, out_len, seg_ends, seg_cap, n_out_segs);
 }
@@ -697,9 +739,8 @@ int kvr_compact_stage(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
     if (!c || (!segs && n) || (n && !gidx) || n_ranks == 0 || !counts || !key_bytes) return KVR_EINVAL;
     for (uint32_t o = 0; o < n_ranks; ++o) counts[o] = key_bytes[o] = 0;
     c->c_ranks = n_ranks;
-    c->c_staged = false;
     size_t nt = 0;
-    const int rc = compact_front(c, segs, n, flags, err, &nt);
+    const int rc = compact_front(c, segs, n, flags, err, &nt, true, &c->cstats);
     if (rc != KVR_OK) return rc;
     c->c_staged = true;
     if (nt == 0) return KVR_OK;
@@ -714,7 +755,7 @@ int kvr_compact_stage(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
     if (c->ctmp.n < t3 && c->ctmp.ensure(t3)) return KVR_ENOMEM;
     HIPCHK(hipMemcpyAsync(c->c_gidx.p, gidx, n * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(c->c_gstart.p, 0, 2 * (n_ranks + 1) * 8, st));
-    hipLaunchKernelGGL(k_cand, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->ht_best.p, c->cslot.p, n_ranks,
+    hipLaunchKernelGGL(k_cand, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->fent.p, c->cslot.p, n_ranks,
                        c->c_own.p);
     for (uint32_t o = 0; o < n_ranks; ++o) {   // one group per owner rank, in owner order
         hipLaunchKernelGGL(k_cand_val, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->c_own.p, o, c->c_val.p);
@@ -785,7 +826,7 @@ int kvr_compact_finish(kvr_ctx *c, const uint8_t *d_win, uint32_t flags, uint64_
     const size_t nt = c->c_nt;
     if (nt == 0) return KVR_OK;
     hipLaunchKernelGGL(k_live_global, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, c->stream, c->ctup.p,
-                       (uint64_t)nt, c->ht_best.p, c->cslot.p, c->c_sidx.p, d_win, c->csize.p, c->cflag.p);
+                       (uint64_t)nt, c->fent.p, c->cslot.p, c->c_sidx.p, d_win, c->csize.p, c->cflag.p);
     HIPCHK(hipGetLastError());
     return compact_back(c, flags, seg_target, out, out_cap, out_len, seg_ends, seg_cap, n_out_segs);
 }
@@ -1131,57 +1172,5 @@ void kvr_etag_format(uint32_t crc, char *out) {
 
 }  // extern "C"
 
-// ---------------------------------------------------------------------------------------
-// replay + last-writer fold in HBM: only the live index leaves the device (SURVEY §8b
-// dedup_last_writer; engine.rs:137 / :141)
-// ---------------------------------------------------------------------------------------
-namespace {
-__global__ void k_live_tuples(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ flag,
-                              const uint32_t *__restrict__ pos, kvr_tuple *__restrict__ out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n && flag[i]) out[pos[i]] = tup[i];
-}
-}  // namespace
-
-extern "C" {
-
-int kvr_replay_live(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, kvr_tuple *out, size_t cap,
-                    size_t *n_out, kvr_error *err) {
-    if (!c || (!segs && n) || !n_out || (cap && !out)) return KVR_EINVAL;
-    if (flags & ~(KVR_SEGS_ON_DEVICE | KVR_OUT_ON_DEVICE)) return KVR_EINVAL;
-    *n_out = 0;
-    size_t nt = 0;
-    int rc = compact_front(c, segs, n, flags, err, &nt);   // replay + k_fold_insert (kvr_compact.hip)
-    if (rc != KVR_OK || nt == 0) return rc;
-    hipStream_t st = c->stream;
-    const uint32_t g = (uint32_t)((nt + 255) / 256);
-    hipLaunchKernelGGL(k_live, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->ht_best.p, c->cslot.p,
-                       c->csize.p, c->cflag.p);
-    HIPCHK(hipGetLastError());
-    size_t tb = c->ctmp.n;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->cflag.p, c->cpos.p, (int)nt, st));
-    uint32_t last[2] = {0, 0};
-    HIPCHK(hipMemcpyAsync(&last[0], c->cpos.p + nt - 1, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(&last[1], c->cflag.p + nt - 1, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    const uint64_t total = (uint64_t)last[0] + last[1];
-    *n_out = total;
-    c->cstats.n_live = total;
-    if (total > cap) return KVR_CAPACITY;
-    if (total == 0) return KVR_OK;
-    kvr_tuple *d_out = out;
-    if (!(flags & KVR_OUT_ON_DEVICE)) {
-        if (c->lout.ensure(total)) return KVR_ENOMEM;
-        d_out = c->lout.p;
-    }
-    hipLaunchKernelGGL(k_live_tuples, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->cflag.p, c->cpos.p, d_out);
-    HIPCHK(hipGetLastError());
-    if (!(flags & KVR_OUT_ON_DEVICE))
-        HIPCHK(hipMemcpyAsync(out, d_out, total * sizeof(kvr_tuple), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    return KVR_OK;
-}
-
-}  // extern "C"
-
+#include "kvr_index.hip"
 #include "kvr_multi.hip"

@@ -8,10 +8,18 @@
  *
  * Input: the replay tuples of the store (kvr_replay, in (segment, offset) order) and the
  * segment bytes in HBM.  Device pipeline, one stream:
- *   k_fold_insert   every tuple into an open-addressing table keyed by its key bytes
- *                   (key_tag = CRC-32 of the key as the hash): atomicCAS claims an empty slot
- *                   for the key's first tuple, atomicMax keeps the key's LAST tuple index — the
- *                   last-writer-wins fold of engine.rs:137 / :141 as an associative max
+ *   k_fold_claim    every tuple into an open-addressing table of 32-B entries keyed by its
+ *                   key bytes (key_tag = CRC-32 of the key as the hash): an atomicCAS of
+ *                   (tag << 32 | tuple) claims an empty entry for a key's first tuple, whose
+ *                   length and first 16 key bytes the claimer copies into the entry; a tuple
+ *                   that meets its own tag stops there (tentatively)
+ *   k_fold_verify   every tuple checks its key against the entry it stopped at (length and the
+ *                   16-B prefix from the entry itself, the rest of a longer key from the
+ *                   representative's bytes) and, when equal, keeps the key's LAST tuple index by
+ *                   atomicMin of ~index — the last-writer-wins fold of engine.rs:137 / :141 as
+ *                   an associative max.  A tag collision between two keys sends the tuple to the
+ *                   next round, which resumes its probe one entry further (rounds until no tuple
+ *                   is left; distinct keys sharing a CRC-32 are a few hundred per million keys)
  *   k_live          a tuple is live iff it is a SET and its key's last tuple: size 9 + k + v
  *   (scan)          exclusive sums of sizes (output offsets) and live flags (dense index)
  *   k_scatter       dense live list (source address, output offset) and, for every 512-B
@@ -71,38 +79,112 @@ __device__ bool key_eq(const SegDesc *segs, const kvr_tuple &a, const kvr_tuple 
     return bytes_eq(key_ptr(segs, a), key_ptr(segs, b), a.key_len);
 }
 
-// the table: rep[h] = the key's first tuple (HT_EMPTY: free), best[h] = 1 + the key's last
-// tuple (0: none); mask + 1 slots, at least 2 n
-__global__ void k_fold_insert(const kvr_tuple *__restrict__ tup, uint64_t n, const SegDesc *__restrict__ segs,
-                              uint32_t *__restrict__ rep, uint32_t *__restrict__ best, uint32_t mask,
-                              uint32_t *__restrict__ slot) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// the fold table: one 32-B entry per slot, at least 2 n slots (a power of two)
+struct __align__(32) FoldEnt {
+    unsigned long long tagrep;   // (key_tag << 32) | representative tuple; FE_EMPTY: free
+    uint32_t best;               // ~(the key's last tuple index); every claimed entry has one
+    uint32_t klen;               // the representative's key length
+    uint32_t key[4];             // its first 16 key bytes, zero padded
+};
+static_assert(sizeof(FoldEnt) == 32, "fold entry");
+constexpr unsigned long long FE_EMPTY = ~0ull;   // the table is memset to 0xFF
+
+// bytes [0, min(klen, 16)) of the key of tuple t, zero padded.  Aligned dword loads: a dword is
+// read only if it starts before the segment's end, so it holds a segment byte and cannot cross
+// into an unmapped page, whatever padding the caller's buffer has.
+__device__ __forceinline__ void key_prefix16(const SegDesc &g, const kvr_tuple &t, uint32_t w[4]) {
+    const uintptr_t p = reinterpret_cast<uintptr_t>(g.base) + t.rec_off + 5;
+    const uintptr_t end = reinterpret_cast<uintptr_t>(g.base) + g.len;
+    const uintptr_t pa = p & ~(uintptr_t)3;
+    const uint32_t sh = (uint32_t)(p & 3u);
+    uint32_t d[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        d[k] = pa + 4u * k < end ? *reinterpret_cast<const uint32_t *>(pa + 4u * k) : 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t x = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+        const int valid = (int)t.key_len - 4 * j;   // bytes of this dword inside the key
+        w[j] = valid >= 4 ? x : valid <= 0 ? 0u : (x & ((1u << (8 * valid)) - 1u));
+    }
+}
+
+// one probe round: tuple i (all tuples in round 0, list[] afterwards) walks from its start entry
+// (the tag's home slot in round 0, slot[i] afterwards) to the first entry that is free (claimed
+// here) or holds its tag (verified by k_fold_verify)
+__global__ void k_fold_claim(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ list,
+                             const SegDesc *__restrict__ segs, FoldEnt *__restrict__ ent, uint32_t mask,
+                             uint32_t *__restrict__ slot) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    const uint32_t i = list ? list[g] : (uint32_t)g;
     const kvr_tuple t = tup[i];
-    uint32_t h = ht_mix(t.key_tag) & mask;
+    uint32_t h = list ? slot[i] : (ht_mix(t.key_tag) & mask);
+    const unsigned long long mine = ((unsigned long long)t.key_tag << 32) | i;
     for (uint32_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
-        uint32_t r = __hip_atomic_load(&rep[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (r == HT_EMPTY) {
-            r = atomicCAS(&rep[h], HT_EMPTY, (uint32_t)i);
-            if (r == HT_EMPTY) r = (uint32_t)i;   // claimed: this tuple represents the key
+        unsigned long long v = __hip_atomic_load(&ent[h].tagrep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v == FE_EMPTY) {
+            v = atomicCAS(&ent[h].tagrep, FE_EMPTY, mine);
+            if (v == FE_EMPTY) {   // claimed: this tuple represents its key in entry h
+                uint32_t w[4];
+                key_prefix16(segs[t.seg_idx], t, w);
+                ent[h].klen = t.key_len;
+                *reinterpret_cast<uint4 *>(ent[h].key) = make_uint4(w[0], w[1], w[2], w[3]);
+                slot[i] = h;
+                return;
+            }
         }
-        if (r == (uint32_t)i || key_eq(segs, tup[r], t)) {
-            atomicMax(&best[h], (uint32_t)i + 1u);
+        if ((uint32_t)(v >> 32) == t.key_tag) {
             slot[i] = h;
             return;
         }
     }
-    slot[i] = HT_EMPTY;   // unreachable: the table has at least n empty slots
+    slot[i] = HT_EMPTY;   // unreachable: the table has at least n free entries
+}
+
+// same key as the entry's representative: keep the last index; else on to the next round
+__global__ void k_fold_verify(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ list,
+                              const SegDesc *__restrict__ segs, FoldEnt *__restrict__ ent, uint32_t mask,
+                              uint32_t *__restrict__ slot, uint32_t *__restrict__ next, uint32_t *__restrict__ n_next) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    const uint32_t i = list ? list[g] : (uint32_t)g;
+    const uint32_t h = slot[i];
+    if (h == HT_EMPTY) return;
+    const uint4 a = reinterpret_cast<const uint4 *>(&ent[h])[0];
+    const uint32_t rep = a.x;
+    bool same = rep == i;
+    if (!same) {
+        const kvr_tuple t = tup[i];
+        if (a.w == t.key_len) {
+            const uint4 k = reinterpret_cast<const uint4 *>(&ent[h])[1];
+            uint32_t w[4];
+            key_prefix16(segs[t.seg_idx], t, w);
+            same = ((w[0] ^ k.x) | (w[1] ^ k.y) | (w[2] ^ k.z) | (w[3] ^ k.w)) == 0u;
+            if (same && t.key_len > 16u)
+                same = bytes_eq(key_ptr(segs, tup[rep]) + 16, key_ptr(segs, t) + 16, t.key_len - 16u);
+        }
+    }
+    if (same) {
+        atomicMin(&ent[h].best, ~i);
+    } else {   // another key with this tag holds entry h: probe on from h + 1 next round
+        next[atomicAdd(n_next, 1u)] = i;
+        slot[i] = (h + 1) & mask;
+    }
+}
+
+__device__ __forceinline__ bool is_last(const FoldEnt *ent, const uint32_t *slot, uint64_t i) {
+    const uint32_t s = slot[i];
+    return s != HT_EMPTY && ~ent[s].best == (uint32_t)i;
 }
 
 // live flag and output size of every tuple
-__global__ void k_live(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ best,
+__global__ void k_live(const kvr_tuple *__restrict__ tup, uint64_t n, const FoldEnt *__restrict__ ent,
                        const uint32_t *__restrict__ slot, uint64_t *__restrict__ size, uint32_t *__restrict__ flag) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const kvr_tuple t = tup[i];
-    const uint32_t s = slot[i];
-    const bool live = t.op == 0 && s != HT_EMPTY && best[s] == (uint32_t)i + 1u;
+    const bool live = t.op == 0 && is_last(ent, slot, i);
     size[i] = live ? 9ull + t.key_len + t.val_len : 0ull;   // SET framing, engine.rs:169-173
     flag[i] = live ? 1u : 0u;
 }
@@ -235,12 +317,11 @@ __device__ __forceinline__ uint32_t owner_of(uint32_t key_tag, uint32_t n_ranks)
     return (ht_mix(key_tag) >> 7) % n_ranks;   // other bits than the table slot's
 }
 
-__global__ void k_cand(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ best,
+__global__ void k_cand(const kvr_tuple *__restrict__ tup, uint64_t n, const FoldEnt *__restrict__ ent,
                        const uint32_t *__restrict__ slot, uint32_t n_ranks, uint32_t *__restrict__ cown) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint32_t s = slot[i];
-    cown[i] = (s != HT_EMPTY && best[s] == (uint32_t)i + 1u) ? owner_of(tup[i].key_tag, n_ranks) : NO_OWNER;
+    cown[i] = is_last(ent, slot, i) ? owner_of(tup[i].key_tag, n_ranks) : NO_OWNER;
 }
 
 // per owner o: (1 << 40) | padded key bytes for its candidates (one exclusive scan gives both
@@ -332,14 +413,13 @@ __global__ void k_res_flag(const kvr_cand *__restrict__ hdr, uint64_t m, const u
 
 // this rank's live records after the exchange: a SET that is its key's local last AND the
 // key's global last (its candidate won at the owner)
-__global__ void k_live_global(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ best,
+__global__ void k_live_global(const kvr_tuple *__restrict__ tup, uint64_t n, const FoldEnt *__restrict__ ent,
                               const uint32_t *__restrict__ slot, const uint32_t *__restrict__ send_idx,
                               const uint8_t *__restrict__ win, uint64_t *__restrict__ size, uint32_t *__restrict__ flag) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const kvr_tuple t = tup[i];
-    const uint32_t s = slot[i];
-    const bool cand = s != HT_EMPTY && best[s] == (uint32_t)i + 1u;
+    const bool cand = is_last(ent, slot, i);
     const bool live = t.op == 0 && cand && win[send_idx[i]] != 0;
     size[i] = live ? 9ull + t.key_len + t.val_len : 0ull;
     flag[i] = live ? 1u : 0u;

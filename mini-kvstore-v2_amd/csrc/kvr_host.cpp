@@ -9,9 +9,14 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -75,11 +80,19 @@ struct KeyEq {
 struct kvs_store {
     std::string dir;
     std::vector<uint64_t> ids;
-    std::vector<std::vector<uint8_t>> bytes;
-    struct Ent { uint32_t seg_idx; uint64_t val_off; uint32_t len; };
-    std::unordered_map<KeyRef, Ent, KeyHash, KeyEq> index;
+    std::vector<kvr_segment> segs;               // host bytes of every resident segment
+    uint8_t *pinned = nullptr;                   // the segments' arena (kvr_host_alloc) ...
+    std::vector<uint8_t> heap;                   // ... or pageable memory
+    std::vector<std::vector<uint8_t>> owned;     // segments written by kvs_compact
+    // the index (index.rs:5-7 shape): live keys' final SETs and the table over them
+    // (kvr_replay_index / kvr_index_find)
+    std::vector<kvr_tuple> live;
+    std::vector<uint32_t> slots;
     uint64_t total_bytes = 0;
     uint64_t active_id = 0;
+    uint32_t open_flags = 0;
+    kvs_open_stats ost{};
+    ~kvs_store() { kvr_host_free(pinned); }
 };
 
 extern "C" {
@@ -285,64 +298,104 @@ uint64_t kvh_fold_parallel(const kvr_segment *segs, const kvr_tuple *t, size_t n
     return k;
 }
 
-static int read_file(const std::string &path, std::vector<uint8_t> &out, int *os_err) {
-    const int fd = open(path.c_str(), O_RDONLY);
-    if (fd < 0) { *os_err = errno; return -1; }   // engine.rs:80-82: open failure -> CorruptedData
-    struct stat st;
-    if (fstat(fd, &st) == 0 && S_ISDIR(st.st_mode)) {   // read() fails -> treated as EOF (engine.rs:88)
-        close(fd);
-        out.clear();
-        return 0;
-    }
-    out.clear();
-    uint8_t buf[1 << 16];
-    for (;;) {
-        const ssize_t r = read(fd, buf, sizeof(buf));
-        if (r < 0) { if (errno == EINTR) continue; break; }   // a read error ends the segment like EOF
-        if (r == 0) break;
-        out.insert(out.end(), buf, buf + r);
-    }
-    close(fd);
-    return 0;
+}  // extern "C"
+
+namespace {
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-// replay the store's resident segments on ctx's GPU and fold the index (engine.rs:53-57, :137, :141)
-static int build_index(kvs_store *s, kvr_ctx *ctx, kvr_error *err, char *msg, size_t msg_cap,
-                       const std::vector<std::string> *paths) {
-    const size_t n = s->ids.size();
-    s->index.clear();
-    s->total_bytes = 0;
-    std::vector<kvr_segment> segs(n);
+// the host-fold path (kvs_open with KVS_OPEN_HOST_FOLD, or when the device index cannot hold the
+// store): kvr_replay_stream's batches -> tuples in host memory -> kvh_fold_parallel -> live list
+// -> the same table on the host
+int index_host_fold(kvs_store *s, kvr_ctx *ctx, uint32_t stream_flags, kvr_error *err) {
+    const size_t n = s->segs.size();
     uint64_t total = 0;
-    for (size_t i = 0; i < n; ++i) {
-        segs[i] = kvr_segment{s->ids[i], s->bytes[i].data(), s->bytes[i].size()};
-        total += s->bytes[i].size();
-    }
-    // the replay and the last-writer fold (engine.rs:137, :141) both run on the GPU
-    // (kvr_replay_live): only each live key's final SET comes back
-    std::vector<kvr_tuple> tuples(std::max<size_t>(16, total / 256));
+    for (const kvr_segment &g : s->segs) total += g.len;
+    std::vector<kvr_tuple> t((size_t)(total / 256) + 16);
     size_t nt = 0;
     kvr_error e{};
-    int rc = n ? kvr_replay_live(ctx, segs.data(), n, 0, tuples.data(), tuples.size(), &nt, &e) : KVR_OK;
+    int rc = n ? kvr_replay_stream(ctx, s->segs.data(), n, stream_flags, 0, nullptr, 0, t.data(), t.size(), &nt, &e)
+               : KVR_OK;
     if (rc == KVR_CAPACITY) {
-        tuples.resize(nt);
-        rc = kvr_replay_live(ctx, segs.data(), n, 0, tuples.data(), tuples.size(), &nt, &e);
+        t.resize(nt);
+        rc = kvr_replay_stream(ctx, s->segs.data(), n, stream_flags, 0, nullptr, 0, t.data(), t.size(), &nt, &e);
     }
-    if (rc == KVR_CORRUPTED) {
-        if (err) *err = e;
-        if (msg && paths) kvr_format_error(&e, (*paths)[e.seg_idx].c_str(), msg, msg_cap);
-        return rc;
+    if (rc == KVR_CORRUPTED && err) *err = e;
+    if (rc != KVR_OK) return rc;
+    std::vector<uint8_t> flag(nt);
+    uint64_t tb = 0;
+    const uint64_t nk = kvh_fold_parallel(s->segs.data(), t.data(), nt, 0, flag.data(), &tb);
+    s->live.clear();
+    s->live.reserve(nk);
+    for (size_t i = 0; i < nt; ++i)
+        if (flag[i]) s->live.push_back(t[i]);
+    s->slots.assign(kvr_index_slots(s->live.size()), 0u);
+    return kvr_index_build_host(s->live.data(), s->live.size(), s->slots.data(), s->slots.size());
+}
+
+// the index from a finished device call: live list + table (KVR_CAPACITY: fetch at full size)
+template <class F>
+int index_device(kvs_store *s, kvr_ctx *ctx, F call) {
+    size_t nl = 0;
+    uint64_t ns = 0;
+    s->live.resize(std::max<size_t>(16, s->live.capacity()));
+    s->slots.resize(std::max<size_t>(16, s->slots.capacity()));
+    int rc = call(s->live.data(), s->live.size(), s->slots.data(), s->slots.size(), &nl, &ns);
+    if (rc == KVR_CAPACITY) {
+        s->live.resize(nl);
+        s->slots.resize(ns);
+        rc = kvr_index_fetch(ctx, 0, s->live.data(), nl, s->slots.data(), ns);
     }
     if (rc != KVR_OK) return rc;
-    s->index.reserve(nt + 16);
-    for (size_t i = 0; i < nt; ++i) {   // one live SET per key, already folded
-        const kvr_tuple &t = tuples[i];
-        const KeyRef k{segs[t.seg_idx].bytes + t.rec_off + 5, t.key_len, t.key_tag};
-        s->index[k] = kvs_store::Ent{t.seg_idx, t.rec_off + 9 + t.key_len, t.val_len};
-    }
-    for (const auto &kv : s->index) s->total_bytes += kv.second.len;
+    s->live.resize(nl);
+    s->slots.resize(ns);
     return KVR_OK;
 }
+
+void finish_index(kvs_store *s) {
+    s->total_bytes = 0;   // stats().total_bytes: live value bytes (engine.rs:253-255)
+    for (const kvr_tuple &t : s->live) s->total_bytes += t.val_len;
+    s->ost.n_live = s->live.size();
+}
+
+// (re)build the index over s->segs (host bytes): the device index, the host fold when the device
+// cannot hold the store (KVR_ENOMEM, or KVR_EINVAL at the fold's 2^31-tuple limit)
+int build_index(kvs_store *s, kvr_ctx *ctx, uint32_t open_flags, kvr_error *err) {
+    s->live.clear();
+    s->slots.clear();
+    int rc = KVR_ENOMEM;
+    if (!(open_flags & KVS_OPEN_HOST_FOLD)) {
+        rc = index_device(s, ctx, [&](kvr_tuple *l, size_t lc, uint32_t *sl, uint64_t sc, size_t *nl, uint64_t *ns) {
+            return kvr_replay_index(ctx, s->segs.data(), s->segs.size(), 0, l, lc, sl, sc, nl, ns, err);
+        });
+        s->ost.path = KVS_PATH_DEVICE_INDEX;
+    }
+    if (rc == KVR_ENOMEM || rc == KVR_EINVAL) {
+        rc = index_host_fold(s, ctx, s->pinned ? KVR_HOST_PINNED : 0, err);
+        s->ost.path = KVS_PATH_HOST_FOLD;
+    }
+    if (rc == KVR_OK) finish_index(s);
+    return rc;
+}
+
+// a reader for one segment file: pread into dst until len bytes or EOF (a read error ends the
+// segment like EOF, engine.rs:88); returns the bytes read
+uint64_t read_fd(int fd, uint8_t *dst, uint64_t len) {
+    uint64_t o = 0;
+    while (o < len) {
+        const ssize_t r = pread(fd, dst + o, (size_t)std::min<uint64_t>(len - o, 1ull << 30), (off_t)o);
+        if (r < 0) { if (errno == EINTR) continue; break; }
+        if (r == 0) break;
+        o += (uint64_t)r;
+    }
+    return o;
+}
+
+}  // namespace
+
+extern "C" {
 
 static bool is_segment_name(const char *name) {   // compaction.rs:41-43
     const size_t n = strlen(name);
@@ -363,11 +416,13 @@ static int write_file_sync(const std::string &path, const uint8_t *p, size_t n) 
     return rc;
 }
 
-int kvs_open(const char *dir, kvr_ctx *ctx, kvs_store **out, kvr_error *err, char *msg, size_t msg_cap) {
+int kvs_open_ex(const char *dir, kvr_ctx *ctx, uint32_t flags, kvs_store **out, kvr_error *err, char *msg,
+                size_t msg_cap) {
     if (!dir || !ctx || !out) return KVR_EINVAL;
     *out = nullptr;
     if (err) memset(err, 0, sizeof(*err));
     if (msg && msg_cap) msg[0] = 0;
+    const auto t0 = std::chrono::steady_clock::now();
     struct stat st;
     if (stat(dir, &st) != 0 && mkdir(dir, 0777) != 0 && errno != EEXIST) return KVR_EIO;   // engine.rs:26-28
     size_t n = 0;
@@ -377,58 +432,179 @@ int kvs_open(const char *dir, kvr_ctx *ctx, kvs_store **out, kvr_error *err, cha
     std::vector<char> pbuf(n * 4200 + 16);
     rc = kvh_discover(dir, ids.data(), n, pbuf.data(), pbuf.size(), &n);
     if (rc != KVR_OK) return rc;
-    kvs_store *s = new kvs_store();
-    s->dir = dir;
-    s->ids = ids;
-    s->bytes.resize(n);
     std::vector<std::string> paths(n);
     size_t po = 0;
     for (size_t i = 0; i < n; ++i) { paths[i] = std::string(pbuf.data() + po); po += paths[i].size() + 1; }
+
+    // engine.rs:55-57 opens segment k only after segments 0 .. k-1 replayed: an unopenable file
+    // ends the list, and its error stands only if the segments before it replay cleanly
+    std::vector<int> fds;
+    std::vector<uint64_t> sizes;
+    size_t n_ok = n;
+    int open_errno = 0;
     for (size_t i = 0; i < n; ++i) {
-        int e = 0;
-        if (read_file(paths[i], s->bytes[i], &e) != 0) {
-            if (err) { err->kind = KVR_E_OPEN; err->seg_idx = (uint32_t)i; err->aux = (uint64_t)e; }
-            if (msg && err) kvr_format_error(err, paths[i].c_str(), msg, msg_cap);
-            delete s;
-            return KVR_CORRUPTED;
-        }
+        const int fd = open(paths[i].c_str(), O_RDONLY);
+        if (fd < 0) { n_ok = i; open_errno = errno; break; }   // engine.rs:80-82
+        struct stat fs;
+        const bool dir_like = fstat(fd, &fs) != 0 || S_ISDIR(fs.st_mode);   // read() fails -> EOF (engine.rs:88)
+        fds.push_back(fd);
+        sizes.push_back(dir_like ? 0 : (uint64_t)fs.st_size);
     }
-    std::vector<std::string> *pp = &paths;
-    rc = build_index(s, ctx, err, msg, msg_cap, pp);
-    if (rc != KVR_OK) { delete s; return rc; }
+    auto close_all = [&]() { for (int fd : fds) close(fd); fds.clear(); };
+
+    std::unique_ptr<kvs_store> s(new kvs_store());
+    s->dir = dir;
+    s->open_flags = flags;
+    s->ids.assign(ids.begin(), ids.begin() + (ptrdiff_t)n_ok);
+    s->ost.n_segments = n_ok;
+    // one arena for every segment (256-B aligned starts): pinned, so the transfers are plain DMA
+    std::vector<uint64_t> offs(n_ok);
+    uint64_t arena = 0;
+    for (size_t i = 0; i < n_ok; ++i) { offs[i] = arena; arena += (sizes[i] + 255) & ~255ull; }
+    const auto ta = std::chrono::steady_clock::now();
+    uint8_t *base = nullptr;
+    if (!(flags & KVS_OPEN_NO_PIN) && kvr_host_alloc(arena + 256, reinterpret_cast<void **>(&s->pinned)) == KVR_OK) {
+        base = s->pinned;
+    } else {
+        s->heap.resize(arena + 256);
+        base = s->heap.data();
+    }
+    s->ost.ms_alloc = ms_since(ta);
+    s->segs.resize(n_ok);
+    for (size_t i = 0; i < n_ok; ++i) s->segs[i] = kvr_segment{ids[i], base + offs[i], sizes[i]};
+
+    // readers: 8-MiB pieces of the files, in store order, over up to 16 threads; segment i is
+    // pushed to HBM as soon as all its pieces are in, while the readers go on with later files
+    const bool device = !(flags & KVS_OPEN_HOST_FOLD) && kvr_ingest_begin(ctx, arena, n_ok) == KVR_OK;
+    constexpr uint64_t PIECE = 8ull << 20;
+    std::vector<uint64_t> pstart(n_ok + 1, 0);
+    for (size_t i = 0; i < n_ok; ++i) pstart[i + 1] = pstart[i] + std::max<uint64_t>(1, (sizes[i] + PIECE - 1) / PIECE);
+    const uint64_t n_pieces = pstart[n_ok];
+    std::unique_ptr<std::atomic<uint64_t>[]> left(new std::atomic<uint64_t>[n_ok + 1]);
+    std::unique_ptr<std::atomic<uint64_t>[]> end(new std::atomic<uint64_t>[n_ok + 1]);
+    for (size_t i = 0; i < n_ok; ++i) { left[i] = pstart[i + 1] - pstart[i]; end[i] = sizes[i]; }
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<uint64_t> next_piece{0};
+    const uint32_t n_threads = (uint32_t)std::min<uint64_t>(
+        std::max<uint64_t>(1, n_pieces), std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+    s->ost.read_threads = n_threads;
+    const auto tr = std::chrono::steady_clock::now();
+    std::vector<std::thread> readers;
+    for (uint32_t w = 0; w < n_threads && n_ok; ++w) {
+        readers.emplace_back([&]() {
+            for (;;) {
+                const uint64_t p = next_piece.fetch_add(1);
+                if (p >= n_pieces) return;
+                const size_t i = (size_t)(std::upper_bound(pstart.begin(), pstart.end(), p) - pstart.begin()) - 1;
+                const uint64_t o = (p - pstart[i]) * PIECE;
+                const uint64_t want = o < sizes[i] ? std::min(PIECE, sizes[i] - o) : 0;
+                uint64_t r = 0;
+                while (r < want) {   // a short read (EOF, error) ends the segment there
+                    const ssize_t k = pread(fds[i], base + offs[i] + o + r, (size_t)(want - r), (off_t)(o + r));
+                    if (k < 0 && errno == EINTR) continue;
+                    if (k <= 0) break;
+                    r += (uint64_t)k;
+                }
+                if (r < want) {   // the segment ends at the first short piece's last byte
+                    uint64_t cur = end[i].load();
+                    while (o + r < cur && !end[i].compare_exchange_weak(cur, o + r)) {}
+                }
+                if (--left[i] == 0) {
+                    std::lock_guard<std::mutex> g(mu);
+                    cv.notify_all();
+                }
+            }
+        });
+    }
+    int push_rc = KVR_OK;
+    for (size_t i = 0; i < n_ok; ++i) {
+        {
+            std::unique_lock<std::mutex> g(mu);
+            cv.wait(g, [&] { return left[i].load() == 0; });
+        }
+        // a file shorter than its size at discovery ends at its last byte read; one that grew is
+        // replayed as it was at discovery
+        s->segs[i].len = end[i].load();
+        if (device && push_rc == KVR_OK) push_rc = kvr_ingest_push(ctx, s->segs[i].seg_id, s->segs[i].bytes, s->segs[i].len);
+    }
+    for (auto &t : readers) t.join();
+    s->ost.ms_read = ms_since(tr);
+    close_all();
+    uint64_t bytes = 0;
+    for (const kvr_segment &g : s->segs) bytes += g.len;
+    s->ost.bytes = bytes;
+
+    const auto ti = std::chrono::steady_clock::now();
+    rc = KVR_ENOMEM;
+    if (device && push_rc == KVR_OK) {
+        rc = index_device(s.get(), ctx, [&](kvr_tuple *l, size_t lc, uint32_t *sl, uint64_t sc, size_t *nl, uint64_t *ns) {
+            return kvr_ingest_index(ctx, 0, l, lc, sl, sc, nl, ns, err);
+        });
+        s->ost.path = KVS_PATH_DEVICE_INDEX;
+    }
+    if (rc == KVR_ENOMEM || rc == KVR_EINVAL) {   // HBM too small for the store, or the fold's limits
+        rc = index_host_fold(s.get(), ctx, s->pinned ? KVR_HOST_PINNED : 0, err);
+        s->ost.path = KVS_PATH_HOST_FOLD;
+    }
+    s->ost.ms_index = ms_since(ti);
+    if (rc == KVR_CORRUPTED) {
+        if (msg && err) kvr_format_error(err, paths[err->seg_idx].c_str(), msg, msg_cap);
+        return rc;
+    }
+    if (rc != KVR_OK) return rc;
+    if (n_ok < n) {   // every segment before the unopenable one replayed: the open error stands
+        if (err) { err->kind = KVR_E_OPEN; err->seg_idx = (uint32_t)n_ok; err->rec_off = 0; err->aux = (uint64_t)open_errno; }
+        if (msg && err) kvr_format_error(err, paths[n_ok].c_str(), msg, msg_cap);
+        return KVR_CORRUPTED;
+    }
+    finish_index(s.get());
     // engine.rs:59-68: next id = max + 1, create the (empty) active segment for appends
     s->active_id = (n ? ids[n - 1] : 0) + 1;
     const std::string ap = std::string(dir) + "/segment-" + std::to_string(s->active_id) + ".dat";
     const int fd = open(ap.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
     if (fd >= 0) close(fd);
-    *out = s;
+    s->ost.ms_total = ms_since(t0);
+    *out = s.release();
+    return KVR_OK;
+}
+
+int kvs_open(const char *dir, kvr_ctx *ctx, kvs_store **out, kvr_error *err, char *msg, size_t msg_cap) {
+    return kvs_open_ex(dir, ctx, 0, out, err, msg, msg_cap);
+}
+
+int kvs_last_open_stats(const kvs_store *s, kvs_open_stats *out) {
+    if (!s || !out) return KVR_EINVAL;
+    *out = s->ost;
     return KVR_OK;
 }
 
 int kvs_get(const kvs_store *s, const uint8_t *key, size_t klen, const uint8_t **val, size_t *vlen) {
     if (!s) return KVR_EINVAL;
-    const KeyRef k{key, (uint32_t)klen, crc32_update(0, key, klen)};
-    auto it = s->index.find(k);
-    if (it == s->index.end()) return 0;
-    if (val) *val = s->bytes[it->second.seg_idx].data() + it->second.val_off;
-    if (vlen) *vlen = it->second.len;
+    if (s->live.empty()) return 0;
+    const int64_t j = kvr_index_find(s->live.data(), s->slots.data(), s->slots.size(), s->segs.data(), key, klen);
+    if (j < 0) return 0;
+    const kvr_tuple &t = s->live[(size_t)j];
+    if (val) *val = s->segs[t.seg_idx].bytes + t.rec_off + 9 + t.key_len;
+    if (vlen) *vlen = t.val_len;
     return 1;
 }
 
 int kvs_locate(const kvs_store *s, const uint8_t *key, size_t klen, uint64_t *seg_id, uint64_t *val_off, uint64_t *len) {
     if (!s) return KVR_EINVAL;
-    const KeyRef k{key, (uint32_t)klen, crc32_update(0, key, klen)};
-    auto it = s->index.find(k);
-    if (it == s->index.end()) return 0;
-    if (seg_id) *seg_id = s->ids[it->second.seg_idx];
-    if (val_off) *val_off = it->second.val_off;
-    if (len) *len = it->second.len;
+    if (s->live.empty()) return 0;
+    const int64_t j = kvr_index_find(s->live.data(), s->slots.data(), s->slots.size(), s->segs.data(), key, klen);
+    if (j < 0) return 0;
+    const kvr_tuple &t = s->live[(size_t)j];
+    if (seg_id) *seg_id = s->ids[t.seg_idx];
+    if (val_off) *val_off = t.rec_off + 9 + t.key_len;
+    if (len) *len = t.val_len;
     return 1;
 }
 
 int kvs_stats_get(const kvs_store *s, kvs_stats *out) {
     if (!s || !out) return KVR_EINVAL;
-    out->num_keys = s->index.size();
+    out->num_keys = s->live.size();
     uint64_t nseg = 0;   // engine.rs:239-250: entries named segment-*.dat, parse or not
     if (DIR *d = opendir(s->dir.c_str())) {
         while (struct dirent *e = readdir(d)) {
@@ -446,18 +622,15 @@ int kvs_stats_get(const kvs_store *s, kvs_stats *out) {
     return KVR_OK;
 }
 
-size_t kvs_num_keys(const kvs_store *s) { return s ? s->index.size() : 0; }
+size_t kvs_num_keys(const kvs_store *s) { return s ? s->live.size() : 0; }
 
 int kvs_compact(kvs_store *s, kvr_ctx *ctx, uint64_t seg_target, kvr_error *err) {
     if (!s || !ctx) return KVR_EINVAL;
     if (err) memset(err, 0, sizeof(*err));
-    const size_t n = s->ids.size();
-    std::vector<kvr_segment> segs(n);
+    const size_t n = s->segs.size();
+    const std::vector<kvr_segment> &segs = s->segs;
     uint64_t bytes_in = 0;
-    for (size_t i = 0; i < n; ++i) {
-        segs[i] = kvr_segment{s->ids[i], s->bytes[i].data(), s->bytes[i].size()};
-        bytes_in += s->bytes[i].size();
-    }
+    for (const kvr_segment &g : segs) bytes_in += g.len;
     // 1. the live records, re-framed into new segments, on the GPU
     std::vector<uint8_t> out(std::max<uint64_t>(bytes_in, 1));
     std::vector<uint64_t> ends(seg_target ? bytes_in / seg_target + 2 : 1);
@@ -507,10 +680,16 @@ int kvs_compact(kvs_store *s, kvr_ctx *ctx, uint64_t seg_target, kvr_error *err)
     const int fd = open(ap.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
     if (fd < 0) return KVR_EIO;
     close(fd);
-    // 5. the store now reads the new files; the index is rebuilt over them (same map)
+    // 5. the store now reads the new files; the index is rebuilt over them (same map).
+    // kvr_replay_index leaves kvr_last_compact_stats to this compaction.
     s->ids = new_ids;
-    s->bytes = std::move(new_bytes);
-    return build_index(s, ctx, err, nullptr, 0, nullptr);
+    s->owned = std::move(new_bytes);
+    s->segs.resize(n_new);
+    for (size_t j = 0; j < n_new; ++j) s->segs[j] = kvr_segment{new_ids[j], s->owned[j].data(), s->owned[j].size()};
+    kvr_host_free(s->pinned);
+    s->pinned = nullptr;
+    std::vector<uint8_t>().swap(s->heap);
+    return build_index(s, ctx, s->open_flags, err);
 }
 
 void kvs_close(kvs_store *s) { delete s; }

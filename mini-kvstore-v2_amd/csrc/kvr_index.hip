@@ -1,0 +1,250 @@
+/*
+ * kvr_index.hip — the open-time index on the device, included by kvr_api.hip.
+ *
+ * KVStore::open (engine.rs:24-76) ends with a HashMap<String, Vec<u8>> (index.rs:5-7 has the
+ * shape) holding every live key's final value: replay (engine.rs:55-57), then the fold of
+ * engine.rs:137 (insert) / :141 (remove).  Here both run in HBM and only the result crosses
+ * PCIe, as two flat arrays:
+ *   live[]    each live key's final SET tuple, in (segment, offset) order (kvr_replay_live);
+ *   slots[]   an open-addressing table over live[]: slots[h] = 1 + index into live[] (0: free),
+ *             home slot kvr_index_hash(key_tag) & (n_slots - 1), linear probing; n_slots =
+ *             kvr_index_slots(n_live) (a power of two, >= 2 n_live).
+ * A lookup (kvr_index_find) is one CRC-32 of the key and a probe that compares tags first, so the
+ * host folds nothing.  The ingest calls stage the store's bytes in HBM as the caller reads the
+ * files, so reading, PCIe transfer and (at the end) the replay and fold overlap.
+ */
+
+namespace {
+// live list: tuple i -> out[pos[i]] if flag[i]
+__global__ void k_live_tuples(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ flag,
+                              const uint32_t *__restrict__ pos, kvr_tuple *__restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && flag[i]) out[pos[i]] = tup[i];
+}
+
+// MurmurHash3's 32-bit finaliser: the home slot of a key tag (kvr_index_hash, host and device)
+__host__ __device__ __forceinline__ uint32_t ix_hash(uint32_t h) {
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    return h;
+}
+
+// live keys are distinct: every insert claims a free slot (no key compare)
+__global__ void k_index_insert(const kvr_tuple *__restrict__ live, uint64_t n, uint32_t *__restrict__ slots, uint32_t mask) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    uint32_t h = ix_hash(live[j].key_tag) & mask;
+    for (uint32_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask)
+        if (atomicCAS(&slots[h], 0u, (uint32_t)j + 1u) == 0u) return;
+}
+
+uint64_t index_slots(uint64_t n_live) {
+    uint64_t s = 16;
+    while (s < 2 * n_live) s <<= 1;
+    return s;
+}
+
+// after compact_front: live flags, their scan and the dense live list in c->lout; *total = n_live
+int live_list(kvr_ctx *c, size_t nt, uint64_t *total) {
+    *total = 0;
+    if (nt == 0) return KVR_OK;
+    hipStream_t st = c->stream;
+    const uint32_t g = (uint32_t)((nt + 255) / 256);
+    hipLaunchKernelGGL(k_live, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->fent.p, c->cslot.p,
+                       c->csize.p, c->cflag.p);
+    HIPCHK(hipGetLastError());
+    size_t tb = c->ctmp.n;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->cflag.p, c->cpos.p, (int)nt, st));
+    uint32_t last[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(&last[0], c->cpos.p + nt - 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&last[1], c->cflag.p + nt - 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *total = (uint64_t)last[0] + last[1];
+    if (*total == 0) return KVR_OK;
+    if (c->lout.ensure(*total)) return KVR_ENOMEM;
+    hipLaunchKernelGGL(k_live_tuples, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->cflag.p, c->cpos.p, c->lout.p);
+    HIPCHK(hipGetLastError());
+    return KVR_OK;
+}
+
+int index_copy_out(kvr_ctx *c, uint32_t flags, kvr_tuple *live, size_t live_cap, uint32_t *slots, uint64_t slot_cap) {
+    if (c->ix_live > live_cap || c->ix_slots > slot_cap) return KVR_CAPACITY;
+    const hipMemcpyKind k = (flags & KVR_OUT_ON_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    hipStream_t st = c->stream;
+    if (c->ix_live) HIPCHK(hipMemcpyAsync(live, c->lout.p, c->ix_live * sizeof(kvr_tuple), k, st));
+    if (c->ix_slots) HIPCHK(hipMemcpyAsync(slots, c->islots.p, c->ix_slots * 4, k, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return KVR_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int kvr_replay_live(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, kvr_tuple *out, size_t cap,
+                    size_t *n_out, kvr_error *err) {
+    if (!c || (!segs && n) || !n_out || (cap && !out)) return KVR_EINVAL;
+    if (flags & ~(KVR_SEGS_ON_DEVICE | KVR_OUT_ON_DEVICE)) return KVR_EINVAL;
+    *n_out = 0;
+    c->ix_valid = false;
+    size_t nt = 0;
+    kvr_compact_stats cs{};
+    int rc = compact_front(c, segs, n, flags, err, &nt, false, &cs);   // replay + fold (kvr_compact.hip)
+    if (rc != KVR_OK || nt == 0) return rc;
+    uint64_t total = 0;
+    rc = live_list(c, nt, &total);
+    if (rc != KVR_OK) return rc;
+    *n_out = total;
+    if (total > cap) return KVR_CAPACITY;
+    if (total == 0) return KVR_OK;
+    const hipMemcpyKind k = (flags & KVR_OUT_ON_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    HIPCHK(hipMemcpyAsync(out, c->lout.p, total * sizeof(kvr_tuple), k, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return KVR_OK;
+}
+
+uint64_t kvr_index_slots(uint64_t n_live) { return index_slots(n_live); }
+
+uint32_t kvr_index_hash(uint32_t key_tag) { return ix_hash(key_tag); }
+
+int kvr_replay_index(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, kvr_tuple *live, size_t live_cap,
+                     uint32_t *slots, uint64_t slot_cap, size_t *n_live, uint64_t *n_slots, kvr_error *err) {
+    if (!c || (!segs && n) || !n_live || !n_slots || (live_cap && !live) || (slot_cap && !slots)) return KVR_EINVAL;
+    if (flags & ~(KVR_SEGS_ON_DEVICE | KVR_OUT_ON_DEVICE)) return KVR_EINVAL;
+    *n_live = 0;
+    *n_slots = 0;
+    c->ix_valid = false;
+    c->ix_live = c->ix_slots = 0;
+    memset(&c->istats, 0, sizeof(c->istats));
+    const auto t0 = std::chrono::steady_clock::now();
+    size_t nt = 0;
+    kvr_compact_stats cs{};
+    int rc = compact_front(c, segs, n, flags, err, &nt, false, &cs);
+    c->istats.bytes_in = cs.bytes_in;
+    c->istats.n_tuples = nt;
+    c->istats.ms_replay = cs.ms_replay;
+    if (rc != KVR_OK) return rc;
+    uint64_t total = 0;
+    if (nt) {
+        rc = live_list(c, nt, &total);
+        if (rc != KVR_OK) return rc;
+    }
+    const uint64_t ns = index_slots(total);
+    if (c->islots.ensure(ns)) return KVR_ENOMEM;
+    hipStream_t st = c->stream;
+    HIPCHK(hipMemsetAsync(c->islots.p, 0, ns * 4, st));
+    if (total) {
+        hipLaunchKernelGGL(k_index_insert, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, st, c->lout.p, total,
+                           c->islots.p, (uint32_t)(ns - 1));
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(c->ev[4], st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (nt) c->istats.ms_fold = ev_ms(c->ev[0], c->ev[4]);   // fold rounds .. index table
+    c->ix_live = total;
+    c->ix_slots = ns;
+    c->ix_valid = true;
+    c->istats.n_live = total;
+    c->istats.n_slots = ns;
+    c->istats.fold_rounds = c->fold_rounds;
+    *n_live = total;
+    *n_slots = ns;
+    rc = index_copy_out(c, flags, live, live_cap, slots, slot_cap);
+    c->istats.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+int kvr_index_fetch(kvr_ctx *c, uint32_t flags, kvr_tuple *live, size_t live_cap, uint32_t *slots, uint64_t slot_cap) {
+    if (!c || !c->ix_valid || (live_cap && !live) || (slot_cap && !slots)) return KVR_EINVAL;
+    if (flags & ~KVR_OUT_ON_DEVICE) return KVR_EINVAL;
+    return index_copy_out(c, flags, live, live_cap, slots, slot_cap);
+}
+
+int kvr_last_index_stats(const kvr_ctx *c, kvr_index_stats *out) {
+    if (!c || !out) return KVR_EINVAL;
+    *out = c->istats;
+    return KVR_OK;
+}
+
+int kvr_ingest_begin(kvr_ctx *c, uint64_t total_bytes, size_t n_segs) {
+    if (!c) return KVR_EINVAL;
+    c->ix_valid = false;
+    c->ing_off = 0;
+    c->ing_segs.clear();
+    HIPCHK(hipSetDevice(c->device));
+    if (c->copy) HIPCHK(hipStreamSynchronize(c->copy));   // no copy of an earlier ingest in flight
+    if (c->ing.ensure(total_bytes + 256 * ((uint64_t)n_segs + 1))) return KVR_ENOMEM;
+    c->ing_segs.reserve(n_segs);
+    if (!c->copy) {
+        HIPCHK(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+        for (auto &e : c->ev_copy) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    return KVR_OK;
+}
+
+int kvr_ingest_push(kvr_ctx *c, uint64_t seg_id, const uint8_t *bytes, uint64_t len) {
+    if (!c || (len && !bytes) || !c->copy) return KVR_EINVAL;
+    if (!c->ing_segs.empty() && seg_id < c->ing_segs.back().seg_id) return KVR_EINVAL;   // engine.rs:51 order
+    const uint64_t padded = (len + 255) & ~255ull;
+    if (c->ing_off + padded > c->ing.n) return KVR_CAPACITY;
+    uint8_t *d = c->ing.p + c->ing_off;
+    if (len) HIPCHK(hipMemcpyAsync(d, bytes, len, hipMemcpyHostToDevice, c->copy));
+    c->ing_segs.push_back(kvr_segment{seg_id, d, len});
+    c->ing_off += padded;
+    return KVR_OK;
+}
+
+int kvr_ingest_index(kvr_ctx *c, uint32_t flags, kvr_tuple *live, size_t live_cap, uint32_t *slots, uint64_t slot_cap,
+                     size_t *n_live, uint64_t *n_slots, kvr_error *err) {
+    if (!c || !c->copy) return KVR_EINVAL;
+    if (flags & ~KVR_OUT_ON_DEVICE) return KVR_EINVAL;
+    HIPCHK(hipSetDevice(c->device));
+    // the replay waits for the last transfer on the device, not on the host
+    HIPCHK(hipEventRecord(c->ev_copy[0], c->copy));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_copy[0], 0));
+    return kvr_replay_index(c, c->ing_segs.data(), c->ing_segs.size(), KVR_SEGS_ON_DEVICE | flags, live, live_cap,
+                            slots, slot_cap, n_live, n_slots, err);
+}
+
+int64_t kvr_index_find(const kvr_tuple *live, const uint32_t *slots, uint64_t n_slots, const kvr_segment *segs,
+                       const uint8_t *key, size_t klen) {
+    if (!live || !slots || !segs || n_slots == 0 || (n_slots & (n_slots - 1)) || (klen && !key)) return -1;
+    const uint32_t tag = kvr_crc32(0, key, klen);
+    const uint64_t mask = n_slots - 1;
+    for (uint64_t h = ix_hash(tag) & mask, probe = 0; probe < n_slots; ++probe, h = (h + 1) & mask) {
+        const uint32_t v = slots[h];
+        if (v == 0) return -1;
+        const kvr_tuple &t = live[v - 1];
+        if (t.key_tag == tag && t.key_len == klen &&
+            (klen == 0 || memcmp(segs[t.seg_idx].bytes + t.rec_off + 5, key, klen) == 0))
+            return (int64_t)(v - 1);
+    }
+    return -1;
+}
+
+int kvr_index_build_host(const kvr_tuple *live, size_t n_live, uint32_t *slots, uint64_t n_slots) {
+    if ((n_live && !live) || !slots || n_slots <= n_live || (n_slots & (n_slots - 1)) || n_live >= 0xFFFFFFFFull)
+        return KVR_EINVAL;
+    memset(slots, 0, n_slots * 4);
+    const uint64_t mask = n_slots - 1;
+    for (size_t j = 0; j < n_live; ++j) {
+        uint64_t h = ix_hash(live[j].key_tag) & mask;
+        while (slots[h]) h = (h + 1) & mask;
+        slots[h] = (uint32_t)j + 1u;
+    }
+    return KVR_OK;
+}
+
+int kvr_host_alloc(uint64_t bytes, void **out) {
+    if (!out) return KVR_EINVAL;
+    *out = nullptr;
+    if (hipHostMalloc(out, bytes ? bytes : 1) != hipSuccess) {
+        *out = nullptr;
+        return KVR_ENOMEM;
+    }
+    return KVR_OK;
+}
+
+void kvr_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
+}  // extern "C"

@@ -86,6 +86,22 @@ class CompactStats(C.Structure):
                 ("bytes_out", C.c_uint64)]
 
 
+class IndexStats(C.Structure):
+    _fields_ = [("ms_wall", C.c_double), ("ms_replay", C.c_double), ("ms_fold", C.c_double),
+                ("bytes_in", C.c_uint64), ("n_tuples", C.c_uint64), ("n_live", C.c_uint64),
+                ("n_slots", C.c_uint64), ("fold_rounds", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class OpenStats(C.Structure):
+    _fields_ = [("ms_total", C.c_double), ("ms_alloc", C.c_double), ("ms_read", C.c_double),
+                ("ms_index", C.c_double), ("bytes", C.c_uint64), ("n_segments", C.c_uint64),
+                ("n_live", C.c_uint64), ("path", C.c_uint32), ("read_threads", C.c_uint32)]
+
+
+OPEN_HOST_FOLD, OPEN_NO_PIN = 0x1, 0x2
+PATH_DEVICE_INDEX, PATH_HOST_FOLD = 1, 2
+
+
 # ---- library loading ---------------------------------------------------------------------------
 _rep = None
 _host = None
@@ -123,6 +139,23 @@ def _load():
                                       C.POINTER(Error)]
     rep.kvr_replay_live.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
     rep.kvr_last_stream_stats.argtypes = [P, C.POINTER(StreamStats)]
+    rep.kvr_replay_index.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, P, U64, C.POINTER(SZ), C.POINTER(U64),
+                                     C.POINTER(Error)]
+    rep.kvr_index_fetch.argtypes = [P, U32, P, SZ, P, U64]
+    rep.kvr_last_index_stats.argtypes = [P, C.POINTER(IndexStats)]
+    rep.kvr_index_slots.argtypes = [U64]
+    rep.kvr_index_slots.restype = U64
+    rep.kvr_index_hash.argtypes = [U32]
+    rep.kvr_index_hash.restype = U32
+    rep.kvr_index_find.argtypes = [P, P, U64, C.POINTER(Segment), P, SZ]
+    rep.kvr_index_find.restype = C.c_int64
+    rep.kvr_index_build_host.argtypes = [P, SZ, P, U64]
+    rep.kvr_ingest_begin.argtypes = [P, U64, SZ]
+    rep.kvr_ingest_push.argtypes = [P, U64, P, U64]
+    rep.kvr_ingest_index.argtypes = [P, U32, P, SZ, P, U64, C.POINTER(SZ), C.POINTER(U64), C.POINTER(Error)]
+    rep.kvr_host_alloc.argtypes = [U64, C.POINTER(P)]
+    rep.kvr_host_free.argtypes = [P]
+    rep.kvr_host_free.restype = None
     rep.kvr_etag_batch.argtypes = [P, P, U64, P, P, SZ, U32, P, P, C.POINTER(U64)]
     rep.kvr_last_etag_stats.argtypes = [P, C.POINTER(EtagStats)]
     rep.kvr_etag_format.argtypes = [U32, C.c_char_p]
@@ -149,6 +182,8 @@ def _load():
     host.kvh_fold_parallel.argtypes = [C.POINTER(Segment), P, SZ, U32, P, C.POINTER(U64)]
     host.kvh_fold_parallel.restype = U64
     host.kvs_open.argtypes = [C.c_char_p, P, C.POINTER(P), C.POINTER(Error), C.c_char_p, SZ]
+    host.kvs_open_ex.argtypes = [C.c_char_p, P, U32, C.POINTER(P), C.POINTER(Error), C.c_char_p, SZ]
+    host.kvs_last_open_stats.argtypes = [P, C.POINTER(OpenStats)]
     host.kvs_get.argtypes = [P, P, SZ, C.POINTER(P), C.POINTER(SZ)]
     host.kvs_locate.argtypes = [P, P, SZ, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]
     host.kvs_stats_get.argtypes = [P, C.POINTER(StoreStats)]
@@ -511,6 +546,81 @@ class Context:
         tuples = out_arr[: n_out.value] if out_arr is not None and rc == OK else None
         return ReplayResult(rc, tuples, n_out.value, err if rc == CORRUPTED else None, self.last_stats())
 
+    def replay_index(self, segments, seg_ids=None, on_device=False):
+        """Replay + fold + key table on the device (kvr_replay_index) -> Index (live tuples in
+        (segment, offset) order and the slot table; lookups through Index.find)."""
+        segs, keep, total = self._segments(segments, seg_ids, on_device)
+        flags = SEGS_ON_DEVICE if on_device else 0
+        nl, ns = C.c_size_t(), C.c_uint64()
+        err = Error()
+        rc = self._rep.kvr_replay_index(self.h, segs, len(segments), flags, None, 0, None, 0, C.byref(nl),
+                                        C.byref(ns), C.byref(err))
+        if rc == CORRUPTED:
+            return ReplayResult(rc, None, 0, err, self.last_stats())
+        live = np.zeros(max(nl.value, 1), dtype=TUPLE_DTYPE)
+        slots = np.zeros(max(ns.value, 1), dtype=np.uint32)
+        if rc == CAPACITY:
+            rc = self._rep.kvr_index_fetch(self.h, 0, live.ctypes.data, nl.value, slots.ctypes.data, ns.value)
+        if rc != OK:
+            raise NativeError(f"kvr_replay_index: {self._rep.kvr_strerror(rc).decode()} ({rc})")
+        st = IndexStats()
+        self._rep.kvr_last_index_stats(self.h, C.byref(st))
+        return Index(live[: nl.value], slots[: ns.value], None if on_device else keep, st)
+
+    def ingest_index(self, segments, seg_ids=None, pinned=False, host_ptrs=False):
+        """The open path's device calls: kvr_ingest_begin, one kvr_ingest_push per segment (host
+        bytes; pinned=True stages them in kvr_host_alloc memory first; host_ptrs=True: segments
+        are (pointer, length) pairs into host memory the caller keeps), kvr_ingest_index."""
+        n = len(segments)
+        if host_ptrs:
+            class _P:   # (pointer, length) with the ndarray attributes used below
+                def __init__(self, p, ln):
+                    self.size, self.ctypes = ln, type("c", (), {"data": p})()
+            arrs = [_P(p, ln) for p, ln in segments]
+        else:
+            arrs = [np.frombuffer(s, dtype=np.uint8) if isinstance(s, (bytes, bytearray)) else np.ascontiguousarray(s)
+                    for s in segments]
+        total = sum((a.size + 255) & ~255 for a in arrs)
+        host_mem = None
+        if pinned and not host_ptrs:
+            hp = C.c_void_p()
+            if self._rep.kvr_host_alloc(total + 256, C.byref(hp)) != OK:
+                raise NativeError("kvr_host_alloc failed")
+            host_mem = hp.value
+            staged, o = [], 0
+            for a in arrs:
+                v = np.ctypeslib.as_array((C.c_uint8 * max(a.size, 1)).from_address(host_mem + o))[: a.size]
+                v[:] = a
+                staged.append(v)
+                o += (a.size + 255) & ~255
+            arrs = staged
+        try:
+            rc = self._rep.kvr_ingest_begin(self.h, total, n)
+            if rc != OK:
+                raise NativeError(f"kvr_ingest_begin: {rc}")
+            for i, a in enumerate(arrs):
+                sid = seg_ids[i] if seg_ids is not None else i
+                rc = self._rep.kvr_ingest_push(self.h, sid, a.ctypes.data if a.size else None, a.size)
+                if rc != OK:
+                    raise NativeError(f"kvr_ingest_push: {rc}")
+            nl, ns = C.c_size_t(), C.c_uint64()
+            err = Error()
+            rc = self._rep.kvr_ingest_index(self.h, 0, None, 0, None, 0, C.byref(nl), C.byref(ns), C.byref(err))
+            if rc == CORRUPTED:
+                return ReplayResult(rc, None, 0, err, self.last_stats())
+            live = np.zeros(max(nl.value, 1), dtype=TUPLE_DTYPE)
+            slots = np.zeros(max(ns.value, 1), dtype=np.uint32)
+            if rc == CAPACITY:
+                rc = self._rep.kvr_index_fetch(self.h, 0, live.ctypes.data, nl.value, slots.ctypes.data, ns.value)
+            if rc != OK:
+                raise NativeError(f"kvr_ingest_index: {rc}")
+            st = IndexStats()
+            self._rep.kvr_last_index_stats(self.h, C.byref(st))
+            return Index(live[: nl.value], slots[: ns.value], None if host_ptrs else [np.array(a) for a in arrs], st)
+        finally:
+            if host_mem:
+                self._rep.kvr_host_free(host_mem)
+
     def etag_batch(self, data, offs, lens, expected=None, on_device=False, data_len=None):
         """Batch ETag (kvr_etag_batch): CRC-32 of data[offs[i]:offs[i]+lens[i]] for every i.
         data is bytes / a uint8 array, or a device pointer with on_device=True (then data_len).
@@ -646,6 +756,47 @@ def gen_segment_size(spec: GenSpec, seg_no: int):
     return ln.value, nr.value
 
 
+class Index:
+    """The open-time index (kvr_replay_index): live tuples + the key table over them."""
+
+    def __init__(self, live, slots, segments, stats):
+        self.live, self.slots, self.stats = live, slots, stats
+        self.status = OK
+        self._segs = segments
+
+    def find(self, key, segments=None):
+        """Index into live[] of key's final SET, or -1 (kvr_index_find)."""
+        rep, _ = _load()
+        segs = segments if segments is not None else self._segs
+        arrs = [np.frombuffer(s, dtype=np.uint8) if isinstance(s, (bytes, bytearray)) else np.ascontiguousarray(s)
+                for s in segs]
+        cs = (Segment * max(len(arrs), 1))(*[Segment(i, a.ctypes.data if a.size else None, a.size)
+                                             for i, a in enumerate(arrs)])
+        kb = key.encode() if isinstance(key, str) else bytes(key)
+        k = np.frombuffer(kb, dtype=np.uint8)
+        if len(self.live) == 0:
+            return -1
+        return int(rep.kvr_index_find(self.live.ctypes.data, self.slots.ctypes.data, len(self.slots), cs,
+                                      k.ctypes.data if k.size else None, k.size))
+
+
+def index_build_host(live):
+    """kvr_index_build_host: the device table's layout built on the host from a live list."""
+    rep, _ = _load()
+    live = np.ascontiguousarray(live, dtype=TUPLE_DTYPE)
+    ns = int(rep.kvr_index_slots(len(live)))
+    slots = np.zeros(ns, dtype=np.uint32)
+    rc = rep.kvr_index_build_host(live.ctypes.data if len(live) else None, len(live), slots.ctypes.data, ns)
+    if rc != OK:
+        raise NativeError(f"kvr_index_build_host: {rc}")
+    return slots
+
+
+def index_hash(tag):
+    rep, _ = _load()
+    return int(rep.kvr_index_hash(tag))
+
+
 # ---- KVStore mirror ----------------------------------------------------------------------------
 class KVStore:
     """The reference's KVStore::open / get / stats path with replay on the GPU."""
@@ -656,13 +807,14 @@ class KVStore:
         _, self._host = _load()
 
     @classmethod
-    def open(cls, dirpath: str, ctx: Context | None = None):
+    def open(cls, dirpath: str, ctx: Context | None = None, flags: int = 0):
+        """flags: OPEN_HOST_FOLD (the batch path with the host fold), OPEN_NO_PIN (kvs_open_ex)."""
         _, host = _load()
         ctx = ctx or Context(0)
         h = C.c_void_p()
         err = Error()
         msg = C.create_string_buffer(8192)
-        rc = host.kvs_open(str(dirpath).encode(), ctx.h, C.byref(h), C.byref(err), msg, len(msg))
+        rc = host.kvs_open_ex(str(dirpath).encode(), ctx.h, flags, C.byref(h), C.byref(err), msg, len(msg))
         if rc == CORRUPTED:
             raise CorruptedData(err.kind, err.seg_idx, err.rec_off, err.aux, msg.value.decode())
         if rc != OK:
@@ -690,6 +842,11 @@ class KVStore:
     def stats(self):
         s = StoreStats()
         self._host.kvs_stats_get(self._h, C.byref(s))
+        return s
+
+    def open_stats(self):
+        s = OpenStats()
+        self._host.kvs_last_open_stats(self._h, C.byref(s))
         return s
 
     def compact(self, seg_target: int = 0):

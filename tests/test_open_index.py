@@ -1,0 +1,279 @@
+"""The open-time index (kvr_replay_index / kvr_ingest_*, kvs_open_ex) and the fold's tag rounds.
+
+Parity: the live list is exactly the oracle's (oracle_fold_live: engine.rs:137 insert / :141
+remove over oracle_replay's tuples, in (segment, offset) order), every live key is found at its
+live index through the table, and every other key is absent (engine.rs:200 get -> None).
+
+The fold compares key bytes only when the CRC-32 tags match; keys that share a CRC-32 are found
+here by brute force (zlib.crc32 over a fixed key set, deterministic), so the collision rounds of
+k_fold_verify run on real collisions: same-length short keys, and long keys whose first 16 bytes
+(the part the fold entry holds) are equal too.
+"""
+import os
+import shutil
+import zlib
+
+import numpy as np
+import pytest
+
+import kvreplay as K
+import oracle_py as O
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def rec_set(k, v):
+    return b"\x00" + len(k).to_bytes(4, "little") + k + len(v).to_bytes(4, "little") + v
+
+
+def rec_del(k):
+    return b"\x01" + len(k).to_bytes(4, "little") + k
+
+
+def crc_collisions(prefix, n, want):
+    """Pairs of distinct keys prefix + 16 hex digits of a scrambled i (i < n) with equal CRC-32, up
+    to want pairs.  (Keys differing only in a few trailing bytes never collide: CRC-32 catches
+    every burst of up to 32 bits, so the varying part is spread over 16 bytes.)"""
+    seen, pairs = {}, []
+    for i in range(n):
+        k = prefix + b"%016x" % ((i * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF)
+        c = zlib.crc32(k)
+        if c in seen:
+            pairs.append((seen[c], k))
+            if len(pairs) >= want:
+                break
+        else:
+            seen[c] = k
+    return pairs
+
+
+def collision_store():
+    """Segments whose keys include CRC-32-colliding pairs, with SETs, overwrites and DELs."""
+    short = crc_collisions(b"", 400_000, 6)
+    long_ = crc_collisions(b"shared-prefix-16-tail-", 400_000, 6)
+    pairs = short + long_
+    assert len(short) >= 3 and len(long_) >= 3
+    assert all(len(a) == len(b) and a != b and zlib.crc32(a) == zlib.crc32(b) for a, b in pairs)
+    assert all(a[:16] == b[:16] for a, b in long_)
+    segs = []
+    for s in range(4):
+        b = bytearray()
+        for j, (a, c) in enumerate(pairs):
+            # per pair and segment: a different mix of writes to the two keys
+            m = (s * 7 + j) % 5
+            if m == 0:
+                b += rec_set(a, b"A%d-%d" % (s, j)) + rec_set(c, b"C%d-%d" % (s, j))
+            elif m == 1:
+                b += rec_set(c, b"c%d" % s) + rec_del(a)
+            elif m == 2:
+                b += rec_del(c) + rec_set(a, b"a%d" % s) + rec_set(a, b"aa%d" % s)
+            elif m == 3:
+                b += rec_set(a, b"") + rec_set(c, b"x" * (j + s))
+            else:
+                b += rec_del(a) + rec_del(c)
+            b += rec_set(b"plain-%d-%d" % (s, j), b"v")
+        segs.append(bytes(b))
+    return segs, pairs
+
+
+def expect(segs, seg_ids=None):
+    rc, t, err = O.replay(segs, seg_ids=seg_ids)
+    assert rc == 0
+    live, nk, tb = O.fold_live(segs, t)
+    return t[live], nk, tb
+
+
+def keys_of(segs, tuples):
+    return [bytes(segs[t["seg_idx"]][t["rec_off"] + 5: t["rec_off"] + 5 + t["key_len"]]) for t in tuples]
+
+
+def check_index(idx, segs, want, absent=()):
+    assert np.array_equal(idx.live, want)
+    ns = len(idx.slots)
+    assert ns == max(16, 1 << max(0, (2 * len(want) - 1).bit_length())) or (len(want) == 0 and ns == 16)
+    used = idx.slots[idx.slots != 0]
+    assert len(used) == len(want) and len(np.unique(used)) == len(want)
+    for j, k in enumerate(keys_of(segs, want)):
+        assert idx.find(k, segs) == j
+    for k in absent:
+        assert idx.find(k, segs) == -1
+
+
+# ---- host side (no GPU): the table layout and the lookup ----------------------------------------
+def test_index_build_host_and_find():
+    segs, pairs = collision_store()
+    want, nk, _ = expect(segs)
+    slots = K.index_build_host(want)
+    idx = K.Index(want, slots, segs, None)
+    live_keys = set(keys_of(segs, want))
+    absent = [k for p in pairs for k in p if k not in live_keys] + [b"never-written", b""]
+    check_index(idx, segs, want, absent)
+    # every entry sits on its probe path: home slot, then linear probing without a free slot between
+    mask = len(slots) - 1
+    for h in np.nonzero(slots)[0]:
+        home = K.index_hash(int(want[slots[h] - 1]["key_tag"])) & mask
+        p = home
+        while p != h:
+            assert slots[p] != 0
+            p = (p + 1) & mask
+    assert len(K.index_build_host(want[:0])) == 16
+
+
+# ---- device index --------------------------------------------------------------------------------
+@pytest.mark.gpu
+def test_fold_tag_collisions(gctx):
+    """Distinct keys with equal CRC-32 (short, and long with equal 16-B prefixes) fold exactly."""
+    segs, pairs = collision_store()
+    want, nk, tb = expect(segs)
+    r = gctx.replay_live(segs)
+    assert r.status == 0 and np.array_equal(r.tuples, want)
+    idx = gctx.replay_index(segs)
+    live_keys = set(keys_of(segs, want))
+    check_index(idx, segs, want, [k for p in pairs for k in p if k not in live_keys])
+    assert idx.stats.fold_rounds >= 2 and idx.stats.n_live == nk
+    # the rewrite uses the same fold: its output replays to the same map
+    c = gctx.compact(segs)
+    rc, t2, _ = O.replay(c.segments())
+    assert rc == 0 and len(t2) == nk
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["persistence", "store_integration", "compaction_example", "large_dataset"])
+def test_replay_index_golden(gctx, name):
+    d = os.path.join(GOLD, name)
+    names = sorted((n for n in os.listdir(d) if n.startswith("segment-")), key=lambda n: int(n[8:-4]))
+    segs = [open(os.path.join(d, n), "rb").read() for n in names]
+    ids = [int(n[8:-4]) for n in names]
+    want, nk, _ = expect(segs, ids)
+    idx = gctx.replay_index(segs, seg_ids=ids)
+    check_index(idx, segs, want, [b"no-such-key"])
+    for pinned in (False, True):
+        ig = gctx.ingest_index(segs, seg_ids=ids, pinned=pinned)
+        check_index(ig, segs, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", [
+    K.GenSpec(seed=95, seg_bytes=600_000, key_space_log2=12, val_min=0, val_max=200, del_permille=300),
+    K.GenSpec(seed=96, seg_bytes=3_000_000, key_dist=1, key_space_log2=20, val_min=8, val_max=4096,
+              del_permille=50),
+])
+def test_replay_index_generated(gctx, spec):
+    segs = [K.gen_segment_cpu(spec, s)[0] for s in range(6)]
+    want, nk, tb = expect(segs)
+    idx = gctx.replay_index(segs)
+    assert np.array_equal(idx.live, want) and idx.stats.n_live == nk
+    used = idx.slots[idx.slots != 0]
+    assert len(np.unique(used)) == nk
+    ks = keys_of(segs, want)
+    for j in range(0, nk, max(1, nk // 300)):
+        assert idx.find(ks[j], segs) == j
+    ig = gctx.ingest_index(segs, pinned=True)
+    assert np.array_equal(ig.live, want)
+    assert all(ig.find(ks[j], segs) == j for j in range(0, nk, max(1, nk // 100)))
+
+
+@pytest.mark.gpu
+def test_replay_index_errors(gctx):
+    spec = K.GenSpec(seed=97, seg_bytes=200_000, key_space_log2=8, val_min=0, val_max=64, del_permille=300)
+    segs = [K.gen_segment_cpu(spec, s)[0] for s in range(3)]
+    bad = segs[:1] + [segs[1][:-2]] + segs[2:]
+    rc, _, err = O.replay(bad)
+    r = gctx.replay_index(bad)
+    assert r.status == rc == 1 and (r.error.kind, r.error.seg_idx, r.error.rec_off) == (err.kind, err.seg_idx, err.rec_off)
+    r = gctx.ingest_index(bad)
+    assert r.status == 1 and (r.error.kind, r.error.seg_idx, r.error.rec_off) == (err.kind, err.seg_idx, err.rec_off)
+    e = gctx.replay_index([])
+    assert len(e.live) == 0 and len(e.slots) == 16 and e.find(b"x", []) == -1
+
+
+@pytest.mark.gpu
+def test_live_index_device_buffers(gctx):
+    """kvr_replay_live with segments in HBM (KVR_SEGS_ON_DEVICE) and tuples left in HBM
+    (KVR_OUT_ON_DEVICE), and its KVR_CAPACITY answer for a device buffer."""
+    torch = pytest.importorskip("torch")
+    spec = K.GenSpec(seed=98, seg_bytes=500_000, key_space_log2=11, val_min=0, val_max=300, del_permille=250)
+    segs = [K.gen_segment_cpu(spec, s)[0] for s in range(4)]
+    want, nk, _ = expect(segs)
+    buf = torch.zeros(sum(len(s) + 64 for s in segs), dtype=torch.uint8, device="cuda")
+    ptrs, off = [], 5
+    for s in segs:
+        buf[off: off + len(s)] = torch.from_numpy(s).cuda()
+        ptrs.append((buf.data_ptr() + off, len(s)))
+        off += len(s) + 9
+    torch.cuda.synchronize()
+    out = torch.zeros((nk + 8) * 32, dtype=torch.uint8, device="cuda")
+    r = gctx.replay_live(ptrs, on_device=True, out_ptr=out.data_ptr(), cap=nk + 8)
+    assert r.status == 0 and r.n == nk
+    got = out[: nk * 32].cpu().numpy().view(K.TUPLE_DTYPE)
+    assert np.array_equal(got, want)
+    r = gctx.replay_live(ptrs, on_device=True, out_ptr=out.data_ptr(), cap=nk - 1)
+    assert r.status == K.CAPACITY and r.n == nk
+    r = gctx.replay_live(ptrs, on_device=True)   # segments in HBM, tuples to the host
+    assert r.status == 0 and np.array_equal(r.tuples, want)
+
+
+# ---- kvs_open_ex: the files -> index path ---------------------------------------------------------
+def _write_store(d, segs, ids):
+    d.mkdir()
+    for i, s in zip(ids, segs):
+        (d / f"segment-{i}.dat").write_bytes(bytes(s))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [0, K.OPEN_NO_PIN, K.OPEN_HOST_FOLD, K.OPEN_HOST_FOLD | K.OPEN_NO_PIN])
+def test_kvs_open_paths_agree(gctx, tmp_path, flags):
+    spec = K.GenSpec(seed=99, seg_bytes=900_000, key_space_log2=12, val_min=0, val_max=500, del_permille=200)
+    segs = [K.gen_segment_cpu(spec, s)[0] for s in range(7)]
+    ids = [3, 4, 10, 11, 12, 40, 41]
+    d = tmp_path / "db"
+    _write_store(d, segs, ids)
+    want, nk, tb = expect(segs, ids)
+    s = K.KVStore.open(str(d), gctx, flags=flags)
+    st = s.stats()
+    assert (st.num_keys, st.total_bytes, st.active_segment_id) == (nk, tb, 42)
+    os_ = s.open_stats()
+    assert os_.path == (K.PATH_HOST_FOLD if flags & K.OPEN_HOST_FOLD else K.PATH_DEVICE_INDEX)
+    assert os_.bytes == sum(len(x) for x in segs) and os_.n_segments == 7 and os_.n_live == nk
+    for t, k in list(zip(want, keys_of(segs, want)))[:: max(1, nk // 200)]:
+        vo = t["rec_off"] + 9 + t["key_len"]
+        assert s.get(k) == bytes(segs[t["seg_idx"]][vo: vo + t["val_len"]])
+        assert s.locate(k) == (ids[t["seg_idx"]], vo, t["val_len"])
+    assert s.get(b"absent-key") is None
+    s.compact(seg_target=1 << 20)   # the rebuild after compaction uses the store's path too
+    assert s.stats().num_keys == nk and s.stats().total_bytes == tb
+    k0 = keys_of(segs, want[:1])[0]
+    v0 = want[0]
+    assert s.get(k0) == bytes(segs[v0["seg_idx"]][v0["rec_off"] + 9 + v0["key_len"]:][: v0["val_len"]])
+    s.close()
+
+
+@pytest.mark.gpu
+def test_kvs_open_unopenable_segment_order(gctx, tmp_path):
+    """engine.rs:55-57 opens segment k after 0 .. k-1 replayed: an earlier corruption wins over a
+    later unopenable file; with clean segments before it, the open error is reported."""
+    d = tmp_path / "db"
+    d.mkdir()
+    (d / "segment-1.dat").write_bytes(rec_set(b"a", b"1"))
+    os.symlink(str(d / "missing-target"), str(d / "segment-2.dat"))
+    (d / "segment-3.dat").write_bytes(rec_set(b"b", b"2"))
+    with pytest.raises(K.CorruptedData) as ei:
+        K.KVStore.open(str(d), gctx)
+    assert (ei.value.kind, ei.value.seg_idx) == (K.E_OPEN, 1)
+    assert str(ei.value) == (f"Corrupted data: Failed to open segment {d}/segment-2.dat: "
+                             f"No such file or directory (os error 2)")
+    (d / "segment-1.dat").write_bytes(rec_set(b"a", b"1") + b"\x00\x05")
+    with pytest.raises(K.CorruptedData) as ei:
+        K.KVStore.open(str(d), gctx)
+    assert (ei.value.kind, ei.value.seg_idx) == (K.E_KEY_LEN, 0)
+
+
+@pytest.mark.gpu
+def test_kvs_open_golden_host_fold(gctx, tmp_path):
+    d = tmp_path / "persisted_store"
+    shutil.copytree(os.path.join(GOLD, "persistence"), d)
+    s = K.KVStore.open(str(d), gctx, flags=K.OPEN_HOST_FOLD)
+    assert s.get("session") == b"first" and s.get("counter") == b"43" and s.get("name") is None
+    assert s.locate("counter") == (2, 16, 2)
+    assert (s.stats().num_keys, s.stats().total_bytes) == (2, 7)
+    s.close()
