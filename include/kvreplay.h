@@ -197,9 +197,13 @@ int  kvr_ingest_begin(kvr_ctx *ctx, uint64_t total_bytes, size_t n_segs);
 int  kvr_ingest_push(kvr_ctx *ctx, uint64_t seg_id, const uint8_t *bytes, uint64_t len);
 int  kvr_ingest_index(kvr_ctx *ctx, uint32_t flags, kvr_tuple *live, size_t live_cap, uint32_t *slots,
                       uint64_t slot_cap, size_t *n_live, uint64_t *n_slots, kvr_error *err);
-/* Pinned (page-locked) host memory for segment bytes: hipHostMalloc / hipHostFree. */
+/* Pinned (page-locked) host memory for segment bytes: hipHostMalloc / hipHostFree.  Or register
+ * existing host memory for DMA (hipHostRegister / hipHostUnregister; cheap once its pages exist)
+ * and pass it as pinned. */
 int  kvr_host_alloc(uint64_t bytes, void **out);
 void kvr_host_free(void *p);
+int  kvr_host_register(void *p, uint64_t bytes);
+void kvr_host_unregister(void *p);
 
 /* ---- streamed ingest: host segments larger than one transfer ----------
  * The same loop as kvr_replay (engine.rs:55-57) over host-resident segment bytes, e.g. files

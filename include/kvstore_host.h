@@ -65,29 +65,38 @@ typedef struct kvs_stats {          /* StoreStats, src/store/stats.rs:3-10 */
  * (engine.rs:59-68).  On KVR_CORRUPTED, *err and msg (the exact engine.rs message, without
  * error.rs's "Corrupted data: " prefix) describe the first error. */
 int kvs_open(const char *dir, kvr_ctx *ctx, kvs_store **out, kvr_error *err, char *msg, size_t msg_cap);
-/* kvs_open with options.  The default path: up to 16 reader threads pread the files (8-MiB
- * pieces, store order) into one pinned arena (kvr_host_alloc); each segment is pushed to HBM
- * (kvr_ingest_push) as soon as its bytes are in, so reading and PCIe overlap; then
- * kvr_ingest_index replays, folds and builds the key table on the GPU and only the live tuples
- * and the table come back.  When the store does not fit in HBM (KVR_ENOMEM) or exceeds the
- * fold's 2^31-tuple limit (KVR_EINVAL), the host-fold path takes over: kvr_replay_stream in
- * batches, kvh_fold_parallel, kvr_index_build_host.  Both give the same index.
+/* kvs_open with options.  The default path maps every segment file read-only (mmap, populated
+ * from the page cache by up to 16 threads: the store's host bytes are the page cache, no copy),
+ * registers each mapping for DMA (kvr_host_register) and pushes the segment to HBM
+ * (kvr_ingest_push) in store order.  KVS_OPEN_PREAD (or a failed mmap) reads the files instead:
+ * 16 threads pread 8-MiB pieces into one arena on 2-MiB pages, and groups of consecutive segments
+ * (>= 256 MiB) are registered and pushed as soon as their bytes are in, so reading and PCIe
+ * overlap.  Then kvr_ingest_index replays, folds and builds the key table on the GPU and only the
+ * live tuples and the table come back.  When the store does not fit in HBM (KVR_ENOMEM) or
+ * exceeds the fold's 2^31-tuple limit (KVR_EINVAL), the host-fold path takes over:
+ * kvr_replay_stream in batches, kvh_fold_parallel, kvr_index_build_host.  Both give the same index.
  * An unopenable segment k is reported (KVR_E_OPEN) only when segments 0 .. k-1 replay cleanly,
  * as engine.rs:55-57 opens the files one after the other. */
 #define KVS_OPEN_HOST_FOLD  0x1u   /* force the host-fold path                         */
-#define KVS_OPEN_NO_PIN     0x2u   /* read into pageable memory (no kvr_host_alloc)     */
+#define KVS_OPEN_NO_PIN     0x2u   /* no kvr_host_register: HIP stages the transfers    */
+#define KVS_OPEN_PREAD      0x4u   /* read the files into an arena instead of mapping   */
 #define KVS_PATH_DEVICE_INDEX 1u
 #define KVS_PATH_HOST_FOLD    2u
+#define KVS_LOAD_MMAP  1u
+#define KVS_LOAD_PREAD 2u
 typedef struct kvs_open_stats {
     double   ms_total;       /* the whole kvs_open_ex call                                        */
-    double   ms_alloc;       /* the segments' host arena (pinning)                                 */
-    double   ms_read;        /* reader threads, first piece to last (transfers overlap it)          */
-    double   ms_index;       /* last byte read -> index ready: transfer tail, replay, fold, copies  */
-    uint64_t bytes;          /* segment bytes read                                                 */
+    double   ms_register;    /* kvr_host_register calls (inside ms_read)                           */
+    double   ms_push;        /* kvr_ingest_push calls (inside ms_read)                             */
+    double   ms_read;        /* loading: mapping or reading, registration, pushes                  */
+    double   ms_index;       /* after loading -> index ready: transfer tail, replay, fold, copies  */
+    uint64_t bytes;          /* segment bytes                                                      */
     uint64_t n_segments;
     uint64_t n_live;         /* stats().num_keys                                                   */
     uint32_t path;           /* KVS_PATH_DEVICE_INDEX or KVS_PATH_HOST_FOLD (last index build)      */
     uint32_t read_threads;
+    uint32_t mode;           /* KVS_LOAD_MMAP or KVS_LOAD_PREAD                                     */
+    uint32_t pad;
 } kvs_open_stats;
 int kvs_open_ex(const char *dir, kvr_ctx *ctx, uint32_t flags, kvs_store **out, kvr_error *err, char *msg,
                 size_t msg_cap);

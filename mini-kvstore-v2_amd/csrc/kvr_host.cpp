@@ -5,6 +5,7 @@
  */
 #include <dirent.h>
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -17,6 +18,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <numeric>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -81,8 +83,10 @@ struct kvs_store {
     std::string dir;
     std::vector<uint64_t> ids;
     std::vector<kvr_segment> segs;               // host bytes of every resident segment
-    uint8_t *pinned = nullptr;                   // the segments' arena (kvr_host_alloc) ...
-    std::vector<uint8_t> heap;                   // ... or pageable memory
+    std::vector<std::pair<void *, uint64_t>> maps;   // kvs_open's mappings: one per segment file
+                                                 // (mmap path) or the read arena (pread path)
+    std::vector<void *> regs;                    // ranges registered for DMA (kvr_host_register)
+    bool pinned = false;                         // every segment byte lies in a registered range
     std::vector<std::vector<uint8_t>> owned;     // segments written by kvs_compact
     // the index (index.rs:5-7 shape): live keys' final SETs and the table over them
     // (kvr_replay_index / kvr_index_find)
@@ -92,7 +96,14 @@ struct kvs_store {
     uint64_t active_id = 0;
     uint32_t open_flags = 0;
     kvs_open_stats ost{};
-    ~kvs_store() { kvr_host_free(pinned); }
+    void drop_arena() {
+        for (void *r : regs) kvr_host_unregister(r);
+        regs.clear();
+        for (auto &m : maps) munmap(m.first, m.second);
+        maps.clear();
+        pinned = false;
+    }
+    ~kvs_store() { drop_arena(); }
 };
 
 extern "C" {
@@ -380,17 +391,140 @@ int build_index(kvs_store *s, kvr_ctx *ctx, uint32_t open_flags, kvr_error *err)
     return rc;
 }
 
-// a reader for one segment file: pread into dst until len bytes or EOF (a read error ends the
-// segment like EOF, engine.rs:88); returns the bytes read
-uint64_t read_fd(int fd, uint8_t *dst, uint64_t len) {
-    uint64_t o = 0;
-    while (o < len) {
-        const ssize_t r = pread(fd, dst + o, (size_t)std::min<uint64_t>(len - o, 1ull << 30), (off_t)o);
-        if (r < 0) { if (errno == EINTR) continue; break; }
-        if (r == 0) break;
-        o += (uint64_t)r;
+constexpr uint64_t PAGE = 4096;
+constexpr uint64_t HUGE_PAGE = 2ull << 20;
+constexpr uint64_t PIECE = 8ull << 20;   // pread granule
+uint64_t page_up(uint64_t n) { return (n + PAGE - 1) & ~(PAGE - 1); }
+
+// segment readiness shared by the loader threads and the push loop: a segment is ready when all
+// its pieces are in (pread) or it is mapped (mmap); len[i] = its bytes (a file shorter than at
+// discovery ends at its last byte; one that grew is taken as it was)
+struct Loader {
+    size_t n;
+    std::unique_ptr<std::atomic<uint64_t>[]> left, len;
+    std::unique_ptr<std::atomic<uint32_t>[]> group_end;   // pread: a registration group's end
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<std::thread> th;
+    explicit Loader(size_t n_) : n(n_), left(new std::atomic<uint64_t>[n_ + 1]), len(new std::atomic<uint64_t>[n_ + 1]),
+                                 group_end(new std::atomic<uint32_t>[n_ + 1]) {
+        for (size_t i = 0; i <= n; ++i) { left[i] = 1; len[i] = 0; group_end[i] = (uint32_t)(i + 1); }
     }
-    return o;
+    void done_one(size_t i) {
+        if (--left[i] == 0) {
+            std::lock_guard<std::mutex> g(mu);
+            cv.notify_all();
+        }
+    }
+    // the group starting at g0 once all its segments are ready: returns its end
+    size_t wait_group(size_t g0) {
+        const size_t g1 = group_end[g0];
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] {
+            for (size_t i = g0; i < g1; ++i) if (left[i].load()) return false;
+            return true;
+        });
+        return g1;
+    }
+    void join() { for (auto &t : th) t.join(); th.clear(); }
+};
+
+// mmap path: every file mapped read-only and populated from the page cache (no copy; about 1 ms
+// for 4 GiB when cached), one file per task over the threads in store order.  Each mapping is
+// its own registration (a transfer must lie inside one).  false: a mapping failed (the pread
+// path takes over; nothing is left mapped).
+bool load_mmap(kvs_store *s, const std::vector<int> &fds, const std::vector<uint64_t> &sizes, uint32_t n_threads,
+               Loader &L) {
+    const size_t n = L.n;
+    std::vector<void *> mp(n, nullptr);
+    std::atomic<size_t> next{0};
+    std::atomic<bool> failed{false};
+    for (uint32_t w = 0; w < n_threads && n; ++w) {
+        L.th.emplace_back([&]() {
+            for (;;) {
+                const size_t i = next.fetch_add(1);
+                if (i >= n) return;
+                if (sizes[i] && !failed) {
+                    void *p = mmap(nullptr, sizes[i], PROT_READ, MAP_PRIVATE | MAP_POPULATE, fds[i], 0);
+                    if (p == MAP_FAILED) failed = true;
+                    else mp[i] = p;
+                }
+                L.len[i] = sizes[i];
+                L.done_one(i);
+            }
+        });
+    }
+    L.join();   // mapping is ~1 ms per GiB when cached: no overlap needed with the pushes
+    if (failed) {
+        for (size_t i = 0; i < n; ++i) if (mp[i]) munmap(mp[i], sizes[i]);
+        for (size_t i = 0; i < n; ++i) { L.left[i] = 1; L.len[i] = 0; }
+        return false;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        if (mp[i]) s->maps.emplace_back(mp[i], sizes[i]);
+        s->segs[i].bytes = static_cast<const uint8_t *>(mp[i]);
+    }
+    return true;
+}
+
+// pread path: one anonymous arena on 2-MiB pages (page-aligned segment starts), 8-MiB pieces in
+// store order over the threads (they fault the arena in parallel); consecutive segments form
+// registration groups of >= 256 MiB, each ready when all its pieces are in
+void load_pread(kvs_store *s, const std::vector<int> &fds, const std::vector<uint64_t> &sizes, uint32_t n_threads,
+                Loader &L) {
+    const size_t n = L.n;
+    std::vector<uint64_t> offs(n);
+    uint64_t arena = 0;
+    for (size_t i = 0; i < n; ++i) { offs[i] = arena; arena += page_up(sizes[i]); }
+    const uint64_t map_len = ((arena + HUGE_PAGE - 1) & ~(HUGE_PAGE - 1)) + HUGE_PAGE;
+    void *m = mmap(nullptr, map_len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (m == MAP_FAILED) {   // nothing to read into: every segment empty, the replay sees no bytes
+        for (size_t i = 0; i < n; ++i) { L.len[i] = 0; L.left[i] = 0; }
+        return;
+    }
+    s->maps.emplace_back(m, map_len);
+    uint8_t *base = reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(m) + HUGE_PAGE - 1) & ~(HUGE_PAGE - 1));
+    madvise(base, (arena + HUGE_PAGE - 1) & ~(HUGE_PAGE - 1), MADV_HUGEPAGE);   // 2-MiB faults, fast registration
+    for (size_t i = 0; i < n; ++i) s->segs[i].bytes = base + offs[i];
+    const uint64_t GROUP = std::max<uint64_t>(256ull << 20, arena / 16);
+    for (size_t g0 = 0; g0 < n;) {
+        size_t g1 = g0;
+        uint64_t gb = 0;
+        while (g1 < n && (g1 == g0 || gb < GROUP)) gb += page_up(sizes[g1++]);
+        L.group_end[g0] = (uint32_t)g1;
+        g0 = g1;
+    }
+    auto pstart = std::make_shared<std::vector<uint64_t>>(n + 1, 0);
+    for (size_t i = 0; i < n; ++i) {
+        (*pstart)[i + 1] = (*pstart)[i] + std::max<uint64_t>(1, (sizes[i] + PIECE - 1) / PIECE);
+        L.left[i] = (*pstart)[i + 1] - (*pstart)[i];
+        L.len[i] = sizes[i];
+    }
+    auto next = std::make_shared<std::atomic<uint64_t>>(0);
+    const uint64_t n_pieces = (*pstart)[n];
+    for (uint32_t w = 0; w < n_threads && n; ++w) {
+        L.th.emplace_back([&L, &fds, &sizes, base, offs, pstart, next, n_pieces]() {
+            for (;;) {
+                const uint64_t p = next->fetch_add(1);
+                if (p >= n_pieces) return;
+                const size_t i = (size_t)(std::upper_bound(pstart->begin(), pstart->end(), p) - pstart->begin()) - 1;
+                const uint64_t o = (p - (*pstart)[i]) * PIECE;
+                const uint64_t want = o < sizes[i] ? std::min(PIECE, sizes[i] - o) : 0;
+                uint64_t r = 0;
+                while (r < want) {   // a short read (EOF, error) ends the segment there (engine.rs:88)
+                    const ssize_t k = pread(fds[i], base + offs[i] + o + r, (size_t)(want - r), (off_t)(o + r));
+                    if (k < 0 && errno == EINTR) continue;
+                    if (k <= 0) break;
+                    r += (uint64_t)k;
+                }
+                if (r < want) {
+                    uint64_t cur = L.len[i].load();
+                    while (o + r < cur && !L.len[i].compare_exchange_weak(cur, o + r)) {}
+                }
+                L.done_one(i);
+            }
+        });
+    }
 }
 
 }  // namespace
@@ -457,79 +591,47 @@ int kvs_open_ex(const char *dir, kvr_ctx *ctx, uint32_t flags, kvs_store **out, 
     s->open_flags = flags;
     s->ids.assign(ids.begin(), ids.begin() + (ptrdiff_t)n_ok);
     s->ost.n_segments = n_ok;
-    // one arena for every segment (256-B aligned starts): pinned, so the transfers are plain DMA
-    std::vector<uint64_t> offs(n_ok);
-    uint64_t arena = 0;
-    for (size_t i = 0; i < n_ok; ++i) { offs[i] = arena; arena += (sizes[i] + 255) & ~255ull; }
-    const auto ta = std::chrono::steady_clock::now();
-    uint8_t *base = nullptr;
-    if (!(flags & KVS_OPEN_NO_PIN) && kvr_host_alloc(arena + 256, reinterpret_cast<void **>(&s->pinned)) == KVR_OK) {
-        base = s->pinned;
-    } else {
-        s->heap.resize(arena + 256);
-        base = s->heap.data();
-    }
-    s->ost.ms_alloc = ms_since(ta);
     s->segs.resize(n_ok);
-    for (size_t i = 0; i < n_ok; ++i) s->segs[i] = kvr_segment{ids[i], base + offs[i], sizes[i]};
-
-    // readers: 8-MiB pieces of the files, in store order, over up to 16 threads; segment i is
-    // pushed to HBM as soon as all its pieces are in, while the readers go on with later files
-    const bool device = !(flags & KVS_OPEN_HOST_FOLD) && kvr_ingest_begin(ctx, arena, n_ok) == KVR_OK;
-    constexpr uint64_t PIECE = 8ull << 20;
-    std::vector<uint64_t> pstart(n_ok + 1, 0);
-    for (size_t i = 0; i < n_ok; ++i) pstart[i + 1] = pstart[i] + std::max<uint64_t>(1, (sizes[i] + PIECE - 1) / PIECE);
-    const uint64_t n_pieces = pstart[n_ok];
-    std::unique_ptr<std::atomic<uint64_t>[]> left(new std::atomic<uint64_t>[n_ok + 1]);
-    std::unique_ptr<std::atomic<uint64_t>[]> end(new std::atomic<uint64_t>[n_ok + 1]);
-    for (size_t i = 0; i < n_ok; ++i) { left[i] = pstart[i + 1] - pstart[i]; end[i] = sizes[i]; }
-    std::mutex mu;
-    std::condition_variable cv;
-    std::atomic<uint64_t> next_piece{0};
-    const uint32_t n_threads = (uint32_t)std::min<uint64_t>(
-        std::max<uint64_t>(1, n_pieces), std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+    for (size_t i = 0; i < n_ok; ++i) s->segs[i] = kvr_segment{ids[i], nullptr, sizes[i]};
+    const bool device = !(flags & KVS_OPEN_HOST_FOLD) && kvr_ingest_begin(ctx, page_up(std::accumulate(
+                            sizes.begin(), sizes.end(), (uint64_t)0, [](uint64_t a, uint64_t b) { return a + page_up(b); })), n_ok) == KVR_OK;
+    const bool reg = !(flags & KVS_OPEN_NO_PIN);
+    const uint32_t n_threads = (uint32_t)std::min<uint64_t>(16, std::max(1u, std::thread::hardware_concurrency()));
     s->ost.read_threads = n_threads;
+    Loader L(n_ok);
     const auto tr = std::chrono::steady_clock::now();
-    std::vector<std::thread> readers;
-    for (uint32_t w = 0; w < n_threads && n_ok; ++w) {
-        readers.emplace_back([&]() {
-            for (;;) {
-                const uint64_t p = next_piece.fetch_add(1);
-                if (p >= n_pieces) return;
-                const size_t i = (size_t)(std::upper_bound(pstart.begin(), pstart.end(), p) - pstart.begin()) - 1;
-                const uint64_t o = (p - pstart[i]) * PIECE;
-                const uint64_t want = o < sizes[i] ? std::min(PIECE, sizes[i] - o) : 0;
-                uint64_t r = 0;
-                while (r < want) {   // a short read (EOF, error) ends the segment there
-                    const ssize_t k = pread(fds[i], base + offs[i] + o + r, (size_t)(want - r), (off_t)(o + r));
-                    if (k < 0 && errno == EINTR) continue;
-                    if (k <= 0) break;
-                    r += (uint64_t)k;
-                }
-                if (r < want) {   // the segment ends at the first short piece's last byte
-                    uint64_t cur = end[i].load();
-                    while (o + r < cur && !end[i].compare_exchange_weak(cur, o + r)) {}
-                }
-                if (--left[i] == 0) {
-                    std::lock_guard<std::mutex> g(mu);
-                    cv.notify_all();
-                }
-            }
-        });
-    }
+    // the segments' host bytes: the files mapped (page cache, no copy) or read into an arena;
+    // the loader threads make segment i ready in store order as far as they can, and the push
+    // loop below registers and transfers each one as soon as it is
+    bool mapped = !(flags & KVS_OPEN_PREAD) && load_mmap(s.get(), fds, sizes, n_threads, L);
+    if (!mapped) load_pread(s.get(), fds, sizes, n_threads, L);
+    s->ost.mode = mapped ? KVS_LOAD_MMAP : KVS_LOAD_PREAD;
+    bool all_reg = reg;
+    double ms_reg = 0, ms_push = 0;
     int push_rc = KVR_OK;
-    for (size_t i = 0; i < n_ok; ++i) {
-        {
-            std::unique_lock<std::mutex> g(mu);
-            cv.wait(g, [&] { return left[i].load() == 0; });
+    for (size_t g0 = 0; g0 < n_ok;) {
+        const size_t g1 = L.wait_group(g0);   // [g0, g1): ready, one registration
+        for (size_t i = g0; i < g1; ++i) s->segs[i].len = L.len[i];
+        const uint8_t *p0 = s->segs[g0].bytes;
+        const uint64_t gb = page_up((uint64_t)(s->segs[g1 - 1].bytes + s->segs[g1 - 1].len - p0));
+        if (reg && gb && p0) {
+            const auto tg = std::chrono::steady_clock::now();
+            void *p = const_cast<uint8_t *>(p0);
+            if (kvr_host_register(p, gb) == KVR_OK) s->regs.push_back(p);
+            else all_reg = false;   // stays pageable: HIP stages the transfers
+            ms_reg += ms_since(tg);
         }
-        // a file shorter than its size at discovery ends at its last byte read; one that grew is
-        // replayed as it was at discovery
-        s->segs[i].len = end[i].load();
-        if (device && push_rc == KVR_OK) push_rc = kvr_ingest_push(ctx, s->segs[i].seg_id, s->segs[i].bytes, s->segs[i].len);
+        const auto tp = std::chrono::steady_clock::now();
+        for (size_t i = g0; i < g1; ++i)
+            if (device && push_rc == KVR_OK) push_rc = kvr_ingest_push(ctx, s->segs[i].seg_id, s->segs[i].bytes, s->segs[i].len);
+        ms_push += ms_since(tp);
+        g0 = g1;
     }
-    for (auto &t : readers) t.join();
+    L.join();
     s->ost.ms_read = ms_since(tr);
+    s->ost.ms_register = ms_reg;
+    s->ost.ms_push = ms_push;
+    s->pinned = all_reg;
     close_all();
     uint64_t bytes = 0;
     for (const kvr_segment &g : s->segs) bytes += g.len;
@@ -686,9 +788,7 @@ int kvs_compact(kvs_store *s, kvr_ctx *ctx, uint64_t seg_target, kvr_error *err)
     s->owned = std::move(new_bytes);
     s->segs.resize(n_new);
     for (size_t j = 0; j < n_new; ++j) s->segs[j] = kvr_segment{new_ids[j], s->owned[j].data(), s->owned[j].size()};
-    kvr_host_free(s->pinned);
-    s->pinned = nullptr;
-    std::vector<uint8_t>().swap(s->heap);
+    s->drop_arena();
     return build_index(s, ctx, s->open_flags, err);
 }
 

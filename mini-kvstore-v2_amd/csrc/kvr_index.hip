@@ -247,4 +247,13 @@ void kvr_host_free(void *p) {
     if (p) (void)hipHostFree(p);
 }
 
+int kvr_host_register(void *p, uint64_t bytes) {
+    if (!p || !bytes) return KVR_EINVAL;
+    return hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess ? KVR_OK : KVR_EHIP;
+}
+
+void kvr_host_unregister(void *p) {
+    if (p) (void)hipHostUnregister(p);
+}
+
 }  // extern "C"

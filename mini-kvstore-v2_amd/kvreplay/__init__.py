@@ -93,12 +93,15 @@ class IndexStats(C.Structure):
 
 
 class OpenStats(C.Structure):
-    _fields_ = [("ms_total", C.c_double), ("ms_alloc", C.c_double), ("ms_read", C.c_double),
+    _fields_ = [("ms_total", C.c_double), ("ms_register", C.c_double), ("ms_push", C.c_double),
+                ("ms_read", C.c_double),
                 ("ms_index", C.c_double), ("bytes", C.c_uint64), ("n_segments", C.c_uint64),
-                ("n_live", C.c_uint64), ("path", C.c_uint32), ("read_threads", C.c_uint32)]
+                ("n_live", C.c_uint64), ("path", C.c_uint32), ("read_threads", C.c_uint32),
+                ("mode", C.c_uint32), ("pad", C.c_uint32)]
 
 
-OPEN_HOST_FOLD, OPEN_NO_PIN = 0x1, 0x2
+OPEN_HOST_FOLD, OPEN_NO_PIN, OPEN_PREAD = 0x1, 0x2, 0x4
+LOAD_MMAP, LOAD_PREAD = 1, 2
 PATH_DEVICE_INDEX, PATH_HOST_FOLD = 1, 2
 
 
@@ -156,6 +159,9 @@ def _load():
     rep.kvr_host_alloc.argtypes = [U64, C.POINTER(P)]
     rep.kvr_host_free.argtypes = [P]
     rep.kvr_host_free.restype = None
+    rep.kvr_host_register.argtypes = [P, U64]
+    rep.kvr_host_unregister.argtypes = [P]
+    rep.kvr_host_unregister.restype = None
     rep.kvr_etag_batch.argtypes = [P, P, U64, P, P, SZ, U32, P, P, C.POINTER(U64)]
     rep.kvr_last_etag_stats.argtypes = [P, C.POINTER(EtagStats)]
     rep.kvr_etag_format.argtypes = [U32, C.c_char_p]

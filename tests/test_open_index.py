@@ -221,10 +221,12 @@ def _write_store(d, segs, ids):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("flags", [0, K.OPEN_NO_PIN, K.OPEN_HOST_FOLD, K.OPEN_HOST_FOLD | K.OPEN_NO_PIN])
+@pytest.mark.parametrize("flags", [0, K.OPEN_NO_PIN, K.OPEN_PREAD, K.OPEN_PREAD | K.OPEN_NO_PIN, K.OPEN_HOST_FOLD,
+                                   K.OPEN_HOST_FOLD | K.OPEN_PREAD])
 def test_kvs_open_paths_agree(gctx, tmp_path, flags):
     spec = K.GenSpec(seed=99, seg_bytes=900_000, key_space_log2=12, val_min=0, val_max=500, del_permille=200)
     segs = [K.gen_segment_cpu(spec, s)[0] for s in range(7)]
+    segs[2] = segs[2][:0]   # an empty segment file (a fresh active segment) among them
     ids = [3, 4, 10, 11, 12, 40, 41]
     d = tmp_path / "db"
     _write_store(d, segs, ids)
@@ -235,6 +237,7 @@ def test_kvs_open_paths_agree(gctx, tmp_path, flags):
     os_ = s.open_stats()
     assert os_.path == (K.PATH_HOST_FOLD if flags & K.OPEN_HOST_FOLD else K.PATH_DEVICE_INDEX)
     assert os_.bytes == sum(len(x) for x in segs) and os_.n_segments == 7 and os_.n_live == nk
+    assert os_.mode == (K.LOAD_PREAD if flags & K.OPEN_PREAD else K.LOAD_MMAP)
     for t, k in list(zip(want, keys_of(segs, want)))[:: max(1, nk // 200)]:
         vo = t["rec_off"] + 9 + t["key_len"]
         assert s.get(k) == bytes(segs[t["seg_idx"]][vo: vo + t["val_len"]])
