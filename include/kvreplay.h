@@ -151,10 +151,12 @@ int  kvr_replay_live(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint3
  * folds nothing itself:
  *   live[0 .. *n_live)     each live key's final SET tuple, in (segment, offset) order — exactly
  *                          kvr_replay_live's output; *n_live = stats().num_keys
- *   slots[0 .. *n_slots)   slots[h] = 1 + index into live[] (0 = free); *n_slots =
- *                          kvr_index_slots(*n_live); a key's home slot is
- *                          kvr_index_hash(CRC-32 of the key) & (*n_slots - 1), then linear probing.
- *                          Which free slot an insert took may differ between runs; lookups do not.
+ *   slots[0 .. *n_slots)   the fold's own hash table, entry for entry: slots[h] = 1 + index into
+ *                          live[], 0 = free, 0xFFFFFFFF = a key whose last record is a DEL (probe
+ *                          on).  *n_slots is a power of two > *n_live (the fold table's size); a
+ *                          key's home slot is kvr_index_hash(CRC-32 of the key) & (*n_slots - 1),
+ *                          then linear probing.  Which slot a key took may differ between runs;
+ *                          lookups do not.
  * flags: KVR_SEGS_ON_DEVICE, KVR_OUT_ON_DEVICE (live and slots are device pointers).
  * Returns as kvr_replay_live; KVR_CAPACITY when live_cap < *n_live or slot_cap < *n_slots — the
  * result then stays in the context until its next call, and kvr_index_fetch copies it out. */
@@ -167,7 +169,9 @@ typedef struct kvr_index_stats {
     uint64_t n_live;
     uint64_t n_slots;
     uint32_t fold_rounds;   /* probe rounds of the fold (1 + rounds for keys sharing a CRC-32)     */
-    uint32_t pad;
+    uint32_t fold_redo;     /* 1 if the fold table filled up and was redone at 2 n_tuples entries   */
+    uint64_t fold_est;      /* distinct-key estimate that sized the table (HyperLogLog; 0: small)   */
+    uint64_t fold_slots;    /* fold table entries                                                  */
 } kvr_index_stats;
 
 int      kvr_replay_index(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint32_t flags,
@@ -176,8 +180,8 @@ int      kvr_replay_index(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, 
 int      kvr_index_fetch(kvr_ctx *ctx, uint32_t flags, kvr_tuple *live, size_t live_cap, uint32_t *slots,
                          uint64_t slot_cap);
 int      kvr_last_index_stats(const kvr_ctx *ctx, kvr_index_stats *out);
-uint64_t kvr_index_slots(uint64_t n_live);     /* max(16, the power of two >= 2 n_live)            */
-uint32_t kvr_index_hash(uint32_t key_tag);     /* MurmurHash3 fmix32                               */
+uint64_t kvr_index_slots(uint64_t n_live);     /* max(16, the power of two >= 2 n_live): host tables */
+uint32_t kvr_index_hash(uint32_t key_tag);     /* the "lowbias32" integer mix of the tag            */
 /* Host lookup of key (klen bytes) in an index whose keys live in segs[] (host bytes): the index
  * into live[] of its final SET, or -1 when the key is not live (engine.rs:200 get -> None). */
 int64_t  kvr_index_find(const kvr_tuple *live, const uint32_t *slots, uint64_t n_slots, const kvr_segment *segs,

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -94,6 +95,9 @@ struct kvr_ctx {
     DevBuf<uint8_t> cout, ctmp;
     kvr_compact_stats cstats{};
     uint32_t fold_rounds = 0;              // probe rounds of the last fold (1 = no tag collision)
+    uint32_t fold_redo = 0;                // folds redone at full size (the estimate was low)
+    uint64_t fold_est = 0, fold_slots = 0;  // distinct-key estimate, table entries used
+    DevBuf<uint8_t> hpart, hreg;           // HyperLogLog registers per workgroup, merged
     size_t c_nt = 0;                       // tuples of the last compaction front half
     uint32_t c_ranks = 0;                  // sharded compaction state (kvr_compact_stage .. finish)
     bool c_staged = false;
@@ -279,7 +283,7 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->bsum.release();
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
     c->ctup.release(); c->lout.release(); c->fent.release(); c->flist.release(); c->fcnt.release();
-    c->cslot.release(); c->cflag.release(); c->islots.release(); c->ing.release();
+    c->cslot.release(); c->cflag.release(); c->islots.release(); c->ing.release(); c->hpart.release(); c->hreg.release();
     c->cpos.release(); c->cfirst.release(); c->csize.release(); c->coff.release(); c->l_src.release();
     c->l_off.release(); c->ctot.release(); c->ccuts.release(); c->cout.release(); c->ctmp.release();
     c->c_gidx.release(); c->c_own.release(); c->c_sidx.release(); c->c_val.release(); c->c_scan.release();
@@ -572,6 +576,23 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
 // ---------------------------------------------------------------------------------------
 // live-record rewrite (kvr_compact.hip): replay -> fold -> live list -> gather -> cuts
 // ---------------------------------------------------------------------------------------
+// HyperLogLog estimate from the merged registers (alpha_m m^2 / sum 2^-M, the linear-counting
+// correction for small counts, the 2^32 range correction for 32-bit hashes)
+static double hll_estimate(const uint8_t *reg) {
+    double sum = 0;
+    uint32_t zeros = 0;
+    for (int j = 0; j < HLL_M; ++j) {
+        sum += std::ldexp(1.0, -(int)reg[j]);
+        zeros += reg[j] == 0;
+    }
+    const double m = HLL_M, alpha = 0.7213 / (1.0 + 1.079 / m);
+    double e = alpha * m * m / sum;
+    if (e <= 2.5 * m && zeros) e = m * std::log(m / zeros);
+    const double two32 = 4294967296.0;
+    if (e > two32 / 30.0) e = e < two32 ? -two32 * std::log(1.0 - e / two32) : two32;
+    return e;
+}
+
 // replay + the local last-writer fold (k_fold_claim / k_fold_verify): the front half of every
 // compaction and of kvr_replay_live / kvr_replay_index.  It reuses the buffers of a staged
 // sharded compaction, so it ends one (kvr_compact_export / _finish then return KVR_EINVAL until
@@ -584,6 +605,8 @@ static int compact_front(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t
     c->c_staged = false;
     c->c_nt = 0;
     c->fold_rounds = 0;
+    c->fold_redo = 0;
+    c->fold_est = 0;
     memset(cs, 0, sizeof(*cs));
     if (err) memset(err, 0, sizeof(*err));
     uint64_t bytes_in = 0;
@@ -607,11 +630,31 @@ static int compact_front(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t
     if (nt >= 0x7FFFFFFFull) return KVR_EINVAL;   // 32-bit tuple indices in the fold table
     c->c_nt = nt;
     hipStream_t st = c->stream;
-    // 2. the key's last tuple (open addressing over the key bytes, kvr_compact.hip)
-    uint64_t slots = 1;
-    while (slots < 2 * (uint64_t)nt) slots <<= 1;
-    if (c->fent.ensure(slots) || c->cslot.ensure(nt) || c->cflag.ensure(nt) || c->cpos.ensure(nt) ||
-        c->csize.ensure(nt) || c->flist.ensure(2 * nt) || c->fcnt.ensure(1))
+    // 2. the key's last tuple (open addressing over the key bytes, kvr_compact.hip).  The table
+    // is sized for the distinct keys (HyperLogLog estimate, load <= 0.63) rather than the tuples,
+    // so it stays in the caches; a table that fills up is redone at 2 n entries.
+    HIPCHK(hipEventRecord(c->ev[0], st));
+    uint64_t full_slots = 1;
+    while (full_slots < 2 * (uint64_t)nt) full_slots <<= 1;
+    uint64_t slots = full_slots;
+    if (nt >= 65536 || getenv("KVR_FOLD_TINY_TABLE")) {
+        const uint32_t hb = (uint32_t)std::min<uint64_t>((nt + HLL_T - 1) / HLL_T, (uint64_t)c->n_cu);
+        if (c->hpart.ensure((uint64_t)hb * HLL_M) || c->hreg.ensure(HLL_M)) return KVR_ENOMEM;
+        hipLaunchKernelGGL(k_hll, dim3(hb), dim3(HLL_T), 0, st, c->ctup.p, (uint64_t)nt, c->hpart.p);
+        hipLaunchKernelGGL(k_hll_merge, dim3(HLL_M / 16 / 16), dim3(HLL_MERGE_T), 0, st, c->hpart.p, hb, c->hreg.p);
+        HIPCHK(hipGetLastError());
+        std::vector<uint8_t> reg(HLL_M);
+        HIPCHK(hipMemcpyAsync(reg.data(), c->hreg.p, HLL_M, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        const double est = hll_estimate(reg.data());
+        c->fold_est = (uint64_t)est;
+        uint64_t want = 16;
+        while ((double)want < 1.6 * est + 1024.0) want <<= 1;
+        slots = std::min(want, full_slots);
+        if (getenv("KVR_FOLD_TINY_TABLE")) slots = 16;   // test knob: force the full-size redo
+    }
+    if (c->fent.ensure(full_slots) || c->cslot.ensure(nt) || c->cflag.ensure(nt) || c->cpos.ensure(nt) ||
+        c->csize.ensure(nt) || c->flist.ensure(2 * nt) || c->fcnt.ensure(2))
         return KVR_ENOMEM;
     if (rewrite && (c->coff.ensure(nt) || c->l_src.ensure(nt) || c->l_off.ensure(nt + 1) || c->ctot.ensure(2)))
         return KVR_ENOMEM;
@@ -619,24 +662,37 @@ static int compact_front(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t
     if (rewrite) HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, c->csize.p, c->coff.p, (int)nt, st));
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, c->cflag.p, c->cpos.p, (int)nt, st));
     if (c->ctmp.ensure(std::max(t1, t2))) return KVR_ENOMEM;
-    HIPCHK(hipEventRecord(c->ev[0], st));
+again:
     HIPCHK(hipMemsetAsync(c->fent.p, 0xFF, slots * sizeof(FoldEnt), st));
+    c->fold_slots = slots;
     const uint32_t mask = (uint32_t)(slots - 1);
     const uint32_t *list = nullptr;   // round 0: every tuple
     uint64_t m = nt;
     for (uint32_t r = 0;; ++r) {
         uint32_t *next = c->flist.p + (uint64_t)(r & 1u) * nt;
         const uint32_t g = (uint32_t)((m + 255) / 256);
-        HIPCHK(hipMemsetAsync(c->fcnt.p, 0, 4, st));
-        hipLaunchKernelGGL(k_fold_claim, dim3(g), dim3(256), 0, st, c->ctup.p, m, list, c->segs.p, c->fent.p, mask,
-                           c->cslot.p);
+        HIPCHK(hipMemsetAsync(c->fcnt.p, 0, 8, st));
+        static const bool pre = getenv("KVR_CLAIM_PRELOAD") && atoi(getenv("KVR_CLAIM_PRELOAD"));   // timing knob
+        if (pre)
+            hipLaunchKernelGGL(k_fold_claim<true>, dim3(g), dim3(256), 0, st, c->ctup.p, m, list, c->segs.p, c->fent.p,
+                               mask, c->cslot.p, c->fcnt.p + 1);
+        else
+            hipLaunchKernelGGL(k_fold_claim<false>, dim3(g), dim3(256), 0, st, c->ctup.p, m, list, c->segs.p, c->fent.p,
+                               mask, c->cslot.p, c->fcnt.p + 1);
         hipLaunchKernelGGL(k_fold_verify, dim3(g), dim3(256), 0, st, c->ctup.p, m, list, c->segs.p, c->fent.p, mask,
                            c->cslot.p, next, c->fcnt.p);
         HIPCHK(hipGetLastError());
-        uint32_t left = 0;
-        HIPCHK(hipMemcpyAsync(&left, c->fcnt.p, 4, hipMemcpyDeviceToHost, st));
+        uint32_t cnt[2] = {0, 0};   // tuples left for the next round, claims that found the table full
+        HIPCHK(hipMemcpyAsync(cnt, c->fcnt.p, 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        const uint32_t left = cnt[0];
         c->fold_rounds = r + 1;
+        if (cnt[1]) {
+            if (slots == full_slots) return KVR_EHIP;   // cannot happen: 2 n entries hold every tuple
+            slots = full_slots;
+            ++c->fold_redo;
+            goto again;
+        }
         if (left == 0) break;
         // tuples whose tag another key holds: each round moves every one of them at least one
         // entry on, so mask + 1 rounds bound the loop (a few in practice)
@@ -645,6 +701,17 @@ static int compact_front(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t
         m = left;
     }
     return KVR_OK;
+}
+
+// live flags (and, for a rewrite, record sizes) of the tuples from the fold table
+static hipError_t live_flags(kvr_ctx *c, size_t nt, bool sizes) {
+    hipStream_t st = c->stream;
+    hipError_t e = hipMemsetAsync(c->cflag.p, 0, nt * 4, st);
+    if (e == hipSuccess && sizes) e = hipMemsetAsync(c->csize.p, 0, nt * 8, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_live_ent, dim3((uint32_t)((c->fold_slots + 255) / 256)), dim3(256), 0, st, c->fent.p,
+                       (uint64_t)c->fold_slots, c->ctup.p, sizes ? c->csize.p : nullptr, c->cflag.p);
+    return hipGetLastError();
 }
 
 // sizes and live flags are in csize / cflag: scans, dense live list, cuts, gather, output
@@ -728,9 +795,7 @@ int kvr_compact(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, u
     size_t nt = 0;
     const int rc = compact_front(c, segs, n, flags, err, &nt, true, &c->cstats);
     if (rc != KVR_OK || nt == 0) return rc;
-    hipLaunchKernelGGL(k_live, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, c->stream, c->ctup.p, (uint64_t)nt,
-                       c->fent.p, c->cslot.p, c->csize.p, c->cflag.p);
-    HIPCHK(hipGetLastError());
+    HIPCHK(live_flags(c, nt, true));
     return compact_back(c, flags, seg_target, out, out_cap, out_len, seg_ends, seg_cap, n_out_segs);
 }
 

@@ -17,10 +17,14 @@
  *                   16-B prefix from the entry itself, the rest of a longer key from the
  *                   representative's bytes) and, when equal, keeps the key's LAST tuple index by
  *                   atomicMin of ~index — the last-writer-wins fold of engine.rs:137 / :141 as
- *                   an associative max.  A tag collision between two keys sends the tuple to the
+ *                   an associative max.  Both kernels walk the tuples latest first: the claimer
+ *                   (which stores its own index as best) is then usually the key's last tuple,
+ *                   and a tuple below the best already stored skips its atomic (device-scope
+ *                   atomics execute at the memory side, about 20 G/s chip-wide).  A tag collision between two keys sends the tuple to the
  *                   next round, which resumes its probe one entry further (rounds until no tuple
  *                   is left; distinct keys sharing a CRC-32 are a few hundred per million keys)
- *   k_live          a tuple is live iff it is a SET and its key's last tuple: size 9 + k + v
+ *   k_live_ent      per claimed entry: its key's last tuple is live iff it is a SET: flag, size
+ *                   9 + k + v
  *   (scan)          exclusive sums of sizes (output offsets) and live flags (dense index)
  *   k_scatter       dense live list (source address, output offset) and, for every 512-B
  *                   output block, the live record holding its first byte
@@ -48,7 +52,7 @@ constexpr int CBLK_LOG = 9;
 static_assert(CBLK == 1 << CBLK_LOG, "block size");
 constexpr int CT_GATHER = 256;       // threads per gather workgroup (4 blocks)
 
-__device__ __forceinline__ uint32_t ht_mix(uint32_t h) {   // the key_tag is a CRC: spread it
+__host__ __device__ __forceinline__ uint32_t ht_mix(uint32_t h) {   // the key_tag is a CRC: spread it
     h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
     return h;
 }
@@ -89,9 +93,11 @@ struct __align__(32) FoldEnt {
 static_assert(sizeof(FoldEnt) == 32, "fold entry");
 constexpr unsigned long long FE_EMPTY = ~0ull;   // the table is memset to 0xFF
 
+
 // bytes [0, min(klen, 16)) of the key of tuple t, zero padded.  Aligned dword loads: a dword is
 // read only if it starts before the segment's end, so it holds a segment byte and cannot cross
-// into an unmapped page, whatever padding the caller's buffer has.
+// into an unmapped page, whatever padding the caller's buffer has.  (Two aligned 16-B loads
+// measured slower: 401 vs 333 us for k_fold_verify on cfg2.)
 __device__ __forceinline__ void key_prefix16(const SegDesc &g, const kvr_tuple &t, uint32_t w[4]) {
     const uintptr_t p = reinterpret_cast<uintptr_t>(g.base) + t.rec_off + 5;
     const uintptr_t end = reinterpret_cast<uintptr_t>(g.base) + g.len;
@@ -109,25 +115,83 @@ __device__ __forceinline__ void key_prefix16(const SegDesc &g, const kvr_tuple &
     }
 }
 
+// distinct-key estimate that sizes the fold table (HyperLogLog, 2^14 registers over the key
+// tags): each workgroup keeps registers in LDS and writes them out; k_hll_merge takes the max
+// over the workgroups.  A smaller table stays in the caches (the 256-MiB table for cfg2's 4 M
+// tuples holds 1 M keys).
+constexpr int HLL_P = 14, HLL_M = 1 << HLL_P, HLL_T = 256;
+__device__ __forceinline__ uint32_t hll_mix(uint32_t h) {   // independent of ht_mix's bits
+    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+    return h;
+}
+__global__ void __launch_bounds__(HLL_T) k_hll(const kvr_tuple *__restrict__ tup, uint64_t n, uint8_t *__restrict__ part) {
+    __shared__ uint32_t reg[HLL_M];
+    for (int j = threadIdx.x; j < HLL_M; j += HLL_T) reg[j] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * HLL_T + threadIdx.x; i < n; i += (uint64_t)gridDim.x * HLL_T) {
+        const uint32_t x = hll_mix(tup[i].key_tag);
+        const uint32_t rank = (uint32_t)__clz((x << HLL_P) | (1u << (HLL_P - 1))) + 1u;
+        atomicMax(&reg[x >> (32 - HLL_P)], rank);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < HLL_M; j += HLL_T) part[(uint64_t)blockIdx.x * HLL_M + j] = (uint8_t)reg[j];
+}
+// byte-wise max of two words of four registers each
+__device__ __forceinline__ uint32_t max4u8(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 32; k += 8) r |= max((a >> k) & 255u, (b >> k) & 255u) << k;
+    return r;
+}
+
+// 16 workgroups' worth of registers per thread-row: thread (g, s) takes register group g (16
+// registers, one 16-B load per partition) over partitions s, s + 16, ...; LDS folds the 16 rows
+constexpr int HLL_MERGE_T = 256;
+__global__ void __launch_bounds__(HLL_MERGE_T) k_hll_merge(const uint8_t *__restrict__ part, uint32_t n_parts,
+                                                           uint8_t *__restrict__ out) {
+    __shared__ uint4 acc[16][16];
+    const uint32_t gl = threadIdx.x & 15u, sl = threadIdx.x >> 4;
+    const uint32_t g = blockIdx.x * 16u + gl;   // register group: registers 16 g .. 16 g + 15
+    uint4 m = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t b = sl; b < n_parts; b += 16) {
+        const uint4 v = reinterpret_cast<const uint4 *>(part + (uint64_t)b * HLL_M)[g];
+        m = make_uint4(max4u8(m.x, v.x), max4u8(m.y, v.y), max4u8(m.z, v.z), max4u8(m.w, v.w));
+    }
+    acc[sl][gl] = m;
+    __syncthreads();
+    if (sl == 0) {
+        for (int r = 1; r < 16; ++r) {
+            const uint4 v = acc[r][gl];
+            m = make_uint4(max4u8(m.x, v.x), max4u8(m.y, v.y), max4u8(m.z, v.z), max4u8(m.w, v.w));
+        }
+        reinterpret_cast<uint4 *>(out)[g] = m;
+    }
+}
+
 // one probe round: tuple i (all tuples in round 0, list[] afterwards) walks from its start entry
 // (the tag's home slot in round 0, slot[i] afterwards) to the first entry that is free (claimed
 // here) or holds its tag (verified by k_fold_verify)
+template <bool PRE>
 __global__ void k_fold_claim(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ list,
                              const SegDesc *__restrict__ segs, FoldEnt *__restrict__ ent, uint32_t mask,
-                             uint32_t *__restrict__ slot) {
+                             uint32_t *__restrict__ slot, uint32_t *__restrict__ full) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n) return;
-    const uint32_t i = list ? list[g] : (uint32_t)g;
+    // latest tuples first (workgroups start in index order): a key's claimer is then usually its
+    // last tuple, which k_fold_verify exploits
+    const uint32_t i = list ? list[n - 1 - g] : (uint32_t)(n - 1 - g);
     const kvr_tuple t = tup[i];
     uint32_t h = list ? slot[i] : (ht_mix(t.key_tag) & mask);
     const unsigned long long mine = ((unsigned long long)t.key_tag << 32) | i;
+    uint32_t w[4];   // PRE: the key prefix, loaded alongside the probe (only a claimer stores it)
+    if (PRE) key_prefix16(segs[t.seg_idx], t, w);
     for (uint32_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
         unsigned long long v = __hip_atomic_load(&ent[h].tagrep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (v == FE_EMPTY) {
             v = atomicCAS(&ent[h].tagrep, FE_EMPTY, mine);
             if (v == FE_EMPTY) {   // claimed: this tuple represents its key in entry h
-                uint32_t w[4];
-                key_prefix16(segs[t.seg_idx], t, w);
+                if (!PRE) key_prefix16(segs[t.seg_idx], t, w);
+                ent[h].best = ~i;   // nobody else writes best during the claims
                 ent[h].klen = t.key_len;
                 *reinterpret_cast<uint4 *>(ent[h].key) = make_uint4(w[0], w[1], w[2], w[3]);
                 slot[i] = h;
@@ -139,7 +203,8 @@ __global__ void k_fold_claim(const kvr_tuple *__restrict__ tup, uint64_t n, cons
             return;
         }
     }
-    slot[i] = HT_EMPTY;   // unreachable: the table has at least n free entries
+    slot[i] = HT_EMPTY;   // the table is full (the distinct-key estimate was low): the host
+    atomicAdd(full, 1u);  // folds again with a table of 2 n entries
 }
 
 // same key as the entry's representative: keep the last index; else on to the next round
@@ -148,13 +213,14 @@ __global__ void k_fold_verify(const kvr_tuple *__restrict__ tup, uint64_t n, con
                               uint32_t *__restrict__ slot, uint32_t *__restrict__ next, uint32_t *__restrict__ n_next) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n) return;
-    const uint32_t i = list ? list[g] : (uint32_t)g;
+    const uint32_t i = list ? list[n - 1 - g] : (uint32_t)(n - 1 - g);   // latest first
     const uint32_t h = slot[i];
     if (h == HT_EMPTY) return;
     const uint4 a = reinterpret_cast<const uint4 *>(&ent[h])[0];
     const uint32_t rep = a.x;
-    bool same = rep == i;
-    if (!same) {
+    if (rep == i) return;   // the claimer stored its own index as best
+    bool same = false;
+    {
         const kvr_tuple t = tup[i];
         if (a.w == t.key_len) {
             const uint4 k = reinterpret_cast<const uint4 *>(&ent[h])[1];
@@ -166,7 +232,10 @@ __global__ void k_fold_verify(const kvr_tuple *__restrict__ tup, uint64_t n, con
         }
     }
     if (same) {
-        atomicMin(&ent[h].best, ~i);
+        // best only grows (as an index): a tuple below the best seen needs no atomic.  Latest
+        // first, a key's later tuples are usually done before its earlier ones run, so most
+        // tuples skip the (memory-side) atomic.
+        if (~a.z < i) atomicMin(&ent[h].best, ~i);
     } else {   // another key with this tag holds entry h: probe on from h + 1 next round
         next[atomicAdd(n_next, 1u)] = i;
         slot[i] = (h + 1) & mask;
@@ -178,15 +247,20 @@ __device__ __forceinline__ bool is_last(const FoldEnt *ent, const uint32_t *slot
     return s != HT_EMPTY && ~ent[s].best == (uint32_t)i;
 }
 
-// live flag and output size of every tuple
-__global__ void k_live(const kvr_tuple *__restrict__ tup, uint64_t n, const FoldEnt *__restrict__ ent,
-                       const uint32_t *__restrict__ slot, uint64_t *__restrict__ size, uint32_t *__restrict__ flag) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const kvr_tuple t = tup[i];
-    const bool live = t.op == 0 && is_last(ent, slot, i);
-    size[i] = live ? 9ull + t.key_len + t.val_len : 0ull;   // SET framing, engine.rs:169-173
-    flag[i] = live ? 1u : 0u;
+// live flags and output sizes, from the table's side: one thread per entry; a claimed entry's
+// last tuple is live iff it is a SET (flag and size must be zero beforehand).  Reads the table once (the
+// claimed entries' last tuples at random) instead of every tuple and its entry.
+__global__ void k_live_ent(const FoldEnt *__restrict__ ent, uint64_t n_slots, const kvr_tuple *__restrict__ tup,
+                           uint64_t *__restrict__ size, uint32_t *__restrict__ flag) {
+    const uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= n_slots) return;
+    const uint4 a = reinterpret_cast<const uint4 *>(&ent[h])[0];
+    if (a.x == 0xFFFFFFFFu && a.y == 0xFFFFFFFFu) return;   // free
+    const uint32_t j = ~a.z;
+    const kvr_tuple t = tup[j];
+    if (t.op != 0) return;
+    flag[j] = 1u;
+    if (size) size[j] = 9ull + t.key_len + t.val_len;   // SET framing, engine.rs:169-173
 }
 
 // totals: live bytes, live records, and the end sentinel of the dense offsets

@@ -22,19 +22,26 @@ __global__ void k_live_tuples(const kvr_tuple *__restrict__ tup, uint64_t n, con
     if (i < n && flag[i]) out[pos[i]] = tup[i];
 }
 
-// MurmurHash3's 32-bit finaliser: the home slot of a key tag (kvr_index_hash, host and device)
-__host__ __device__ __forceinline__ uint32_t ix_hash(uint32_t h) {
-    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
-    return h;
-}
+// the home slot of a key tag (kvr_index_hash, host and device): the fold table's hash, since
+// the index IS the fold table, entry for entry
+__host__ __device__ __forceinline__ uint32_t ix_hash(uint32_t h) { return ht_mix(h); }
 
-// live keys are distinct: every insert claims a free slot (no key compare)
-__global__ void k_index_insert(const kvr_tuple *__restrict__ live, uint64_t n, uint32_t *__restrict__ slots, uint32_t mask) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    uint32_t h = ix_hash(live[j].key_tag) & mask;
-    for (uint32_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask)
-        if (atomicCAS(&slots[h], 0u, (uint32_t)j + 1u) == 0u) return;
+constexpr uint32_t IX_DEAD = 0xFFFFFFFFu;   // a key whose last record is a DEL: probe on
+
+// slots[h] from fold entry h: free -> 0, a live key -> 1 + its position in the live list, a
+// deleted key -> IX_DEAD (keeps the probe sequences of the keys behind it intact).  No atomics:
+// the fold already placed every key.
+__global__ void k_index_from_fold(const FoldEnt *__restrict__ ent, uint64_t n_slots, const uint32_t *__restrict__ flag,
+                                  const uint32_t *__restrict__ pos, uint32_t *__restrict__ slots) {
+    const uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= n_slots) return;
+    const uint4 a = reinterpret_cast<const uint4 *>(&ent[h])[0];
+    uint32_t v = 0;
+    if (!(a.x == 0xFFFFFFFFu && a.y == 0xFFFFFFFFu)) {
+        const uint32_t j = ~a.z;
+        v = flag[j] ? pos[j] + 1u : IX_DEAD;
+    }
+    slots[h] = v;
 }
 
 uint64_t index_slots(uint64_t n_live) {
@@ -49,9 +56,7 @@ int live_list(kvr_ctx *c, size_t nt, uint64_t *total) {
     if (nt == 0) return KVR_OK;
     hipStream_t st = c->stream;
     const uint32_t g = (uint32_t)((nt + 255) / 256);
-    hipLaunchKernelGGL(k_live, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->fent.p, c->cslot.p,
-                       c->csize.p, c->cflag.p);
-    HIPCHK(hipGetLastError());
+    HIPCHK(live_flags(c, nt, false));
     size_t tb = c->ctmp.n;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->cflag.p, c->cpos.p, (int)nt, st));
     uint32_t last[2] = {0, 0};
@@ -127,14 +132,15 @@ int kvr_replay_index(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fla
         rc = live_list(c, nt, &total);
         if (rc != KVR_OK) return rc;
     }
-    const uint64_t ns = index_slots(total);
+    const uint64_t ns = nt ? c->fold_slots : 16;
     if (c->islots.ensure(ns)) return KVR_ENOMEM;
     hipStream_t st = c->stream;
-    HIPCHK(hipMemsetAsync(c->islots.p, 0, ns * 4, st));
-    if (total) {
-        hipLaunchKernelGGL(k_index_insert, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, st, c->lout.p, total,
-                           c->islots.p, (uint32_t)(ns - 1));
+    if (nt) {
+        hipLaunchKernelGGL(k_index_from_fold, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, st, c->fent.p, ns,
+                           c->cflag.p, c->cpos.p, c->islots.p);
         HIPCHK(hipGetLastError());
+    } else {
+        HIPCHK(hipMemsetAsync(c->islots.p, 0, ns * 4, st));
     }
     HIPCHK(hipEventRecord(c->ev[4], st));
     HIPCHK(hipStreamSynchronize(st));
@@ -145,6 +151,9 @@ int kvr_replay_index(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fla
     c->istats.n_live = total;
     c->istats.n_slots = ns;
     c->istats.fold_rounds = c->fold_rounds;
+    c->istats.fold_slots = c->fold_slots;
+    c->istats.fold_est = c->fold_est;
+    c->istats.fold_redo = c->fold_redo;
     *n_live = total;
     *n_slots = ns;
     rc = index_copy_out(c, flags, live, live_cap, slots, slot_cap);
@@ -212,6 +221,7 @@ int64_t kvr_index_find(const kvr_tuple *live, const uint32_t *slots, uint64_t n_
     for (uint64_t h = ix_hash(tag) & mask, probe = 0; probe < n_slots; ++probe, h = (h + 1) & mask) {
         const uint32_t v = slots[h];
         if (v == 0) return -1;
+        if (v == IX_DEAD) continue;
         const kvr_tuple &t = live[v - 1];
         if (t.key_tag == tag && t.key_len == klen &&
             (klen == 0 || memcmp(segs[t.seg_idx].bytes + t.rec_off + 5, key, klen) == 0))

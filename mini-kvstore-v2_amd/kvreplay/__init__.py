@@ -89,7 +89,8 @@ class CompactStats(C.Structure):
 class IndexStats(C.Structure):
     _fields_ = [("ms_wall", C.c_double), ("ms_replay", C.c_double), ("ms_fold", C.c_double),
                 ("bytes_in", C.c_uint64), ("n_tuples", C.c_uint64), ("n_live", C.c_uint64),
-                ("n_slots", C.c_uint64), ("fold_rounds", C.c_uint32), ("pad", C.c_uint32)]
+                ("n_slots", C.c_uint64), ("fold_rounds", C.c_uint32), ("fold_redo", C.c_uint32),
+                ("fold_est", C.c_uint64), ("fold_slots", C.c_uint64)]
 
 
 class OpenStats(C.Structure):

@@ -87,11 +87,14 @@ def keys_of(segs, tuples):
     return [bytes(segs[t["seg_idx"]][t["rec_off"] + 5: t["rec_off"] + 5 + t["key_len"]]) for t in tuples]
 
 
+DEAD = 0xFFFFFFFF
+
+
 def check_index(idx, segs, want, absent=()):
     assert np.array_equal(idx.live, want)
     ns = len(idx.slots)
-    assert ns == max(16, 1 << max(0, (2 * len(want) - 1).bit_length())) or (len(want) == 0 and ns == 16)
-    used = idx.slots[idx.slots != 0]
+    assert ns >= 16 and ns & (ns - 1) == 0 and ns > len(want)
+    used = idx.slots[(idx.slots != 0) & (idx.slots != DEAD)]
     assert len(used) == len(want) and len(np.unique(used)) == len(want)
     for j, k in enumerate(keys_of(segs, want)):
         assert idx.find(k, segs) == j
@@ -138,6 +141,34 @@ def test_fold_tag_collisions(gctx):
 
 
 @pytest.mark.gpu
+def test_fold_table_redo(gctx, monkeypatch):
+    """A fold table sized below the distinct keys (forced to 16 entries) fills up; the fold is
+    redone at 2 n entries and gives the same answer."""
+    segs, pairs = collision_store()
+    want, nk, _ = expect(segs)
+    monkeypatch.setenv("KVR_FOLD_TINY_TABLE", "1")
+    idx = gctx.replay_index(segs)
+    assert idx.stats.fold_redo == 1 and np.array_equal(idx.live, want)
+    monkeypatch.delenv("KVR_FOLD_TINY_TABLE")
+    idx = gctx.replay_index(segs)
+    assert idx.stats.fold_redo == 0 and np.array_equal(idx.live, want)
+
+
+@pytest.mark.gpu
+def test_fold_table_estimate(gctx):
+    """cfg-like input with many more tuples than keys: the table is sized from the HyperLogLog
+    estimate (within a few percent of the true key count), not from the tuples."""
+    spec = K.GenSpec(seed=100, seg_bytes=8_000_000, key_space_log2=15, val_min=8, val_max=64, del_permille=0)
+    segs = [K.gen_segment_cpu(spec, s)[0] for s in range(4)]
+    want, nk, _ = expect(segs)
+    idx = gctx.replay_index(segs)
+    st = idx.stats
+    assert np.array_equal(idx.live, want) and st.n_tuples > 8 * nk
+    assert abs(st.fold_est - nk) < 0.05 * nk
+    assert st.fold_slots < st.n_tuples and st.fold_slots >= 1.6 * st.fold_est
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["persistence", "store_integration", "compaction_example", "large_dataset"])
 def test_replay_index_golden(gctx, name):
     d = os.path.join(GOLD, name)
@@ -163,8 +194,8 @@ def test_replay_index_generated(gctx, spec):
     want, nk, tb = expect(segs)
     idx = gctx.replay_index(segs)
     assert np.array_equal(idx.live, want) and idx.stats.n_live == nk
-    used = idx.slots[idx.slots != 0]
-    assert len(np.unique(used)) == nk
+    used = idx.slots[(idx.slots != 0) & (idx.slots != DEAD)]
+    assert len(used) == nk and len(np.unique(used)) == nk
     ks = keys_of(segs, want)
     for j in range(0, nk, max(1, nk // 300)):
         assert idx.find(ks[j], segs) == j

@@ -42,6 +42,17 @@ for s in $STEPS; do
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profc" -o run -- \
         python "$R/bench.py" --mode compact --steps 5 --warmup 2 > "$OUT/profc.log" 2>&1) || { echo "rocprof compact failed"; tail -20 "$OUT/profc.log"; exit 1; }
       find "$OUT/profc" -name '*kernel_stats.csv' -exec cat {} \; ;;
+    profi)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profi" -o run -- \
+        python "$R/tools/prof_index.py" cfg2 5 > "$OUT/profi.log" 2>&1) || { echo "rocprof index failed"; tail -20 "$OUT/profi.log"; exit 1; }
+      cat "$OUT/profi.log"; find "$OUT/profi" -name '*kernel_stats.csv' -exec cat {} \; ;;
+    profi2)   # the same with the claim kernel preloading key prefixes (timing knob)
+      (cd /tmp && KVR_CLAIM_PRELOAD=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profi2" -o run -- \
+        python "$R/tools/prof_index.py" cfg2 5 > "$OUT/profi2.log" 2>&1) || { echo "rocprof index2 failed"; tail -20 "$OUT/profi2.log"; exit 1; }
+      cat "$OUT/profi2.log"; find "$OUT/profi2" -name '*kernel_stats.csv' -exec grep -E "fold|k_live|index" {} \; ;;
+    benchc)
+      timeout -k 10 300 python -u bench.py --mode compact > "$OUT/bench_compact.json" 2> "$OUT/bench_compact.err" || { echo "bench compact failed"; tail -20 "$OUT/bench_compact.err"; exit 1; }
+      cat "$OUT/bench_compact.json" ;;
     phases)
       timeout -k 10 240 python -u tools/prof_phases.py cfg2 > "$OUT/phases_cfg2.txt" 2>&1 || { echo "phases failed"; tail -20 "$OUT/phases_cfg2.txt"; exit 1; }
       cat "$OUT/phases_cfg2.txt" ;;

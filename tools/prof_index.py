@@ -33,4 +33,5 @@ for i in range(reps):
     ix = ctx.replay_index(segs, on_device=True)
     st = ix.stats
     print(f"{cfg} replay_index: wall {st.ms_wall:.3f} ms  replay {st.ms_replay:.3f}  fold+live+table {st.ms_fold:.3f}  "
-          f"tuples {st.n_tuples} live {st.n_live} rounds {st.fold_rounds}", flush=True)
+          f"tuples {st.n_tuples} live {st.n_live} rounds {st.fold_rounds} est {st.fold_est} slots {st.fold_slots} "
+          f"redo {st.fold_redo}", flush=True)
