@@ -190,6 +190,17 @@ int64_t  kvr_index_find(const kvr_tuple *live, const uint32_t *slots, uint64_t n
  * > n_live (kvr_index_slots(n_live) gives the device's size). */
 int      kvr_index_build_host(const kvr_tuple *live, size_t n_live, uint32_t *slots, uint64_t n_slots);
 
+/* Key arena (the KVR_EMIT_KEYS option): the key bytes of the live list of the last
+ * kvr_replay_live / kvr_replay_index / kvr_ingest_index call on ctx, packed in live-list order —
+ * key i is keys[key_off[i] .. key_off[i + 1]), key_off has n_live + 1 entries, *key_bytes = the
+ * total.  With the live tuples it is the reference's String-keyed map (engine.rs:114 from_utf8
+ * of these bytes, index.rs:7) for a host that does not hold the segment bytes, e.g. a store
+ * generated or kept in HBM.  The segments of that call must still be where they were.
+ * flags: KVR_OUT_ON_DEVICE.  KVR_CAPACITY (*key_bytes set) when keys_cap or off_cap is short;
+ * KVR_EINVAL when ctx holds no live list. */
+int  kvr_live_keys(kvr_ctx *ctx, uint32_t flags, uint8_t *keys, uint64_t keys_cap, uint64_t *key_off,
+                   size_t off_cap, uint64_t *key_bytes);
+
 /* ---- ingest: the store's files into HBM while they are being read -------------------------
  * kvr_ingest_begin reserves HBM for total_bytes of segments (KVR_ENOMEM when they do not fit:
  * replay them batch-wise with kvr_replay_stream instead).  kvr_ingest_push queues the copy of one

@@ -132,6 +132,8 @@ struct kvr_ctx {
     // open-time index (kvr_replay_index) and ingest (kvr_ingest_*): the live list stays in lout,
     // the key table in islots, until the next call
     DevBuf<uint32_t> islots;
+    DevBuf<uint64_t> koff, klen;           // key arena (kvr_live_keys): offsets, lengths
+    DevBuf<uint8_t> kbuf;
     uint64_t ix_live = 0, ix_slots = 0;
     bool ix_valid = false;
     kvr_index_stats istats{};
@@ -284,6 +286,7 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
     c->ctup.release(); c->lout.release(); c->fent.release(); c->flist.release(); c->fcnt.release();
     c->cslot.release(); c->cflag.release(); c->islots.release(); c->ing.release(); c->hpart.release(); c->hreg.release();
+    c->koff.release(); c->klen.release(); c->kbuf.release();
     c->cpos.release(); c->cfirst.release(); c->csize.release(); c->coff.release(); c->l_src.release();
     c->l_off.release(); c->ctot.release(); c->ccuts.release(); c->cout.release(); c->ctmp.release();
     c->c_gidx.release(); c->c_own.release(); c->c_sidx.release(); c->c_val.release(); c->c_scan.release();

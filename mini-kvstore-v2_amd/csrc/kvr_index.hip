@@ -44,6 +44,22 @@ __global__ void k_index_from_fold(const FoldEnt *__restrict__ ent, uint64_t n_sl
     slots[h] = v;
 }
 
+// key arena: live key i's bytes to keys[off[i] ..) — one thread per key (keys are short; a
+// long one loops), 4-B stores where the destination allows
+__global__ void k_key_lens(const kvr_tuple *__restrict__ live, uint64_t n, uint64_t *__restrict__ len) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) len[i] = live[i].key_len;
+}
+__global__ void k_key_copy(const kvr_tuple *__restrict__ live, uint64_t n, const SegDesc *__restrict__ segs,
+                           const uint64_t *__restrict__ off, uint8_t *__restrict__ keys) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const kvr_tuple t = live[i];
+    const uint8_t *src = segs[t.seg_idx].base + t.rec_off + 5;   // [op][klen u32][key] (engine.rs:169-171)
+    uint8_t *dst = keys + off[i];
+    for (uint32_t b = 0; b < t.key_len; ++b) dst[b] = src[b];
+}
+
 uint64_t index_slots(uint64_t n_live) {
     uint64_t s = 16;
     while (s < 2 * n_live) s <<= 1;
@@ -93,11 +109,14 @@ int kvr_replay_live(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flag
     size_t nt = 0;
     kvr_compact_stats cs{};
     int rc = compact_front(c, segs, n, flags, err, &nt, false, &cs);   // replay + fold (kvr_compact.hip)
-    if (rc != KVR_OK || nt == 0) return rc;
+    if (rc != KVR_OK) return rc;
     uint64_t total = 0;
     rc = live_list(c, nt, &total);
     if (rc != KVR_OK) return rc;
     *n_out = total;
+    c->ix_live = total;   // kvr_live_keys reads this live list
+    c->ix_slots = 0;
+    c->ix_valid = true;
     if (total > cap) return KVR_CAPACITY;
     if (total == 0) return KVR_OK;
     const hipMemcpyKind k = (flags & KVR_OUT_ON_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -165,6 +184,44 @@ int kvr_index_fetch(kvr_ctx *c, uint32_t flags, kvr_tuple *live, size_t live_cap
     if (!c || !c->ix_valid || (live_cap && !live) || (slot_cap && !slots)) return KVR_EINVAL;
     if (flags & ~KVR_OUT_ON_DEVICE) return KVR_EINVAL;
     return index_copy_out(c, flags, live, live_cap, slots, slot_cap);
+}
+
+int kvr_live_keys(kvr_ctx *c, uint32_t flags, uint8_t *keys, uint64_t keys_cap, uint64_t *key_off, size_t off_cap,
+                  uint64_t *key_bytes) {
+    if (!c || !key_bytes || (keys_cap && !keys) || (off_cap && !key_off)) return KVR_EINVAL;
+    if (flags & ~KVR_OUT_ON_DEVICE) return KVR_EINVAL;
+    if (!c->ix_valid) return KVR_EINVAL;   // no live list (or a later call replaced it)
+    const uint64_t n = c->ix_live;
+    hipStream_t st = c->stream;
+    *key_bytes = 0;
+    if (c->koff.ensure(n + 1)) return KVR_ENOMEM;
+    if (n) {
+        const uint32_t g = (uint32_t)((n + 255) / 256);
+        if (c->klen.ensure(n + 1)) return KVR_ENOMEM;
+        hipLaunchKernelGGL(k_key_lens, dim3(g), dim3(256), 0, st, c->lout.p, n, c->klen.p);
+        HIPCHK(hipMemsetAsync(c->klen.p + n, 0, 8, st));
+        size_t tb = 0;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, c->klen.p, c->koff.p, (int)(n + 1), st));
+        if (c->ctmp.n < tb && c->ctmp.ensure(tb)) return KVR_ENOMEM;
+        tb = c->ctmp.n;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->klen.p, c->koff.p, (int)(n + 1), st));
+        HIPCHK(hipMemcpyAsync(key_bytes, c->koff.p + n, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (c->kbuf.ensure(*key_bytes + 1)) return KVR_ENOMEM;
+        hipLaunchKernelGGL(k_key_copy, dim3(g), dim3(256), 0, st, c->lout.p, n, c->segs.p, c->koff.p, c->kbuf.p);
+        HIPCHK(hipGetLastError());
+    } else {
+        HIPCHK(hipMemsetAsync(c->koff.p, 0, 8, st));
+    }
+    if (*key_bytes > keys_cap || n + 1 > off_cap) {
+        HIPCHK(hipStreamSynchronize(st));
+        return KVR_CAPACITY;
+    }
+    const hipMemcpyKind k = (flags & KVR_OUT_ON_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    if (*key_bytes) HIPCHK(hipMemcpyAsync(keys, c->kbuf.p, *key_bytes, k, st));
+    HIPCHK(hipMemcpyAsync(key_off, c->koff.p, (n + 1) * 8, k, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return KVR_OK;
 }
 
 int kvr_last_index_stats(const kvr_ctx *c, kvr_index_stats *out) {

@@ -146,6 +146,7 @@ def _load():
     rep.kvr_replay_index.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, P, U64, C.POINTER(SZ), C.POINTER(U64),
                                      C.POINTER(Error)]
     rep.kvr_index_fetch.argtypes = [P, U32, P, SZ, P, U64]
+    rep.kvr_live_keys.argtypes = [P, U32, P, U64, P, SZ, C.POINTER(U64)]
     rep.kvr_last_index_stats.argtypes = [P, C.POINTER(IndexStats)]
     rep.kvr_index_slots.argtypes = [U64]
     rep.kvr_index_slots.restype = U64
@@ -627,6 +628,20 @@ class Context:
         finally:
             if host_mem:
                 self._rep.kvr_host_free(host_mem)
+
+    def live_keys(self, n_live):
+        """Key arena of the last replay_live / replay_index / ingest_index (kvr_live_keys), whose
+        live list has n_live tuples -> (packed key bytes uint8 array, offsets: n_live + 1 uint64)."""
+        kb = C.c_uint64()
+        offs = np.zeros(n_live + 1, dtype=np.uint64)
+        rc = self._rep.kvr_live_keys(self.h, 0, None, 0, offs.ctypes.data, offs.size, C.byref(kb))
+        if rc not in (OK, CAPACITY):
+            raise NativeError(f"kvr_live_keys: {rc}")
+        keys = np.zeros(max(kb.value, 1), dtype=np.uint8)
+        rc = self._rep.kvr_live_keys(self.h, 0, keys.ctypes.data, keys.size, offs.ctypes.data, offs.size, C.byref(kb))
+        if rc != OK:
+            raise NativeError(f"kvr_live_keys: {rc}")
+        return keys[: kb.value], offs
 
     def etag_batch(self, data, offs, lens, expected=None, on_device=False, data_len=None):
         """Batch ETag (kvr_etag_batch): CRC-32 of data[offs[i]:offs[i]+lens[i]] for every i.

@@ -311,3 +311,39 @@ def test_kvs_open_golden_host_fold(gctx, tmp_path):
     assert s.locate("counter") == (2, 16, 2)
     assert (s.stats().num_keys, s.stats().total_bytes) == (2, 7)
     s.close()
+
+
+@pytest.mark.gpu
+def test_live_keys_arena(gctx):
+    """kvr_live_keys: the live keys' bytes packed in live order equal the oracle's key bytes —
+    from host segments (replay_index), from segments in HBM (replay_live on device pointers, the
+    host holding no bytes) and after an ingest."""
+    torch = pytest.importorskip("torch")
+    segs, pairs = collision_store()
+    spec = K.GenSpec(seed=101, seg_bytes=300_000, key_space_log2=10, val_min=0, val_max=100, del_permille=300)
+    segs = segs + [K.gen_segment_cpu(spec, s)[0] for s in range(3)]
+    want, nk, _ = expect(segs)
+    wkeys = keys_of(segs, want)
+
+    def check(n):
+        keys, offs = gctx.live_keys(n)
+        assert n == nk and offs[0] == 0 and int(offs[-1]) == len(keys) == sum(len(k) for k in wkeys)
+        assert [bytes(keys[offs[i]: offs[i + 1]]) for i in range(n)] == wkeys
+
+    idx = gctx.replay_index(segs)
+    check(len(idx.live))
+    buf = torch.zeros(sum(len(x) + 16 for x in segs), dtype=torch.uint8, device="cuda")
+    ptrs, off = [], 1
+    for x in segs:
+        buf[off: off + len(x)] = torch.from_numpy(np.frombuffer(bytes(x), dtype=np.uint8).copy()).cuda()
+        ptrs.append((buf.data_ptr() + off, len(x)))
+        off += len(x) + 3
+    torch.cuda.synchronize()
+    r = gctx.replay_live(ptrs, on_device=True)
+    assert r.status == 0 and np.array_equal(r.tuples, want)
+    check(r.n)
+    ig = gctx.ingest_index(segs, pinned=True)
+    check(len(ig.live))
+    gctx.replay_live([])
+    k, o = gctx.live_keys(0)
+    assert len(k) == 0 and list(o) == [0]
