@@ -65,6 +65,17 @@ struct DevBuf {
 
 constexpr uint32_t REDO_GRID = 1024;
 
+// k_replay keeps 32-bit pool slots in LDS; KVR_POOL_LIMIT lowers the limit (test knob)
+uint64_t pool_limit() {
+    const char *e = getenv("KVR_POOL_LIMIT");
+    return e ? std::max<uint64_t>(strtoull(e, nullptr, 10), 1024) : 0xFFFFFF00ull;
+}
+
+__global__ void k_shift_seg(kvr_tuple *t, uint64_t n, uint32_t by) {   // seg_idx of a batch's tuples
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) t[i].seg_idx += by;
+}
+
 }  // namespace
 
 struct kvr_ctx {
@@ -113,6 +124,7 @@ struct kvr_ctx {
     std::vector<SegDesc> h_segs;
     std::vector<StripeDesc> h_stripes;
     uint64_t pool_hint = 0;
+    uint64_t pool_need = 0;                // > 0: the last replay needed more than 32-bit pool slots
     uint32_t tps_override = 0;
     kvr_stats stats{};
     // streamed ingest (kvr_replay_stream): two HBM batch slots filled on a copy stream, two pinned
@@ -334,9 +346,70 @@ static float ev_ms(hipEvent_t a, hipEvent_t b) {
     return ms;
 }
 
+static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, const uint32_t *expected,
+                      size_t n_expected, kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err);
+
+// a replay whose tuples exceed the pool's 32-bit slots (dense small records: more than about
+// 4 G records in one call) runs as consecutive batches of whole segments, each its own
+// pipeline, the tuples appended in order — the same output, errors and return codes
+static int replay_batched(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, const uint32_t *expected,
+                          size_t n_expected, kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err, uint64_t need) {
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; ++i) total += segs[i].len;
+    const uint64_t parts = need / (pool_limit() / 2) + 1;
+    const uint64_t budget = total / parts + 1;
+    size_t done = 0;
+    kvr_stats sum{};
+    for (size_t s0 = 0; s0 < n;) {
+        size_t s1 = s0;
+        uint64_t b = 0;
+        while (s1 < n && (s1 == s0 || b + segs[s1].len <= budget)) b += segs[s1++].len;
+        if (s1 - s0 == n) return KVR_ENOMEM;   // one segment alone is too dense to split here
+        const size_t e0 = std::min(done, n_expected);
+        const size_t room = done < cap ? cap - done : 0;
+        size_t nb = 0;
+        kvr_error e{};
+        const int rc = kvr_replay(c, segs + s0, s1 - s0, flags, expected ? expected + e0 : nullptr,
+                                  expected ? n_expected - e0 : 0, room ? out + done : nullptr, room, &nb, &e);
+        sum.ms_total += c->stats.ms_total; sum.ms_replay += c->stats.ms_replay; sum.ms_link += c->stats.ms_link;
+        sum.ms_compact += c->stats.ms_compact; sum.bytes_in += c->stats.bytes_in; sum.n_records += c->stats.n_records;
+        sum.n_crc_fail += c->stats.n_crc_fail; sum.n_stripes += c->stats.n_stripes; sum.n_tiles += c->stats.n_tiles;
+        sum.n_redo += c->stats.n_redo; sum.n_link_passes += c->stats.n_link_passes;
+        if (rc == KVR_CORRUPTED) {   // batches run in (segment, offset) order: the store's first error
+            if (err) { *err = e; err->seg_idx += (uint32_t)s0; }
+            c->stats = sum;
+            return rc;
+        }
+        if (rc != KVR_OK && rc != KVR_CAPACITY) return rc;
+        if (s0 && !(flags & KVR_OUT_ON_DEVICE)) {   // seg_idx into the caller's segs[]
+            for (size_t t = 0, m = std::min(nb, room); t < m; ++t) out[done + t].seg_idx += (uint32_t)s0;
+        } else if (s0 && nb) {
+            hipLaunchKernelGGL(k_shift_seg, dim3((uint32_t)((std::min(nb, room) + 255) / 256)), dim3(256), 0, c->stream,
+                               out + done, (uint64_t)std::min(nb, room), (uint32_t)s0);
+            HIPCHK(hipStreamSynchronize(c->stream));
+        }
+        done += nb;
+        s0 = s1;
+    }
+    c->stats = sum;
+    *n_out = done;
+    return done > cap ? KVR_CAPACITY : KVR_OK;
+}
+
 int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, const uint32_t *expected,
                size_t n_expected, kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err) {
     if (!c || (!segs && n) || !n_out || (cap && !out)) return KVR_EINVAL;
+    uint64_t need = 0;
+    const int rc = replay_one(c, segs, n, flags, expected, n_expected, out, cap, n_out, err);
+    if (rc != KVR_ENOMEM || !c->pool_need) return rc;
+    need = c->pool_need;   // the pool this input needs exceeds 32-bit slots: batch it
+    c->pool_need = 0;
+    c->pool_hint = 0;
+    return replay_batched(c, segs, n, flags, expected, n_expected, out, cap, n_out, err, need);
+}
+
+static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, const uint32_t *expected,
+                      size_t n_expected, kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err) {
     if (err) memset(err, 0, sizeof(*err));
     *n_out = 0;
     memset(&c->stats, 0, sizeof(c->stats));
@@ -430,7 +503,10 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
         const uint32_t pool_chunk = POOL_CHUNK;
         const uint64_t pool_cap = std::max<uint64_t>(
             c->pool_hint, std::max<uint64_t>(65536, total_bytes / 192 + n + (uint64_t)n_stripes * pool_chunk));
-        if (pool_cap > 0xFFFFFF00ull) return KVR_ENOMEM;   // k_replay keeps 32-bit pool slots in LDS
+        if (pool_cap > pool_limit()) {   // k_replay keeps 32-bit pool slots in LDS: kvr_replay batches
+            c->pool_need = pool_cap;
+            return KVR_ENOMEM;
+        }
         if (c->pool.ensure(pool_cap)) return KVR_ENOMEM;
         kvr_tuple *d_out;
         uint64_t out_cap;

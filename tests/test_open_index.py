@@ -347,3 +347,31 @@ def test_live_keys_arena(gctx):
     gctx.replay_live([])
     k, o = gctx.live_keys(0)
     assert len(k) == 0 and list(o) == [0]
+
+
+@pytest.mark.gpu
+def test_replay_batches_past_pool_limit(gctx, monkeypatch):
+    """A replay whose tuple pool would exceed the 32-bit slot limit runs as consecutive batches
+    of whole segments (the limit lowered by KVR_POOL_LIMIT): same tuples, CRC verification, first
+    error and device output as one pass."""
+    torch = pytest.importorskip("torch")
+    spec = K.GenSpec(seed=102, seg_bytes=300_000, key_space_log2=12, val_min=0, val_max=400, del_permille=200,
+                     flip_per_million=3000)
+    parts = [K.gen_segment_cpu(spec, s) for s in range(12)]
+    segs = [p[0] for p in parts]
+    man = np.concatenate([p[1] for p in parts])
+    rc, want, _ = O.replay(segs, expected=man)
+    assert rc == 0 and (want["flags"] & K.TF_CRC_FAIL).any()
+    monkeypatch.setenv("KVR_POOL_LIMIT", "400000")
+    r = gctx.replay(segs, expected=man)
+    assert r.status == 0 and np.array_equal(r.tuples, want)
+    assert r.stats.n_records == len(want) and r.stats.n_crc_fail == int((want["flags"] & K.TF_CRC_FAIL != 0).sum())
+    bad = segs[:9] + [segs[9][:-3]] + segs[10:]
+    rc, _, err = O.replay(bad)
+    r = gctx.replay(bad)
+    assert r.status == 1 and (r.error.kind, r.error.seg_idx, r.error.rec_off) == (err.kind, err.seg_idx, err.rec_off)
+    out = torch.zeros((len(want) + 8) * 32, dtype=torch.uint8, device="cuda")
+    r = gctx.replay(segs, on_device=False, out_ptr=out.data_ptr(), cap=len(want) + 8)
+    assert r.status == 0 and r.n == len(want)
+    got = out[: len(want) * 32].cpu().numpy().view(K.TUPLE_DTYPE)
+    assert np.array_equal(got["seg_idx"], want["seg_idx"]) and np.array_equal(got["rec_off"], want["rec_off"])
