@@ -97,6 +97,11 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {   // wave-uniform value 
 __device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 // lane l's value, l wave-uniform (v_readlane: no LDS traffic, unlike a shuffle)
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+// old with lane l set to the uniform val (v_writelane_b32: one VALU instruction, no compare/select)
+__device__ __forceinline__ uint32_t wl32(uint32_t old, uint32_t val, uint32_t l) {
+    asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(old) : "s"(val), "s"(l) : "m0");
+    return old;
+}
 __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
     return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
 }
@@ -649,12 +654,14 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         const bool walk = in_stripe && !search && entry < vhi;
         uint64_t tile_exit = entry;
         // the long values touching this tile, folded into every unit's view as they are found
-        bool vx = false;                     // a long value crosses the end of this unit
+        // (per-lane flags as 32-bit values: a per-lane bool lives in an SGPR lane mask, and every
+        // update of it is scalar work in the SALU-bound hop loop)
+        uint32_t vx = 0;                     // a long value crosses the end of this unit
         int32_t a_off = -1;                  // ... starting inside the unit at a_off
-        bool vx_carry = false;               // ... the value carried in from the previous tile
+        uint32_t vx_carry = 0;               // ... the value carried in from the previous tile
         int32_t m = 0;                       // a long value ends inside this unit, at m (1 .. SC)
         uint64_t m_ref = 0;                  // ... its tuple: a slot (m_abs) or a record index of the tile
-        bool m_abs = false;
+        uint32_t m_abs = 0;
         bool any_long = false;               // (uniform) some long value touches the tile
         bool out = false;                    // (uniform) a value crosses the tile end
         uint64_t out_ve = 0, out_ref = 0;
@@ -662,9 +669,22 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         auto consider = [&](int32_t vb, uint64_t ve_abs, uint64_t ref, bool is_abs, bool from_carry) {
             const int64_t v64 = (int64_t)ve_abs - lo;
             const int32_t ver = v64 > FAR ? FAR : (int32_t)v64;
-            if (vb < ue && ver > ue) { vx = true; a_off = vb >= us ? vb - us : -1; vx_carry = from_carry; }
-            if (vb < us && ver > us && ver <= ue) { m = ver - us; m_ref = ref; m_abs = is_abs; }
+            if (vb < ue && ver > ue) { vx = 1u; a_off = vb >= us ? vb - us : -1; vx_carry = from_carry ? 1u : 0u; }
+            if (vb < us && ver > us && ver <= ue) { m = ver - us; m_ref = ref; m_abs = is_abs ? 1u : 0u; }
             if (ver > TILE) { out = true; out_ve = ve_abs; out_ref = ref; out_abs = is_abs; }
+            any_long = true;
+        };
+        // the same for a value of this tile's records, tile-relative [vb, ver) (ver <= 2^31), in
+        // 32-bit arithmetic (the hop loop's common case)
+        auto consider_rel = [&](int32_t vb, int32_t ver, uint32_t ref) {
+            const bool cx = vb < ue && ver > ue, cm = vb < us && ver > us && ver <= ue;
+            vx = cx ? 1u : vx;
+            a_off = cx ? (vb >= us ? vb - us : -1) : a_off;
+            vx_carry = cx ? 0u : vx_carry;
+            m = cm ? ver - us : m;
+            m_ref = cm ? (uint64_t)ref : m_ref;
+            m_abs = cm ? 0u : m_abs;
+            if (ver > TILE) { out = true; out_ve = (uint64_t)(lo + ver); out_ref = ref; out_abs = false; }
             any_long = true;
         };
         uint32_t n_carry = 0;
@@ -734,8 +754,49 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     }
                     return q;
                 };
+                // the common case: 32-bit, flags as integers, the batch's per-lane record fields
+                // written with v_writelane (one instruction each, no lane compare and select)
+                auto hops32 = [&](int32_t q) -> int32_t {
+                    const int32_t remT = (int32_t)rem, vhiT = (int32_t)vhi_r;
+                    uint32_t brk = 0;
+#pragma unroll 1
+                    while (q < vhiT && nb < 64u) {
+                        uint32_t op, klen;
+                        if (q + 8 <= TILE) {
+                            const uint64_t x = tu64((int)q);
+                            op = (uint32_t)x & 255u;
+                            klen = (uint32_t)(x >> 8);
+                        } else {                     // the header crosses the tile end
+                            op = uni32(ts.b8(q));
+                            klen = remT - q >= 5 ? uni32(ts.u32(q + 1)) : 0u;
+                        }
+                        myrec = (int32_t)wl32((uint32_t)myrec, (uint32_t)q, nb);
+                        my_op = wl32(my_op, op, nb);
+                        my_klen = wl32(my_klen, klen, nb);
+                        ++nb;
+                        if (op > 1u || remT - q < 5 || klen > (uint32_t)(remT - q - 5)) { brk = 1; break; }
+                        kmx = klen > kmx ? klen : kmx;
+                        const int32_t e = q + 5 + (int32_t)klen;
+                        if (op == 1u) { q = e; continue; }
+                        if (remT - e < 4) { brk = 1; break; }
+                        const uint32_t vlen = e + 8 <= TILE ? (uint32_t)tu64((int)e) : uni32(ts.u32(e));
+                        my_vlen = wl32(my_vlen, vlen, nb - 1u);
+                        const int32_t vb = e + 4;
+                        if (vlen > (uint32_t)(remT - vb)) { brk = 1; break; }
+                        const int32_t e2 = vb + (int32_t)vlen;
+                        if (vlen > (uint32_t)SMALL && (vb >> SC_LOG) != ((e2 - 1) >> SC_LOG)) {
+                            const uint32_t idx = nrec + nb - 1;
+                            if (KVR_ABLATE & 32) any_long = true;
+                            else if (vb < TILE) consider_rel(vb, e2, idx);
+                            else { n_carry = 2; n_vb = (uint64_t)(lo + vb); n_ve = (uint64_t)(lo + e2); n_ref = idx; n_abs = false; }
+                        }
+                        q = e2;
+                    }
+                    broke = brk != 0;
+                    return q;
+                };
                 if (huge) p = hops((int64_t)p);
-                else p = hops((int32_t)p);
+                else p = hops32((int32_t)p);
                 KVR_STAMP(1);
                 // pool slots of the batch (one run: a fresh chunk holds any tile's rest)
                 if (nb > chunk_left) {
