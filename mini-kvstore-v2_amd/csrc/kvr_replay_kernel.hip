@@ -760,7 +760,9 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     const int32_t remT = (int32_t)rem, vhiT = (int32_t)vhi_r;
                     uint32_t brk = 0;
 #pragma unroll 1
-                    while (q < vhiT && nb < 64u) {
+                    for (;;) {
+                        // (conditions combined as integers: one branch, no lane-mask arithmetic)
+                        if (((uint32_t)(q >= vhiT) | (uint32_t)(nb >= 64u)) != 0u) break;
                         uint32_t op, klen;
                         if (q + 8 <= TILE) {
                             const uint64_t x = tu64((int)q);
@@ -774,15 +776,17 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                         my_op = wl32(my_op, op, nb);
                         my_klen = wl32(my_klen, klen, nb);
                         ++nb;
-                        if (op > 1u || remT - q < 5 || klen > (uint32_t)(remT - q - 5)) { brk = 1; break; }
+                        const uint32_t room = (uint32_t)(remT - q);   // >= 0: q < vhi <= rem
+                        if (((uint32_t)(op > 1u) | (uint32_t)(room < 5u) | (uint32_t)(klen > room - 5u)) != 0u) { brk = 1; break; }
                         kmx = klen > kmx ? klen : kmx;
                         const int32_t e = q + 5 + (int32_t)klen;
                         if (op == 1u) { q = e; continue; }
-                        if (remT - e < 4) { brk = 1; break; }
+                        const uint32_t vroom = (uint32_t)(remT - e);
+                        if (vroom < 4u) { brk = 1; break; }
                         const uint32_t vlen = e + 8 <= TILE ? (uint32_t)tu64((int)e) : uni32(ts.u32(e));
                         my_vlen = wl32(my_vlen, vlen, nb - 1u);
                         const int32_t vb = e + 4;
-                        if (vlen > (uint32_t)(remT - vb)) { brk = 1; break; }
+                        if (vlen > vroom - 4u) { brk = 1; break; }
                         const int32_t e2 = vb + (int32_t)vlen;
                         if (vlen > (uint32_t)SMALL && (vb >> SC_LOG) != ((e2 - 1) >> SC_LOG)) {
                             const uint32_t idx = nrec + nb - 1;
