@@ -38,13 +38,13 @@ PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CONFIGS = {
     # name: (segments per GPU, segment bytes, spec kwargs, description)
     "cfg2": (64, 64 << 20, dict(val_min=1024, val_max=1024, key_space_log2=20),
-             "64 x 64 MiB segments, 1 KiB values, uniform keys over 2^20, 0% DEL"),
+             "{n} x 64 MiB segments, 1 KiB values, uniform keys over 2^20, 0% DEL"),
     "cfg3": (8, 1 << 30, dict(val_min=65536, val_max=65536, key_space_log2=20),
-             "8 x 1 GiB segments, 64 KiB values (volume-server blob shape)"),
+             "{n} x 1 GiB segments, 64 KiB values (volume-server blob shape)"),
     "cfg4": (64, 64 << 20, dict(val_min=1024, val_max=1024, key_space_log2=20, del_permille=500),
-             "64 x 64 MiB segments per GPU (512 over 8 GPUs), 1 KiB values, 50% DEL"),
+             "{n} x 64 MiB segments per GPU (512 over 8 GPUs at 64), 1 KiB values, 50% DEL"),
     "cfg5": (64, 512 << 20, dict(val_min=16, val_max=1 << 20, key_space_log2=24, key_dist=1, del_permille=100),
-             "64 x 512 MiB segments per GPU (256 GiB over 8), Zipf-like keys over 2^24, 16 B-1 MiB values, 10% DEL"),
+             "{n} x 512 MiB segments per GPU (256 GiB over 8 GPUs at 64), Zipf-like keys over 2^24, 16 B-1 MiB values, 10% DEL"),
 }
 
 
@@ -93,6 +93,7 @@ def main():
     nseg, seg_bytes, kw, desc = CONFIGS[args.config]
     if args.segments:
         nseg = args.segments
+    desc = desc.format(n=nseg)   # the workload label names the segments actually replayed
     spec = K.GenSpec(seed=0x6B767265706C6179 + int(args.config[3:]), seg_bytes=seg_bytes, **kw)
     ctx = K.Context(local)
 

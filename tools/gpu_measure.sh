@@ -15,17 +15,17 @@ export TMPDIR=/tmp
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread --durations=15 \
         > "$OUT/tests.log" 2>&1 || { echo "tests failed"; tail -40 "$OUT/tests.log"; exit 1; }
       tail -3 "$OUT/tests.log" ;;
     bench)
       timeout -k 10 300 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; tail -20 "$OUT/bench.err"; exit 1; }
       cat "$OUT/bench.json" ;;
     bench3)
-      timeout -k 10 300 python -u bench.py --config cfg3 --no-cpu > "$OUT/bench_cfg3.json" 2> "$OUT/bench_cfg3.err" || { echo "bench cfg3 failed"; tail -20 "$OUT/bench_cfg3.err"; exit 1; }
+      timeout -k 10 300 python -u bench.py --config cfg3 --no-cpu --no-open > "$OUT/bench_cfg3.json" 2> "$OUT/bench_cfg3.err" || { echo "bench cfg3 failed"; tail -20 "$OUT/bench_cfg3.err"; exit 1; }
       cat "$OUT/bench_cfg3.json" ;;
     bench5)
-      timeout -k 10 300 python -u bench.py --config cfg5 --segments 16 --no-cpu > "$OUT/bench_cfg5.json" 2> "$OUT/bench_cfg5.err" || { echo "bench cfg5 failed"; tail -20 "$OUT/bench_cfg5.err"; exit 1; }
+      timeout -k 10 400 python -u bench.py --config cfg5 --no-cpu --no-open > "$OUT/bench_cfg5.json" 2> "$OUT/bench_cfg5.err" || { echo "bench cfg5 failed"; tail -20 "$OUT/bench_cfg5.err"; exit 1; }
       cat "$OUT/bench_cfg5.json" ;;
     etag)
       timeout -k 10 300 python -u bench.py --mode etag > "$OUT/bench_etag.json" 2> "$OUT/bench_etag.err" || { echo "bench etag failed"; tail -20 "$OUT/bench_etag.err"; exit 1; }
@@ -36,7 +36,7 @@ for s in $STEPS; do
       find "$OUT/profe" -name '*kernel_stats.csv' -exec cat {} \; ;;
     prof)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-        python "$R/bench.py" --no-cpu --no-stream > "$OUT/prof.log" 2>&1) || { echo "rocprof failed"; tail -20 "$OUT/prof.log"; exit 1; }
+        python "$R/bench.py" --no-cpu --no-stream --no-open > "$OUT/prof.log" 2>&1) || { echo "rocprof failed"; tail -20 "$OUT/prof.log"; exit 1; }
       find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \; ;;
     profc)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profc" -o run -- \
