@@ -144,6 +144,10 @@ int  kvr_last_stats(const kvr_ctx *ctx, kvr_stats *out);
  * required count.  flags: KVR_SEGS_ON_DEVICE, KVR_OUT_ON_DEVICE. */
 int  kvr_replay_live(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint32_t flags,
                      kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err);
+/* The same with every key's last record kept, a DEL included (the per-GPU reduction of a sharded
+ * store: kvr_replay_live_multi).  In (segment, offset) order; arguments as kvr_replay_live. */
+int  kvr_replay_last(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint32_t flags,
+                     kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err);
 
 /* ---- the open-time index on the device (engine.rs:24-76, index.rs:5-7) ---------------------
  * kvr_replay_index = kvr_replay_live plus a hash table over the live keys built in HBM, so the
@@ -270,6 +274,12 @@ int  kvr_replay_multi(kvr_mctx *m, const kvr_segment *segs, size_t n_segs, uint3
                       const uint32_t *expected_crc, size_t n_expected,
                       kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err);
 int  kvr_last_multi_stats(const kvr_mctx *m, kvr_multi_stats *out);
+/* kvr_replay_live over several GPUs: each GPU reduces its shard to every key's
+ * last record, tombstones included (a DEL on one GPU may delete a key another GPU SET), only
+ * those come back, and the host keeps each key's last record over all shards if it is a SET —
+ * exactly kvr_replay_live's output for the whole store.  Keys are compared in segs[] (host). */
+int  kvr_replay_live_multi(kvr_mctx *m, const kvr_segment *segs, size_t n_segs, uint32_t flags,
+                           kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err);
 
 /* Host helpers. */
 const char *kvr_strerror(int code);

@@ -783,13 +783,15 @@ again:
 }
 
 // live flags (and, for a rewrite, record sizes) of the tuples from the fold table
-static hipError_t live_flags(kvr_ctx *c, size_t nt, bool sizes) {
+// (keep_del: the last record of every key, tombstones included)
+static hipError_t live_flags(kvr_ctx *c, size_t nt, bool sizes, bool keep_del = false) {
     hipStream_t st = c->stream;
     hipError_t e = hipMemsetAsync(c->cflag.p, 0, nt * 4, st);
     if (e == hipSuccess && sizes) e = hipMemsetAsync(c->csize.p, 0, nt * 8, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_live_ent, dim3((uint32_t)((c->fold_slots + 255) / 256)), dim3(256), 0, st, c->fent.p,
-                       (uint64_t)c->fold_slots, c->ctup.p, sizes ? c->csize.p : nullptr, c->cflag.p);
+                       (uint64_t)c->fold_slots, c->ctup.p, sizes ? c->csize.p : nullptr, c->cflag.p,
+                       keep_del ? 1u : 0u);
     return hipGetLastError();
 }
 

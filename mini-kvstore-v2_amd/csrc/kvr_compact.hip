@@ -253,15 +253,17 @@ __device__ __forceinline__ bool is_last(const FoldEnt *ent, const uint32_t *slot
 // live flags and output sizes, from the table's side: one thread per entry; a claimed entry's
 // last tuple is live iff it is a SET (flag and size must be zero beforehand).  Reads the table once (the
 // claimed entries' last tuples at random) instead of every tuple and its entry.
+// (keep_del: every key's last record, a DEL included — the per-GPU reduction of a sharded store,
+// whose tombstones may delete a key another GPU SET)
 __global__ void k_live_ent(const FoldEnt *__restrict__ ent, uint64_t n_slots, const kvr_tuple *__restrict__ tup,
-                           uint64_t *__restrict__ size, uint32_t *__restrict__ flag) {
+                           uint64_t *__restrict__ size, uint32_t *__restrict__ flag, uint32_t keep_del) {
     const uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= n_slots) return;
     const uint4 a = reinterpret_cast<const uint4 *>(&ent[h])[0];
     if (a.x == 0xFFFFFFFFu && a.y == 0xFFFFFFFFu) return;   // free
     const uint32_t j = ~a.z;
     const kvr_tuple t = tup[j];
-    if (t.op != 0) return;
+    if (t.op != 0 && !keep_del) return;
     flag[j] = 1u;
     if (size) size[j] = 9ull + t.key_len + t.val_len;   // SET framing, engine.rs:169-173
 }

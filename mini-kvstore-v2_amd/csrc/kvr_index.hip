@@ -67,12 +67,13 @@ uint64_t index_slots(uint64_t n_live) {
 }
 
 // after compact_front: live flags, their scan and the dense live list in c->lout; *total = n_live
-int live_list(kvr_ctx *c, size_t nt, uint64_t *total) {
+// (keep_del: every key's last record instead, tombstones included)
+int live_list(kvr_ctx *c, size_t nt, uint64_t *total, bool keep_del = false) {
     *total = 0;
     if (nt == 0) return KVR_OK;
     hipStream_t st = c->stream;
     const uint32_t g = (uint32_t)((nt + 255) / 256);
-    HIPCHK(live_flags(c, nt, false));
+    HIPCHK(live_flags(c, nt, false, keep_del));
     size_t tb = c->ctmp.n;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->cflag.p, c->cpos.p, (int)nt, st));
     uint32_t last[2] = {0, 0};
@@ -98,10 +99,9 @@ int index_copy_out(kvr_ctx *c, uint32_t flags, kvr_tuple *live, size_t live_cap,
 }
 }  // namespace
 
-extern "C" {
-
-int kvr_replay_live(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, kvr_tuple *out, size_t cap,
-                    size_t *n_out, kvr_error *err) {
+namespace {
+int replay_last(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, kvr_tuple *out, size_t cap,
+                       size_t *n_out, kvr_error *err, bool keep_del) {
     if (!c || (!segs && n) || !n_out || (cap && !out)) return KVR_EINVAL;
     if (flags & ~(KVR_SEGS_ON_DEVICE | KVR_OUT_ON_DEVICE)) return KVR_EINVAL;
     *n_out = 0;
@@ -111,7 +111,7 @@ int kvr_replay_live(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flag
     int rc = compact_front(c, segs, n, flags, err, &nt, false, &cs);   // replay + fold (kvr_compact.hip)
     if (rc != KVR_OK) return rc;
     uint64_t total = 0;
-    rc = live_list(c, nt, &total);
+    rc = live_list(c, nt, &total, keep_del);
     if (rc != KVR_OK) return rc;
     *n_out = total;
     c->ix_live = total;   // kvr_live_keys reads this live list
@@ -123,6 +123,19 @@ int kvr_replay_live(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flag
     HIPCHK(hipMemcpyAsync(out, c->lout.p, total * sizeof(kvr_tuple), k, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return KVR_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int kvr_replay_live(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, kvr_tuple *out, size_t cap,
+                    size_t *n_out, kvr_error *err) {
+    return replay_last(c, segs, n, flags, out, cap, n_out, err, false);
+}
+
+int kvr_replay_last(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, kvr_tuple *out, size_t cap,
+                    size_t *n_out, kvr_error *err) {
+    return replay_last(c, segs, n, flags, out, cap, n_out, err, true);
 }
 
 uint64_t kvr_index_slots(uint64_t n_live) { return index_slots(n_live); }
@@ -237,6 +250,8 @@ int kvr_ingest_begin(kvr_ctx *c, uint64_t total_bytes, size_t n_segs) {
     c->ing_segs.clear();
     HIPCHK(hipSetDevice(c->device));
     if (c->copy) HIPCHK(hipStreamSynchronize(c->copy));   // no copy of an earlier ingest in flight
+    const char *lim = getenv("KVR_INGEST_LIMIT");         // test knob: a smaller HBM budget
+    if (lim && total_bytes > strtoull(lim, nullptr, 10)) return KVR_ENOMEM;
     if (c->ing.ensure(total_bytes + 256 * ((uint64_t)n_segs + 1))) return KVR_ENOMEM;
     c->ing_segs.reserve(n_segs);
     if (!c->copy) {

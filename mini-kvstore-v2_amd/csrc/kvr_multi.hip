@@ -14,6 +14,52 @@
  */
 #include <thread>
 
+// key bytes of tuple t in the caller's host segments ([op][klen u32][key], engine.rs:169-171)
+static inline const uint8_t *mkey(const kvr_segment *segs, const kvr_tuple &t) {
+    return segs[t.seg_idx].bytes + t.rec_off + 5;
+}
+
+// the last record of each key over t[0, n) (in (segment, offset) order, keys read from host
+// segments): live[i] = 1 iff t[i] is its key's last record and a SET.  Keys split by tag into one
+// partition per thread; each partition keeps an open-addressing table of (tag << 32 | index).
+static void fold_last_parallel(const kvr_segment *segs, const kvr_tuple *t, size_t n, std::vector<uint8_t> &live) {
+    live.assign(n, 0);
+    if (n == 0) return;
+    const uint32_t P = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    auto part = [P](uint32_t tag) { return (uint32_t)(((uint64_t)(tag * 0x9E3779B1u) * P) >> 32); };
+    std::vector<std::vector<uint32_t>> idx(P);
+    for (size_t i = 0; i < n; ++i) idx[part(t[i].key_tag)].push_back((uint32_t)i);   // each list in order
+    std::vector<std::thread> th;
+    for (uint32_t p = 0; p < P; ++p) {
+        th.emplace_back([&, p]() {
+            const std::vector<uint32_t> &L = idx[p];
+            if (L.empty()) return;
+            uint64_t cap = 16;
+            while (cap < 2 * L.size()) cap <<= 1;
+            constexpr uint64_t EMPTY = ~0ull;
+            std::vector<uint64_t> slot(cap, EMPTY);
+            const uint64_t mask = cap - 1;
+            for (uint32_t i : L) {
+                const kvr_tuple &x = t[i];
+                const uint64_t tag = (uint64_t)x.key_tag << 32;
+                for (uint64_t h = ((uint64_t)x.key_tag * 0x9E3779B97F4A7C15ull) >> 20;; ++h) {
+                    uint64_t &sl = slot[h & mask];
+                    if (sl == EMPTY) { sl = tag | i; break; }
+                    if ((sl & 0xFFFFFFFF00000000ull) != tag) continue;
+                    const kvr_tuple &y = t[(uint32_t)sl];
+                    if (y.key_len == x.key_len && memcmp(mkey(segs, y), mkey(segs, x), x.key_len) == 0) {
+                        sl = tag | i;   // later record wins (engine.rs:137, :141)
+                        break;
+                    }
+                }
+            }
+            for (uint64_t sl : slot)
+                if (sl != EMPTY && t[(uint32_t)sl].op == 0) live[(uint32_t)sl] = 1;
+        });
+    }
+    for (auto &x : th) x.join();
+}
+
 struct kvr_mctx {
     std::vector<kvr_ctx *> c;
     kvr_multi_stats st{};
@@ -52,8 +98,26 @@ int kvr_last_multi_stats(const kvr_mctx *m, kvr_multi_stats *out) {
     return KVR_OK;
 }
 
+static int replay_multi(kvr_mctx *m, const kvr_segment *segs, size_t n, uint32_t flags, const uint32_t *expected,
+                        size_t n_expected, kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err, bool last);
+
 int kvr_replay_multi(kvr_mctx *m, const kvr_segment *segs, size_t n, uint32_t flags, const uint32_t *expected,
                      size_t n_expected, kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err) {
+    return replay_multi(m, segs, n, flags, expected, n_expected, out, cap, n_out, err, false);
+}
+
+int kvr_replay_live_multi(kvr_mctx *m, const kvr_segment *segs, size_t n, uint32_t flags, kvr_tuple *out, size_t cap,
+                          size_t *n_out, kvr_error *err) {
+    return replay_multi(m, segs, n, flags, nullptr, 0, out, cap, n_out, err, true);
+}
+
+}  // extern "C"
+
+// last: each shard reduces its tuples to every key's last record, tombstones included
+// (kvr_replay_last: a DEL on one GPU may delete a key another GPU SET); the host
+// merges the shards in (segment, offset) order and keeps each key's last record if it is a SET
+static int replay_multi(kvr_mctx *m, const kvr_segment *segs, size_t n, uint32_t flags, const uint32_t *expected,
+                        size_t n_expected, kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err, bool last) {
     if (!m || m->c.empty() || (!segs && n) || !n_out || (cap && !out)) return KVR_EINVAL;
     if (flags & (KVR_SEGS_ON_DEVICE | KVR_OUT_ON_DEVICE | KVR_EXPECTED_ON_DEVICE)) return KVR_EINVAL;   // host in, host out
     if (err) memset(err, 0, sizeof(*err));
@@ -84,11 +148,15 @@ int kvr_replay_multi(kvr_mctx *m, const kvr_segment *segs, size_t n, uint32_t fl
             for (const kvr_segment &s : sh[r]) bytes += s.len;
             size_t c = (size_t)(bytes / 256) + 4096 + sh[r].size();
             tv[r].resize(c);
-            int x = kvr_replay(m->c[r], sh[r].data(), sh[r].size(), 0, nullptr, 0, tv[r].data(), c, &nn[r], &er[r]);
+            auto run = [&](size_t cc) {
+                return last ? kvr_replay_last(m->c[r], sh[r].data(), sh[r].size(), 0, tv[r].data(), cc, &nn[r], &er[r])
+                            : kvr_replay(m->c[r], sh[r].data(), sh[r].size(), 0, nullptr, 0, tv[r].data(), cc, &nn[r], &er[r]);
+            };
+            int x = run(c);
             if (x == KVR_CAPACITY) {   // rare: denser than one record per 256 B; replay again into the exact size
                 c = nn[r];
                 tv[r].resize(c);
-                x = kvr_replay(m->c[r], sh[r].data(), sh[r].size(), 0, nullptr, 0, tv[r].data(), c, &nn[r], &er[r]);
+                x = run(c);
             }
             kvr_stats s;
             kvr_last_stats(m->c[r], &s);
@@ -122,6 +190,33 @@ int kvr_replay_multi(kvr_mctx *m, const kvr_segment *segs, size_t n, uint32_t fl
     std::vector<size_t> pos(N, 0);
     size_t o = 0;
     uint64_t fails = 0;
+    if (last) {   // every shard's key-last records, merged, then the last record of each key overall
+        size_t tot = 0;
+        for (size_t r = 0; r < N; ++r) tot += nn[r];
+        std::vector<kvr_tuple> mt;
+        mt.reserve(tot);
+        for (size_t i = 0; i < n; ++i) {
+            const size_t r = i % N;
+            const uint32_t j = (uint32_t)(i / N);
+            size_t &p = pos[r];
+            while (p < nn[r] && tv[r][p].seg_idx == j) {
+                kvr_tuple x = tv[r][p++];
+                x.seg_idx = (uint32_t)i;
+                mt.push_back(x);
+            }
+        }
+        std::vector<uint8_t> live;
+        fold_last_parallel(segs, mt.data(), mt.size(), live);
+        for (size_t i = 0; i < mt.size(); ++i) {
+            if (!live[i]) continue;
+            if (o < cap) out[o] = mt[i];
+            ++o;
+        }
+        *n_out = o;
+        m->st.n_records = o;
+        m->st.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return o > cap ? KVR_CAPACITY : KVR_OK;
+    }
     for (size_t i = 0; i < n; ++i) {
         const size_t r = i % N;
         const uint32_t j = (uint32_t)(i / N);
@@ -144,5 +239,3 @@ int kvr_replay_multi(kvr_mctx *m, const kvr_segment *segs, size_t n, uint32_t fl
     m->st.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return o > cap ? KVR_CAPACITY : KVR_OK;
 }
-
-}  // extern "C"

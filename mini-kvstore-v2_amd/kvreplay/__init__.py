@@ -138,6 +138,8 @@ def _load():
     rep.kvr_mctx_destroy.restype = None
     rep.kvr_mctx_size.argtypes = [P]
     rep.kvr_replay_multi.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
+    rep.kvr_replay_live_multi.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
+    rep.kvr_replay_last.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
     rep.kvr_last_multi_stats.argtypes = [P, C.POINTER(MultiStats)]
     rep.kvr_replay_stream.argtypes = [P, C.POINTER(Segment), SZ, U32, U64, P, SZ, P, SZ, C.POINTER(SZ),
                                       C.POINTER(Error)]
@@ -382,9 +384,10 @@ class MultiContext:
         self._rep.kvr_last_multi_stats(self.h, C.byref(s))
         return s
 
-    def replay(self, segments, seg_ids=None, expected=None, cap=None):
+    def replay(self, segments, seg_ids=None, expected=None, cap=None, live=False):
         """Same contract as Context.replay over host segments; returns ReplayResult (stats:
-        MultiStats)."""
+        MultiStats).  live=True: kvr_replay_live_multi (each GPU reduces its shard to every key's
+        last record, tombstones included; the host keeps the live keys' final SETs)."""
         keep = []
         n = len(segments)
         segs = (Segment * max(n, 1))()
@@ -404,10 +407,14 @@ class MultiContext:
         out_arr = np.zeros(max(cap, 1), dtype=TUPLE_DTYPE)
         n_out = C.c_size_t()
         err = Error()
-        rc = self._rep.kvr_replay_multi(self.h, segs, n, 0, exp_ptr, n_exp, out_arr.ctypes.data, cap, C.byref(n_out),
-                                        C.byref(err))
+        if live:
+            rc = self._rep.kvr_replay_live_multi(self.h, segs, n, 0, out_arr.ctypes.data, cap, C.byref(n_out),
+                                                 C.byref(err))
+        else:
+            rc = self._rep.kvr_replay_multi(self.h, segs, n, 0, exp_ptr, n_exp, out_arr.ctypes.data, cap,
+                                            C.byref(n_out), C.byref(err))
         if rc == CAPACITY:
-            return self.replay(segments, seg_ids, expected, cap=n_out.value + 16)
+            return self.replay(segments, seg_ids, expected, cap=n_out.value + 16, live=live)
         if rc < 0:
             raise NativeError(f"kvr_replay_multi: {self._rep.kvr_strerror(rc).decode()} ({rc})")
         tuples = out_arr[: n_out.value] if rc == OK else None

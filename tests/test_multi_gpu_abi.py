@@ -68,3 +68,25 @@ def test_multi_empty_and_capacity():
         assert r.status == rc == 0 and np.array_equal(r.tuples, ref)
     finally:
         mc.close()
+
+
+@pytest.mark.parametrize("n_ctx", [2, 3])
+def test_live_multi_matches_oracle_fold(n_ctx):
+    """kvr_replay_live_multi: per-GPU reduction to every key's last record (tombstones kept: a DEL
+    in one shard deletes a key SET in another), host merge by (segment, offset) -> exactly the
+    oracle's live map of the whole store."""
+    spec = K.GenSpec(seed=104, seg_bytes=400_000, key_space_log2=9, val_min=0, val_max=200, del_permille=350)
+    segs = [K.gen_segment_cpu(spec, s)[0] for s in range(7)]
+    ids = [2, 3, 5, 8, 13, 21, 34]
+    rc, t, _ = O.replay(segs, seg_ids=ids)
+    live, nk, tb = O.fold_live(segs, t)
+    m = K.MultiContext([0] * n_ctx)
+    try:
+        r = m.replay(segs, seg_ids=ids, live=True)
+        assert r.status == 0 and r.n == nk and np.array_equal(r.tuples, t[live])
+        bad = segs[:4] + [segs[4][:-3]] + segs[5:]
+        rc2, _, err = O.replay(bad, seg_ids=ids)
+        r = m.replay(bad, seg_ids=ids, live=True)
+        assert r.status == 1 and (r.error.kind, r.error.seg_idx, r.error.rec_off) == (err.kind, err.seg_idx, err.rec_off)
+    finally:
+        m.close()

@@ -375,3 +375,26 @@ def test_replay_batches_past_pool_limit(gctx, monkeypatch):
     assert r.status == 0 and r.n == len(want)
     got = out[: len(want) * 32].cpu().numpy().view(K.TUPLE_DTYPE)
     assert np.array_equal(got["seg_idx"], want["seg_idx"]) and np.array_equal(got["rec_off"], want["rec_off"])
+
+
+@pytest.mark.gpu
+def test_kvs_open_falls_back_when_hbm_is_short(gctx, tmp_path, monkeypatch):
+    """kvr_ingest_begin answering KVR_ENOMEM (the store does not fit the HBM budget, lowered here
+    by KVR_INGEST_LIMIT) switches kvs_open to the batched replay + host fold, with the same index."""
+    spec = K.GenSpec(seed=103, seg_bytes=500_000, key_space_log2=11, val_min=0, val_max=300, del_permille=250)
+    segs = [K.gen_segment_cpu(spec, s)[0] for s in range(5)]
+    ids = [1, 2, 3, 4, 5]
+    d = tmp_path / "db"
+    _write_store(d, segs, ids)
+    want, nk, tb = expect(segs, ids)
+    monkeypatch.setenv("KVR_INGEST_LIMIT", "100000")
+    s = K.KVStore.open(str(d), gctx)
+    assert s.open_stats().path == K.PATH_HOST_FOLD
+    assert (s.stats().num_keys, s.stats().total_bytes) == (nk, tb)
+    for t, k in list(zip(want, keys_of(segs, want)))[::7]:
+        assert s.locate(k) == (ids[t["seg_idx"]], t["rec_off"] + 9 + t["key_len"], t["val_len"])
+    s.close()
+    monkeypatch.delenv("KVR_INGEST_LIMIT")
+    s = K.KVStore.open(str(d), gctx)
+    assert s.open_stats().path == K.PATH_DEVICE_INDEX and s.stats().num_keys == nk
+    s.close()
