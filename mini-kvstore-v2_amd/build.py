@@ -100,6 +100,8 @@ VARIANTS = {
     "v9a3": ["-DKVR_KERNEL_V9", "-DKVR_ABLATE=3"],
     "v9a64": ["-DKVR_KERNEL_V9", "-DKVR_ABLATE=64"],
     "v8": ["-DKVR_KERNEL_V8"],
+    "prio0": ["-DKVR_HOP_PRIO=0", "-DKVR_REC_PRIO=0"],
+    "bulklow": ["-DKVR_BULK_LOWPRIO=1"],
 }
 
 

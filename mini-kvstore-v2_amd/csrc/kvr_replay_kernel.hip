@@ -72,6 +72,18 @@ struct __align__(16) Smem {
     uint32_t C2[2 * 256 * 32];            // lane-replicated slice-by-2 byte tables (64 KiB)
 };
 
+// wave priority (s_setprio) of the serial phases: the hop chain and the records phase are the
+// tile's critical path and share the CU's scalar unit with 15 other waves, so they issue ahead
+// of waves in their bulk CRC (cfg2: 1.90 -> 1.77 ms; cfg3 / cfg5 unchanged)
+#ifndef KVR_HOP_PRIO
+#define KVR_HOP_PRIO 2
+#endif
+#ifndef KVR_REC_PRIO
+#define KVR_REC_PRIO 1
+#endif
+#ifndef KVR_BULK_LOWPRIO   // experiment: every phase raised except the unit CRC loop
+#define KVR_BULK_LOWPRIO 0
+#endif
 #ifndef KVR_ABLATE
 #define KVR_ABLATE 0   // diagnostic builds only: 1 skip records, 2 skip value CRC, 4 skip hops,
 #endif                 // 8 skip the unit loop, 16 skip scan + finalize, 32 skip long-value folding,
@@ -564,6 +576,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     unsigned long long t_last = __builtin_amdgcn_s_memtime();
     unsigned long long prof_acc[16] = {};
 #endif
+    if (KVR_BULK_LOWPRIO) __builtin_amdgcn_s_setprio(2);
     for (;; ++k) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         KVR_STAMP(5);
@@ -799,8 +812,12 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     broke = brk != 0;
                     return q;
                 };
+                // the hop chain is the tile's serial critical path and shares the CU's scalar unit
+                // with 15 other waves: it issues at raised priority (KVR_HOP_PRIO)
+                if (KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
                 if (huge) p = hops((int64_t)p);
                 else p = hops32((int32_t)p);
+                if (KVR_HOP_PRIO && !KVR_REC_PRIO) __builtin_amdgcn_s_setprio(KVR_BULK_LOWPRIO ? 2 : 0);
                 KVR_STAMP(1);
                 // pool slots of the batch (one run: a fresh chunk holds any tile's rest)
                 if (nb > chunk_left) {
@@ -886,6 +903,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     err_pos = (uint64_t)(lo + (int64_t)(int32_t)rl32((uint32_t)myrec, el));
                 }
                 nrec = err_rec != N32 ? err_rec : nrec + nb;
+                if (KVR_REC_PRIO) __builtin_amdgcn_s_setprio(KVR_BULK_LOWPRIO ? 2 : 0);   // (records raised too)
                 KVR_STAMP(7);
             }
             tile_exit = broke ? ERRP : (uint64_t)(lo + p);
@@ -901,6 +919,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         // ---- C. CRC of long values --------------------------------------------------------
         if (!(KVR_ABLATE & 2) && any_long) {
             KVR_STAMP(8);
+            if (KVR_BULK_LOWPRIO) __builtin_amdgcn_s_setprio(0);
             // the unit's two halves, words 0..15 (A) and 16..31 (B), CRC'd as independent chains
             // from a zero register, with the snapshot of the raw CRC of the unit's first 4 qm
             // bytes (the value ending here) and the restart at the value starting here (a)
@@ -933,6 +952,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             // the piece of the value crossing the unit end: A pushed through B's bytes, then B
             // (A does not count when that value starts in B's half); the raw CRC of the first
             // 4 qm bytes: A's snapshot, or all of A pushed through 4 (qm - H) bytes, then B's
+            if (KVR_BULK_LOWPRIO) __builtin_amdgcn_s_setprio(2);
             const uint32_t pa = kmul(ca, S.KQ + 128 * H);
             const uint32_t ps = kmul(ca, S.KQ + 128 * (qm > H ? qm - H : 0));
             const uint32_t c = qa >= H ? cb : (pa ^ cb);
