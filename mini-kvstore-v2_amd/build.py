@@ -100,8 +100,10 @@ VARIANTS = {
     "v9a3": ["-DKVR_KERNEL_V9", "-DKVR_ABLATE=3"],
     "v9a64": ["-DKVR_KERNEL_V9", "-DKVR_ABLATE=64"],
     "v8": ["-DKVR_KERNEL_V8"],
-    "prio0": ["-DKVR_HOP_PRIO=0", "-DKVR_REC_PRIO=0"],
+    "prio0": ["-DKVR_HOP_PRIO=0", "-DKVR_REC_PRIO=0"],   # wave priority off
     "bulklow": ["-DKVR_BULK_LOWPRIO=1"],
+    "fin1": ["-DKVR_FIN_PRIO=1"],
+    "base": [],
 }
 
 

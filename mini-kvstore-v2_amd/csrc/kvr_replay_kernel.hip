@@ -81,6 +81,9 @@ struct __align__(16) Smem {
 #ifndef KVR_REC_PRIO
 #define KVR_REC_PRIO 1
 #endif
+#ifndef KVR_FIN_PRIO       // experiment: the scan + finalize chain raised too
+#define KVR_FIN_PRIO 0
+#endif
 #ifndef KVR_BULK_LOWPRIO   // experiment: every phase raised except the unit CRC loop
 #define KVR_BULK_LOWPRIO 0
 #endif
@@ -953,6 +956,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             // (A does not count when that value starts in B's half); the raw CRC of the first
             // 4 qm bytes: A's snapshot, or all of A pushed through 4 (qm - H) bytes, then B's
             if (KVR_BULK_LOWPRIO) __builtin_amdgcn_s_setprio(2);
+            if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(KVR_FIN_PRIO);
             const uint32_t pa = kmul(ca, S.KQ + 128 * H);
             const uint32_t ps = kmul(ca, S.KQ + 128 * (qm > H ? qm - H : 0));
             const uint32_t c = qa >= H ? cb : (pa ^ cb);
@@ -1016,6 +1020,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             }
         }
 
+        if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(0);
         // the tile's registers are dead from here on: the next tile's load overlaps the rest
         if (err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry)) {
             load_unit(abase, d0, len, k + 1, lane, w);
