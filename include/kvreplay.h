@@ -335,7 +335,9 @@ int  kvr_last_compact_stats(const kvr_ctx *ctx, kvr_compact_stats *out);
  *                        a record is live iff it is a SET, its key's local last and the winner;
  *                        the live records are written out exactly as kvr_compact does.
  * Every rank's output is disjoint from the others' (one live record per key in the whole store);
- * together they replay to the pre-compaction map. */
+ * together they replay to the pre-compaction map.  The staged state shares the context's fold
+ * buffers: a kvr_compact / kvr_replay_live / kvr_replay_last / kvr_replay_index call on the same
+ * context in between ends it (kvr_compact_export / _finish then return KVR_EINVAL). */
 typedef struct kvr_cand {
     uint64_t pos;       /* (global segment index << 40) | rec_off                                */
     uint32_t key_len;

@@ -398,3 +398,19 @@ def test_kvs_open_falls_back_when_hbm_is_short(gctx, tmp_path, monkeypatch):
     s = K.KVStore.open(str(d), gctx)
     assert s.open_stats().path == K.PATH_DEVICE_INDEX and s.stats().num_keys == nk
     s.close()
+
+
+@pytest.mark.gpu
+def test_live_replay_ends_a_staged_compaction(gctx):
+    """kvr_compact_stage's state shares the fold buffers: a live replay on the same context in
+    between ends it, and export then answers KVR_EINVAL instead of exporting stale candidates."""
+    torch = pytest.importorskip("torch")
+    spec = K.GenSpec(seed=105, seg_bytes=200_000, key_space_log2=9, val_min=0, val_max=100, del_permille=200)
+    segs = [K.gen_segment_cpu(spec, s)[0] for s in range(3)]
+    counts, kb = gctx.compact_stage(segs, [0, 1, 2], 1)
+    hdr = torch.zeros(int(counts.sum()) * K.CAND_BYTES + 64, dtype=torch.uint8, device="cuda")
+    keys = torch.zeros(int(kb.sum()) + 64, dtype=torch.uint8, device="cuda")
+    gctx.compact_export(hdr.data_ptr(), keys.data_ptr())   # staged: fine
+    gctx.replay_live(segs)
+    with pytest.raises(K.NativeError, match="-1"):
+        gctx.compact_export(hdr.data_ptr(), keys.data_ptr())
