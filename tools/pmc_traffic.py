@@ -54,7 +54,7 @@ def calibrate():
 
 
 def main():
-    args = sys.argv[1:] or ["--steps", "2", "--warmup", "1", "--no-cpu", "--no-stream"]
+    args = sys.argv[1:] or ["--steps", "2", "--warmup", "1", "--no-cpu", "--no-stream", "--no-open"]
     factor, calib_kib, calib_bytes = calibrate()
     fetch_kib, nf = run_pass("FETCH_SIZE", args)
     write_kib, nw = run_pass("WRITE_SIZE", args)
