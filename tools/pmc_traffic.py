@@ -17,10 +17,12 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "mini-kvstore-v2_amd", "lib", "libkvreplay.so")
-OUT = os.path.join(ROOT, "gpurun_out", "pmc_traffic")
+# every run keeps its own rocprofv3 output and logs (a failed pass's cause survives later runs)
+OUT = os.path.join(ROOT, "gpurun_out", "pmc_traffic", time.strftime("%Y%m%d-%H%M%S"))
 
 
 def lib_hash():
@@ -68,6 +70,7 @@ def main():
                          "loads-only build over a known byte count), WRITE_SIZE KiB x1024"}
     res["hbm_bytes"] = res["hbm_read_bytes"] + res["hbm_write_bytes"]
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    res["run_dir"] = os.path.relpath(OUT, ROOT)
     with open(os.path.join(ROOT, "gpurun_out", "pmc_traffic.json"), "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
