@@ -69,7 +69,7 @@ struct __align__(16) Smem {
     uint32_t KT[4 * 8 * 16];              // [j][i][n]: (n << 4i) * x^(8*SC*2^j), j < 4
     uint32_t KQ[NQ * 8 * 16];             // [q][i][n]: (n << 4i) * x^(8*4q), q <= SC/4
     uint32_t IX[NIX + 3];                 // 0xFFFFFFFF * x^(8j): initial register pushed through j bytes
-    uint32_t C2[2 * 256 * 32];            // lane-replicated slice-by-2 byte tables (64 KiB)
+    uint32_t C2[256 * 64];                // byte tables, row b = 256 B (64 KiB), see Crc
 };
 
 // wave priority (s_setprio) of the serial phases: the hop chain and the records phase are the
@@ -131,9 +131,22 @@ __device__ __forceinline__ uint32_t dpp(uint32_t v) {
 // ---------------------------------------------------------------------------------------
 // CRC primitives
 // ---------------------------------------------------------------------------------------
+// Row b of Smem::C2 (64 dwords):
+//   [0, 32):  dword 8 t + r = table t (t = 0: one byte, t = k: a byte then k zero bytes) for byte
+//             b, replica r < 8 -- the slice-by-4 set of the unit loop
+//   [32, 48): table 0, replica lane & 15;  [48, 64): table 1, replica lane & 15 (slice-by-2 set)
+// A slice-by-4 step x = c ^ w needs T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3].  Lane group
+// g = (lane >> 3) & 3 takes table (g + i) & 3 in its i-th lookup and replica lane & 7, so the 32
+// lanes of a half-wave hit 32 distinct banks in every lookup; the group's byte order is absorbed
+// by rotating x left by 8 g first (one v_alignbit), which keeps the four selectors uniform.
+#ifndef KVR_S4
+#define KVR_S4 1
+#endif
 struct Crc {
-    const uint8_t *t;   // the lane-replicated slice-by-2 tables (Smem::C2)
-    uint32_t L;         // byte 0: 4 (lane & 31) (T0 copy), byte 1: 128 + 4 (lane & 31) (T1 copy)
+    const uint8_t *t;   // Smem::C2
+    uint32_t L;         // byte 0: T0 copy (128 + 4 (lane & 15)), byte 1: T1 copy (192 + 4 (lane & 15))
+    uint32_t L4;        // byte i: 4 (8 ((g + i) & 3) + (lane & 7)), this lane's i-th slice-by-4 lookup
+    uint32_t rot;       // (32 - 8 g) & 31: x rotated right by this = x rotated left by 8 g
 };
 // v_perm_b32 builds the LDS address: byte 1 = a byte of x, byte 0 = this lane's table copy
 constexpr uint32_t SEL_T1_B0 = 0x0C0C0401u, SEL_T0_B1 = 0x0C0C0500u, SEL_T0_B0 = 0x0C0C0400u;
@@ -149,8 +162,28 @@ __device__ __forceinline__ uint32_t crc2(const Crc &k, uint32_t x) {
     asm("" : "+v"(t0), "+v"(t1));
     return (x >> 16) ^ t0 ^ t1;
 }
-__device__ __forceinline__ uint32_t crc4(uint32_t c, uint32_t w, const Crc &k) { return crc2(k, crc2(k, c ^ w)); }
-// two independent chains stepped together: their four lookups share one LDS round trip
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {   // one VALU op
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));   // a ^ b ^ c
+    return r;
+}
+// lookup i of a slice-by-4 step on xr = x rotated left by 8 g: byte 1 = xr byte 3 - i, which
+// is x byte 3 - ((g + i) & 3), the byte table (g + i) & 3 takes
+__device__ __forceinline__ uint32_t s4get(const Crc &k, uint32_t xr, uint32_t i) {
+    return *reinterpret_cast<const uint32_t *>(
+        k.t + __builtin_amdgcn_perm(xr, k.L4, 0x0C0C0000u | ((7u - i) << 8) | i));
+}
+__device__ __forceinline__ uint32_t crc4(uint32_t c, uint32_t w, const Crc &k) {
+#if KVR_S4
+    const uint32_t x = c ^ w, xr = __builtin_amdgcn_alignbit(x, x, k.rot);
+    uint32_t a0 = s4get(k, xr, 0), a1 = s4get(k, xr, 1), a2 = s4get(k, xr, 2), a3 = s4get(k, xr, 3);
+    asm("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
+    return xor3(a0, a1, a2) ^ a3;
+#else
+    return crc2(k, crc2(k, c ^ w));
+#endif
+}
+// two independent chains stepped together: their lookups share one LDS round trip
 __device__ __forceinline__ void crc2x2(const Crc &k, uint32_t &xa, uint32_t &xb) {
     uint32_t a0 = tget(k, xa, SEL_T1_B0), a1 = tget(k, xa, SEL_T0_B1);
     uint32_t b0 = tget(k, xb, SEL_T1_B0), b1 = tget(k, xb, SEL_T0_B1);
@@ -159,11 +192,21 @@ __device__ __forceinline__ void crc2x2(const Crc &k, uint32_t &xa, uint32_t &xb)
     xb = (xb >> 16) ^ b0 ^ b1;
 }
 __device__ __forceinline__ void crc4x2(uint32_t &ca, uint32_t wa, uint32_t &cb, uint32_t wb, const Crc &k) {
+#if KVR_S4
+    const uint32_t xa = ca ^ wa, xb = cb ^ wb;
+    const uint32_t ra = __builtin_amdgcn_alignbit(xa, xa, k.rot), rb = __builtin_amdgcn_alignbit(xb, xb, k.rot);
+    uint32_t a0 = s4get(k, ra, 0), a1 = s4get(k, ra, 1), a2 = s4get(k, ra, 2), a3 = s4get(k, ra, 3);
+    uint32_t b0 = s4get(k, rb, 0), b1 = s4get(k, rb, 1), b2 = s4get(k, rb, 2), b3 = s4get(k, rb, 3);
+    asm("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
+    ca = xor3(a0, a1, a2) ^ a3;
+    cb = xor3(b0, b1, b2) ^ b3;
+#else
     uint32_t xa = ca ^ wa, xb = cb ^ wb;
     crc2x2(k, xa, xb);
     crc2x2(k, xa, xb);
     ca = xa;
     cb = xb;
+#endif
 }
 __device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
     const uint32_t x = c ^ b;
@@ -173,11 +216,6 @@ __device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
 // register state v times a constant K (nibble tables; every lane reads table i at once, so the
 // 16 entries sit in 16 banks and equal indices broadcast: conflict free).  The eight lookups
 // are independent: the empty asm makes the scheduler issue them all before the first use.
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {   // one VALU op
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));   // a ^ b ^ c
-    return r;
-}
 __device__ __forceinline__ uint32_t xor8(uint32_t *t) {
     asm("" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]), "+v"(t[7]));
     return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
@@ -526,7 +564,10 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                                                uint32_t pool_chunk) {
     __shared__ Smem S;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    for (int i = tid; i < 2 * 256 * 32; i += RT) S.C2[i] = tb.crc8[((i >> 5) & 1) * 256 + (i >> 6)];
+    for (int i = tid; i < 256 * 64; i += RT) {
+        const int d = i & 63, t = d < 32 ? d >> 3 : (d >> 4) - 2;
+        S.C2[i] = tb.crc8[t * 256 + (i >> 6)];
+    }
     for (int i = tid; i < 8 * 16 * 32; i += RT)
         S.KR[i] = tb.kmul[((KSET_R + (i & 31)) * 8 + (i >> 9)) * 16 + ((i >> 5) & 15)];
     for (int i = tid; i < 4 * 8 * 16; i += RT) S.KT[i] = tb.kmul[i];
@@ -534,8 +575,16 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     if (tid < NIX) S.IX[tid] = tb.initx[tid];
     __syncthreads();   // the only workgroup barrier: from here on every wave is on its own
 
-    const Crc K{reinterpret_cast<const uint8_t *>(S.C2),
-                ((uint32_t)(lane & 31) * 4u) | (((uint32_t)(lane & 31) * 4u + 128u) << 8)};
+    Crc K;
+    {
+        const uint32_t g = (uint32_t)(lane >> 3) & 3u, r = (uint32_t)lane & 7u, r16 = (uint32_t)lane & 15u;
+        K.t = reinterpret_cast<const uint8_t *>(S.C2);
+        K.L = (128u + 4u * r16) | ((192u + 4u * r16) << 8);
+        K.L4 = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) K.L4 |= (4u * (8u * ((g + i) & 3u) + r)) << (8 * i);
+        K.rot = (32u - 8u * g) & 31u;
+    }
     // the stripe index is wave-uniform: say so, so that the whole stripe state lives in SGPRs
     const uint32_t gw = blockIdx.x * WPB + (uint32_t)__builtin_amdgcn_readfirstlane(wv);
     uint32_t si;

@@ -3,7 +3,7 @@
 #   parity tests, the bench line, the rocprofv3 kernel-trace summary of the same bench command,
 #   the per-phase cycle breakdown, ablation timings and PMC counters.  Every GPU step has its
 #   own time limit and the steps are chained, so the first failure ends the batch.
-#   usage: tools/gpu_measure.sh <tag> [tests bench bench3 bench5 prof profc phases ablate traffic pmc ...]
+#   usage: tools/gpu_measure.sh <tag> [tests bench bench3 bench5 prof profc phases ablate vars traffic pmc ...]
 set -o pipefail
 TAG=${1:-run}; shift
 STEPS=${*:-tests bench prof}
@@ -61,6 +61,11 @@ for s in $STEPS; do
         timeout -k 10 120 python -u tools/ablate.py cfg2 0 $m >> "$OUT/ablate_cfg2.txt" 2>&1 || { echo "ablate failed"; tail -20 "$OUT/ablate_cfg2.txt"; exit 1; }
       done
       cat "$OUT/ablate_cfg2.txt" ;;
+    vars)     # build.py VARIANTS named in $VARS, timed one process each (cfg in $VCFG)
+      for v in ${VARS:-base}; do
+        timeout -k 10 120 python -u tools/ablate.py ${VCFG:-cfg2} 0 $v >> "$OUT/vars_${VCFG:-cfg2}.txt" 2>&1 || { echo "variant $v failed"; tail -20 "$OUT/vars_${VCFG:-cfg2}.txt"; exit 1; }
+      done
+      cat "$OUT/vars_${VCFG:-cfg2}.txt" ;;
     traffic)
       timeout -k 10 600 python -u tools/pmc_traffic.py > "$OUT/traffic.log" 2>&1 || { echo "traffic failed"; tail -20 "$OUT/traffic.log"; exit 1; }
       cp gpurun_out/pmc_traffic.json "$OUT/pmc_traffic.json" && tail -1 "$OUT/traffic.log" ;;
