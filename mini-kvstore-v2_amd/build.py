@@ -103,7 +103,8 @@ VARIANTS = {
     "prio0": ["-DKVR_HOP_PRIO=0", "-DKVR_REC_PRIO=0"],   # wave priority off
     "bulklow": ["-DKVR_BULK_LOWPRIO=1"],
     "fin1": ["-DKVR_FIN_PRIO=1"],
-    "s2": ["-DKVR_S4=0"],   # slice-by-2 unit loop (two LDS round trips per word)
+    "s2": ["-DKVR_S4=0"],
+    "kscan": ["-DKVR_XSCAN=0"],   # segmented scan with a multiply at every step   # slice-by-2 unit loop (two LDS round trips per word)
     "base": [],
 }
 

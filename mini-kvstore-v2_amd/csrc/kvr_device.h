@@ -26,8 +26,8 @@ constexpr int      SC    = 128;            // unit: the CRC unit of one lane
 constexpr int      SMALL = 64;             // values <= SMALL: CRC'd whole by their record's lane
 constexpr int      NQ    = SC / 4 + 1;     // X(4q), q <= SC / 4
 constexpr int      KSET_Q = 8;             // kmul sets: X(SC*2^j) j<8, then X(4q) q<=SC/4,
-constexpr int      KSET_R = 8 + NQ;        //   then X(SC(k+1)) k<32 (cross-row scan multipliers)
-constexpr int      KMUL_SETS = 8 + NQ + 32;
+constexpr int      KSET_R = 8 + NQ;        //   then X(SC(k+1)) k<64 (unit-distance multipliers)
+constexpr int      KMUL_SETS = 8 + NQ + 64;
 constexpr int      NIX   = SC + 1;         // 0xFFFFFFFF * X(j), j <= SC
 constexpr uint64_t NONE  = ~0ull;          // "no position"
 constexpr uint64_t ERRP  = ~0ull - 1;      // chain ended in a framing error

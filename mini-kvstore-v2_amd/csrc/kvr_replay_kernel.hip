@@ -65,7 +65,7 @@ constexpr int VALW = SMALL / 4;           // value words of a short value
 // The small tables come first: every table address is a lane-dependent VGPR plus a constant
 // below 64 KiB, which the ds_read instruction carries as its immediate offset.
 struct __align__(16) Smem {
-    uint32_t KR[8 * 16 * 32];             // [i][n][k]: (n << 4i) * x^(8*SC*(k+1)), k < 32
+    uint32_t KR[8 * 16 * 64];             // [i][n][k]: (n << 4i) * x^(8*SC*(k+1)), k < 64
     uint32_t KT[4 * 8 * 16];              // [j][i][n]: (n << 4i) * x^(8*SC*2^j), j < 4
     uint32_t KQ[NQ * 8 * 16];             // [q][i][n]: (n << 4i) * x^(8*4q), q <= SC/4
     uint32_t IX[NIX + 3];                 // 0xFFFFFFFF * x^(8j): initial register pushed through j bytes
@@ -86,6 +86,9 @@ struct __align__(16) Smem {
 #endif
 #ifndef KVR_BULK_LOWPRIO   // experiment: every phase raised except the unit CRC loop
 #define KVR_BULK_LOWPRIO 0
+#endif
+#ifndef KVR_XSCAN   // 1: pieces pushed to their consumer, XOR scan; 0: multiply at every scan step
+#define KVR_XSCAN 1
 #endif
 #ifndef KVR_ABLATE
 #define KVR_ABLATE 0   // diagnostic builds only: 1 skip records, 2 skip value CRC, 4 skip hops,
@@ -114,7 +117,7 @@ __device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 // old with lane l set to the uniform val (v_writelane_b32: one VALU instruction, no compare/select)
 __device__ __forceinline__ uint32_t wl32(uint32_t old, uint32_t val, uint32_t l) {
-    asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(old) : "s"(val), "s"(l) : "m0");
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(old) : "s"(val), "{m0}"(l));   // lane select through m0
     return old;
 }
 __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
@@ -229,13 +232,13 @@ __device__ __forceinline__ uint32_t kmul(uint32_t v, const uint32_t *K) {
     for (int i = 0; i < 8; ++i) t[i] = K[i * 16 + ((pl[i & 1] >> (8 * (i >> 1))) & 255u)];
     return xor8(t);
 }
-// v times x^(8*SC*(k+1)), k per lane (column k of KR: bank k mod 32, conflict free)
+// v times x^(8*SC*(k+1)), k per lane (column k of KR: bank k mod 32)
 __device__ __forceinline__ uint32_t kmulr(uint32_t v, const uint32_t *KR, uint32_t k) {
     uint32_t pl[2] = {v & 0x0F0F0F0Fu, (v >> 4) & 0x0F0F0F0Fu};
     asm("" : "+v"(pl[0]), "+v"(pl[1]));   // keep the planes (no re-fusion into nibble shifts)
     uint32_t t[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) t[i] = KR[(i * 16 + ((pl[i & 1] >> (8 * (i >> 1))) & 255u)) * 32 + k];
+    for (int i = 0; i < 8; ++i) t[i] = KR[(i * 16 + ((pl[i & 1] >> (8 * (i >> 1))) & 255u)) * 64 + k];
     return xor8(t);
 }
 
@@ -568,8 +571,8 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         const int d = i & 63, t = d < 32 ? d >> 3 : (d >> 4) - 2;
         S.C2[i] = tb.crc8[t * 256 + (i >> 6)];
     }
-    for (int i = tid; i < 8 * 16 * 32; i += RT)
-        S.KR[i] = tb.kmul[((KSET_R + (i & 31)) * 8 + (i >> 9)) * 16 + ((i >> 5) & 15)];
+    for (int i = tid; i < 8 * 16 * 64; i += RT)
+        S.KR[i] = tb.kmul[((KSET_R + (i & 63)) * 8 + (i >> 10)) * 16 + ((i >> 6) & 15)];
     for (int i = tid; i < 4 * 8 * 16; i += RT) S.KT[i] = tb.kmul[i];
     for (int i = tid; i < NQ * 8 * 16; i += RT) S.KQ[i] = tb.kmul[KSET_Q * 8 * 16 + i];
     if (tid < NIX) S.IX[tid] = tb.initx[tid];
@@ -721,7 +724,8 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         // the long values touching this tile, folded into every unit's view as they are found
         // (per-lane flags as 32-bit values: a per-lane bool lives in an SGPR lane mask, and every
         // update of it is scalar work in the SALU-bound hop loop)
-        uint32_t vx = 0;                     // a long value crosses the end of this unit
+        int32_t vx = 0;                      // a long value crosses the end of this unit: its end
+                                             // (tile-relative, clamped to FAR; 0: none)
         int32_t a_off = -1;                  // ... starting inside the unit at a_off
         uint32_t vx_carry = 0;               // ... the value carried in from the previous tile
         int32_t m = 0;                       // a long value ends inside this unit, at m (1 .. SC)
@@ -734,7 +738,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         auto consider = [&](int32_t vb, uint64_t ve_abs, uint64_t ref, bool is_abs, bool from_carry) {
             const int64_t v64 = (int64_t)ve_abs - lo;
             const int32_t ver = v64 > FAR ? FAR : (int32_t)v64;
-            if (vb < ue && ver > ue) { vx = 1u; a_off = vb >= us ? vb - us : -1; vx_carry = from_carry ? 1u : 0u; }
+            if (vb < ue && ver > ue) { vx = ver; a_off = vb >= us ? vb - us : -1; vx_carry = from_carry ? 1u : 0u; }
             if (vb < us && ver > us && ver <= ue) { m = ver - us; m_ref = ref; m_abs = is_abs ? 1u : 0u; }
             if (ver > TILE) { out = true; out_ve = ve_abs; out_ref = ref; out_abs = is_abs; }
             any_long = true;
@@ -743,7 +747,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         // 32-bit arithmetic (the hop loop's common case)
         auto consider_rel = [&](int32_t vb, int32_t ver, uint32_t ref) {
             const bool cx = vb < ue && ver > ue, cm = vb < us && ver > us && ver <= ue;
-            vx = cx ? 1u : vx;
+            vx = cx ? ver : vx;
             a_off = cx ? (vb >= us ? vb - us : -1) : a_off;
             vx_carry = cx ? 0u : vx_carry;
             m = cm ? ver - us : m;
@@ -1026,6 +1030,39 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                 v = ok ? (v ^ t_) : v;                                       \
                 f = ok ? of : f;                                             \
             }
+#if KVR_XSCAN
+            // every piece pushed straight to where it is consumed (the unit before the one the
+            // value ends in, or lane 63 for a value running past the tile): one multiply by
+            // x^(8 SC d), then a segmented XOR scan (DPP only) sums each value's pieces there
+            if (!(KVR_ABLATE & 16)) {
+                const int32_t ce = vx > TILE ? 63 : ((vx - 1) >> SC_LOG) - 1;   // (vx = 0: v = 0)
+                const int32_t dd = ce - lane;
+                const uint32_t t_ = kmulr(v, S.KR, dd > 0 ? (uint32_t)(dd - 1) : 0u);
+                v = dd > 0 ? t_ : v;
+#define KVR_XSCAN_ROW(CTRL, D)                                               \
+            {                                                                \
+                const uint32_t ov = dpp<CTRL>(v), of = dpp<CTRL>(f);         \
+                const bool ok = (lane & 15) >= (D) && !f;                    \
+                v = ok ? (v ^ ov) : v;                                       \
+                f = ok ? of : f;                                             \
+            }
+                KVR_XSCAN_ROW(0x111, 1)
+                KVR_XSCAN_ROW(0x112, 2)
+                KVR_XSCAN_ROW(0x114, 4)
+                KVR_XSCAN_ROW(0x118, 8)
+#undef KVR_XSCAN_ROW
+                {
+                    const uint32_t ov = dpp<0x142, 0xA, false>(v), of = dpp<0x142, 0xA, false>(f);
+                    const bool ok = (lane & 16) != 0 && !f;
+                    v = ok ? (v ^ ov) : v;
+                    f = ok ? of : f;
+                }
+                {
+                    const uint32_t ov = dpp<0x143, 0xC, false>(v);
+                    v = (lane >= 32 && !f) ? (v ^ ov) : v;
+                }
+            }
+#else
             if (!(KVR_ABLATE & 16)) {
             KVR_SCAN_ROW(0x111, 1, S.KT)
             KVR_SCAN_ROW(0x112, 2, S.KT + 128)
@@ -1046,6 +1083,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                 v = ok ? (v ^ t_) : v;
             }
             }
+#endif
             KVR_STAMP(10);
             uint32_t sin = dpp<0x138>(v);        // wave_shr:1: the state at this unit's start
             if (lane == 0) sin = c_state;

@@ -57,7 +57,7 @@ for s in $STEPS; do
       timeout -k 10 240 python -u tools/prof_phases.py cfg2 > "$OUT/phases_cfg2.txt" 2>&1 || { echo "phases failed"; tail -20 "$OUT/phases_cfg2.txt"; exit 1; }
       cat "$OUT/phases_cfg2.txt" ;;
     ablate)
-      for m in 0 1 2 3 7; do
+      for m in ${MASKS:-0 1 2 3 7}; do
         timeout -k 10 120 python -u tools/ablate.py cfg2 0 $m >> "$OUT/ablate_cfg2.txt" 2>&1 || { echo "ablate failed"; tail -20 "$OUT/ablate_cfg2.txt"; exit 1; }
       done
       cat "$OUT/ablate_cfg2.txt" ;;
