@@ -104,7 +104,8 @@ VARIANTS = {
     "bulklow": ["-DKVR_BULK_LOWPRIO=1"],
     "fin1": ["-DKVR_FIN_PRIO=1"],
     "s2": ["-DKVR_S4=0"],
-    "kscan": ["-DKVR_XSCAN=0"],   # segmented scan with a multiply at every step   # slice-by-2 unit loop (two LDS round trips per word)
+    "kscan": ["-DKVR_XSCAN=0"],
+    "hopold": ["-DKVR_HOPFAST=0"],   # the hop loop with its separate range checks   # segmented scan with a multiply at every step   # slice-by-2 unit loop (two LDS round trips per word)
     "base": [],
 }
 

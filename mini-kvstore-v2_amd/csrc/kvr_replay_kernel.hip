@@ -87,6 +87,9 @@ struct __align__(16) Smem {
 #ifndef KVR_BULK_LOWPRIO   // experiment: every phase raised except the unit CRC loop
 #define KVR_BULK_LOWPRIO 0
 #endif
+#ifndef KVR_HOPFAST   // 1: one compare per hop-loop check
+#define KVR_HOPFAST 1
+#endif
 #ifndef KVR_XSCAN   // 1: pieces pushed to their consumer, XOR scan; 0: multiply at every scan step
 #define KVR_XSCAN 1
 #endif
@@ -831,7 +834,11 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
 #pragma unroll 1
                     for (;;) {
                         // (conditions combined as integers: one branch, no lane-mask arithmetic)
+#if KVR_HOPFAST
+                        if (((vhiT - 1 - q) | (63 - (int32_t)nb)) < 0) break;   // q >= vhi or 64 records
+#else
                         if (((uint32_t)(q >= vhiT) | (uint32_t)(nb >= 64u)) != 0u) break;
+#endif
                         uint32_t op, klen;
                         if (q + 8 <= TILE) {
                             const uint64_t x = tu64((int)q);
@@ -845,6 +852,22 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                         my_op = wl32(my_op, op, nb);
                         my_klen = wl32(my_klen, klen, nb);
                         ++nb;
+#if KVR_HOPFAST
+                        // (remT < 2^31 and q <= remT: the sums below stay below 2^32; a bad op
+                        // saturates the key length, so one compare covers op, room and klen)
+                        {
+                            const uint32_t kk = __builtin_elementwise_min(klen | (0u - (op >> 1)), 0x80000000u);
+                            if ((uint32_t)q + 5u + kk > (uint32_t)remT) { brk = 1; break; }
+                        }
+                        kmx = klen > kmx ? klen : kmx;
+                        const int32_t e = q + 5 + (int32_t)klen;
+                        if (op == 1u) { q = e; continue; }
+                        // (past the segment end the buffer reads 0; the compare below fails then)
+                        const uint32_t vlen = e + 8 <= TILE ? (uint32_t)tu64((int)e) : uni32(ts.u32(e));
+                        my_vlen = wl32(my_vlen, vlen, nb - 1u);
+                        const int32_t vb = e + 4;
+                        if ((uint32_t)vb + __builtin_elementwise_min(vlen, 0x80000000u) > (uint32_t)remT) { brk = 1; break; }
+#else
                         const uint32_t room = (uint32_t)(remT - q);   // >= 0: q < vhi <= rem
                         if (((uint32_t)(op > 1u) | (uint32_t)(room < 5u) | (uint32_t)(klen > room - 5u)) != 0u) { brk = 1; break; }
                         kmx = klen > kmx ? klen : kmx;
@@ -856,6 +879,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                         my_vlen = wl32(my_vlen, vlen, nb - 1u);
                         const int32_t vb = e + 4;
                         if (vlen > vroom - 4u) { brk = 1; break; }
+#endif
                         const int32_t e2 = vb + (int32_t)vlen;
                         if (vlen > (uint32_t)SMALL && (vb >> SC_LOG) != ((e2 - 1) >> SC_LOG)) {
                             const uint32_t idx = nrec + nb - 1;
