@@ -105,7 +105,9 @@ VARIANTS = {
     "fin1": ["-DKVR_FIN_PRIO=1"],
     "s2": ["-DKVR_S4=0"],
     "kscan": ["-DKVR_XSCAN=0"],
-    "hopold": ["-DKVR_HOPFAST=0"],   # the hop loop with its separate range checks   # segmented scan with a multiply at every step   # slice-by-2 unit loop (two LDS round trips per word)
+    "hopold": ["-DKVR_HOPFAST=0"],
+    "unitsel": ["-DKVR_UNITLITE=0"],
+    "nodefer": ["-DKVR_DEFER=0"],   # long-value unit views updated in the hop loop   # unit loop with per-step register/data selects   # the hop loop with its separate range checks   # segmented scan with a multiply at every step   # slice-by-2 unit loop (two LDS round trips per word)
     "base": [],
 }
 

@@ -90,6 +90,12 @@ struct __align__(16) Smem {
 #ifndef KVR_HOPFAST   // 1: one compare per hop-loop check
 #define KVR_HOPFAST 1
 #endif
+#ifndef KVR_UNITLITE   // 1: unit-loop restarts as one input select, the word at qm loaded from memory
+#define KVR_UNITLITE 1
+#endif
+#ifndef KVR_DEFER   // 1: long-value unit views updated once per hop batch, not per hop
+#define KVR_DEFER 1
+#endif
 #ifndef KVR_XSCAN   // 1: pieces pushed to their consumer, XOR scan; 0: multiply at every scan step
 #define KVR_XSCAN 1
 #endif
@@ -197,9 +203,11 @@ __device__ __forceinline__ void crc2x2(const Crc &k, uint32_t &xa, uint32_t &xb)
     xa = (xa >> 16) ^ a0 ^ a1;
     xb = (xb >> 16) ^ b0 ^ b1;
 }
-__device__ __forceinline__ void crc4x2(uint32_t &ca, uint32_t wa, uint32_t &cb, uint32_t wb, const Crc &k) {
+// (pre = true: wa, wb are already the steps' inputs x = register ^ data)
+__device__ __forceinline__ void crc4x2(uint32_t &ca, uint32_t wa, uint32_t &cb, uint32_t wb, const Crc &k,
+                                       bool pre = false) {
 #if KVR_S4
-    const uint32_t xa = ca ^ wa, xb = cb ^ wb;
+    const uint32_t xa = pre ? wa : ca ^ wa, xb = pre ? wb : cb ^ wb;
     const uint32_t ra = __builtin_amdgcn_alignbit(xa, xa, k.rot), rb = __builtin_amdgcn_alignbit(xb, xb, k.rot);
     uint32_t a0 = s4get(k, ra, 0), a1 = s4get(k, ra, 1), a2 = s4get(k, ra, 2), a3 = s4get(k, ra, 3);
     uint32_t b0 = s4get(k, rb, 0), b1 = s4get(k, rb, 1), b2 = s4get(k, rb, 2), b3 = s4get(k, rb, 3);
@@ -207,7 +215,7 @@ __device__ __forceinline__ void crc4x2(uint32_t &ca, uint32_t wa, uint32_t &cb, 
     ca = xor3(a0, a1, a2) ^ a3;
     cb = xor3(b0, b1, b2) ^ b3;
 #else
-    uint32_t xa = ca ^ wa, xb = cb ^ wb;
+    uint32_t xa = pre ? wa : ca ^ wa, xb = pre ? wb : cb ^ wb;
     crc2x2(k, xa, xb);
     crc2x2(k, xa, xb);
     ca = xa;
@@ -784,6 +792,9 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                 uint32_t nb = 0, kmx = 0;
                 int32_t myrec = -1;
                 uint32_t my_op = 0, my_klen = 0, my_vlen = 0;
+                // KVR_DEFER: a long value found by the hop chain only marks its first unit
+                // (lmark[unit] = its batch index + 1); the unit views are updated once per batch
+                uint32_t lmark = 0, bl = 0;
                 auto hops = [&](auto q) -> decltype(q) {
                     using T = decltype(q);
                     using U = std::make_unsigned_t<T>;
@@ -884,7 +895,10 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                         if (vlen > (uint32_t)SMALL && (vb >> SC_LOG) != ((e2 - 1) >> SC_LOG)) {
                             const uint32_t idx = nrec + nb - 1;
                             if (KVR_ABLATE & 32) any_long = true;
-                            else if (vb < TILE) consider_rel(vb, e2, idx);
+                            else if (vb < TILE) {
+                                if (KVR_DEFER) { lmark = wl32(lmark, nb, (uint32_t)vb >> SC_LOG); bl = 1; }
+                                else consider_rel(vb, e2, idx);
+                            }
                             else { n_carry = 2; n_vb = (uint64_t)(lo + vb); n_ve = (uint64_t)(lo + e2); n_ref = idx; n_abs = false; }
                         }
                         q = e2;
@@ -897,6 +911,37 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                 if (KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
                 if (huge) p = hops((int64_t)p);
                 else p = hops32((int32_t)p);
+                if (KVR_DEFER && bl) {
+                    // unit u's candidates: the batch's last long value starting in a unit <= u (it
+                    // crosses u's end if it ends past ue) and the last one starting before u (it
+                    // ends inside u if us < end <= ue).  Long values are disjoint and in order, so
+                    // these are the only ones that can; a prefix max over the marks finds them.
+                    uint32_t pm = lmark;
+                    pm = __builtin_elementwise_max(pm, dpp<0x111>(pm));
+                    pm = __builtin_elementwise_max(pm, dpp<0x112>(pm));
+                    pm = __builtin_elementwise_max(pm, dpp<0x114>(pm));
+                    pm = __builtin_elementwise_max(pm, dpp<0x118>(pm));
+                    pm = __builtin_elementwise_max(pm, dpp<0x142, 0xA, false>(pm));
+                    pm = __builtin_elementwise_max(pm, dpp<0x143, 0xC, false>(pm));
+                    const uint32_t pp = dpp<0x138>(pm);   // wave_shr:1: the marks before this unit
+                    // lane j holds batch record j: its value [rvb, re2) (tile-relative)
+                    const int32_t rvb = myrec + 9 + (int32_t)my_klen, re2 = rvb + (int32_t)my_vlen;
+                    const int ic = 4 * (int)(pm ? pm - 1u : 0u), ip = 4 * (int)(pp ? pp - 1u : 0u);
+                    const int32_t vbc = __builtin_amdgcn_ds_bpermute(ic, rvb), e2c = __builtin_amdgcn_ds_bpermute(ic, re2);
+                    const int32_t e2p = __builtin_amdgcn_ds_bpermute(ip, re2);
+                    const bool cx = pm != 0u && e2c > ue;
+                    vx = cx ? e2c : vx;
+                    a_off = cx ? (vbc >= us ? vbc - us : -1) : a_off;
+                    vx_carry = cx ? 0u : vx_carry;
+                    const bool cm = pp != 0u && e2p > us && e2p <= ue;
+                    m = cm ? e2p - us : m;
+                    m_ref = cm ? (uint64_t)(nrec + pp - 1u) : m_ref;
+                    m_abs = cm ? 0u : m_abs;
+                    // a value crossing the last unit's end runs past the tile (ue = TILE there)
+                    const uint32_t e63 = rl32(cx ? (uint32_t)e2c : 0u, 63);
+                    if (e63 != 0u) { out = true; out_ve = (uint64_t)(lo + (int32_t)e63); out_ref = nrec + rl32(pm, 63) - 1u; out_abs = false; }
+                    any_long = true;
+                }
                 if (KVR_HOP_PRIO && !KVR_REC_PRIO) __builtin_amdgcn_s_setprio(KVR_BULK_LOWPRIO ? 2 : 0);
                 KVR_STAMP(1);
                 // pool slots of the batch (one run: a fresh chunk holds any tile's rest)
@@ -1017,6 +1062,20 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
 #pragma unroll
                 for (int kk = 0; kk < H; ++kk) crc4x2(ca, w[kk], cb, w[kk + H], K);
             } else {
+#if KVR_UNITLITE
+                // the word at qm comes from memory (issued here, used after the scan), and a restart
+                // is one select of the step's input: x = restart ? (w & amask) : (c ^ w)
+                if (m & 3) wm = ts.w32a(us + 4 * qm);
+#pragma unroll
+                for (int kk = 0; kk < H; ++kk) {
+                    const bool s_ = kk == qh;
+                    sn = s_ ? (mb ? cb : ca) : sn;
+                    const bool r = kk == qah, ra = r && !ab, rb = r && ab;
+                    const uint32_t xa = ra ? (w[kk] & amask) : (ca ^ w[kk]);
+                    const uint32_t xb = rb ? (w[kk + H] & amask) : (cb ^ w[kk + H]);
+                    crc4x2(ca, xa, cb, xb, K, true);
+                }
+#else
 #pragma unroll
                 for (int kk = 0; kk < H; ++kk) {
                     const bool s_ = kk == qh;
@@ -1027,6 +1086,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     cb = rb ? 0u : cb;
                     crc4x2(ca, ra ? (w[kk] & amask) : w[kk], cb, rb ? (w[kk + H] & amask) : w[kk + H], K);
                 }
+#endif
                 sn = qm == UW ? cb : sn;
             }
             // the piece of the value crossing the unit end: A pushed through B's bytes, then B
