@@ -107,7 +107,9 @@ VARIANTS = {
     "kscan": ["-DKVR_XSCAN=0"],
     "hopold": ["-DKVR_HOPFAST=0"],
     "unitsel": ["-DKVR_UNITLITE=0"],
-    "nodefer": ["-DKVR_DEFER=0"],   # long-value unit views updated in the hop loop   # unit loop with per-step register/data selects   # the hop loop with its separate range checks   # segmented scan with a multiply at every step   # slice-by-2 unit loop (two LDS round trips per word)
+    "nodefer": ["-DKVR_DEFER=0"],
+    "foldnokey": ["-DKVR_FOLD_NOKEY"],
+    "foldsplit": ["-DKVR_FOLD_MERGE=0"],   # every tag match verified by k_fold_verify   # fold kernels without key reads (timing bound only)   # long-value unit views updated in the hop loop   # unit loop with per-step register/data selects   # the hop loop with its separate range checks   # segmented scan with a multiply at every step   # slice-by-2 unit loop (two LDS round trips per word)
     "base": [],
 }
 
@@ -126,6 +128,23 @@ def build_variants(names=None):
     for p in procs:
         if p.wait() != 0:
             raise RuntimeError("variant build failed")
+    return out
+
+
+def build_variant_pair(name):
+    """lib/vpair/<name>/: a VARIANTS build of libkvreplay.so with its own libkvhost.so, so a whole
+    process (kvreplay with KVREPLAY_VARIANT=<name>) runs the variant; timing tools only."""
+    out = os.path.join(LIB, "vpair", name)
+    os.makedirs(out, exist_ok=True)
+    rep = os.path.join(out, "libkvreplay.so")
+    deps = _deps(*[f for f in os.listdir(CSRC) if f.endswith((".hip", ".h"))])
+    if _newer(rep, deps):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *VARIANTS[name],
+              "-Wno-unused-result", "-o", rep, os.path.join(CSRC, "kvr_api.hip")])
+    host = os.path.join(out, "libkvhost.so")
+    if _newer(host, _deps("kvr_host.cpp", "kvr_gen_common.h") + [rep]):
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", host, os.path.join(CSRC, "kvr_host.cpp"),
+              "-L", out, "-lkvreplay", "-Wl,-rpath,$ORIGIN", "-Wl,--no-as-needed"])
     return out
 
 

@@ -101,6 +101,8 @@ struct kvr_ctx {
     DevBuf<kvr_tuple> ctup, lout;
     DevBuf<FoldEnt> fent;                  // the fold table (k_fold_claim / k_fold_verify)
     DevBuf<uint32_t> flist, fcnt;          // collision rounds: two tuple lists, their counts
+    DevBuf<uint32_t> fsz;                  // the fold table's size on the device (k_hll_size)
+    bool fold_pending = false;             // deferred rounds launched, not yet checked (fold_settle)
     DevBuf<uint32_t> cslot, cflag, cpos, cfirst;
     DevBuf<uint64_t> csize, coff, l_src, l_off, ctot, ccuts;
     DevBuf<uint8_t> cout, ctmp;
@@ -296,7 +298,7 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->pool.release(); c->dense.release(); c->redo.release(); c->link.release(); c->ctr.release();
     c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->bsum.release();
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
-    c->ctup.release(); c->lout.release(); c->fent.release(); c->flist.release(); c->fcnt.release();
+    c->ctup.release(); c->lout.release(); c->fent.release(); c->flist.release(); c->fcnt.release(); c->fsz.release();
     c->cslot.release(); c->cflag.release(); c->islots.release(); c->ing.release(); c->hpart.release(); c->hreg.release();
     c->koff.release(); c->klen.release(); c->kbuf.release();
     c->cpos.release(); c->cfirst.release(); c->csize.release(); c->coff.release(); c->l_src.release();
@@ -678,8 +680,9 @@ static double hll_estimate(const uint8_t *reg) {
 // the next kvr_compact_stage).  rewrite: also size the buffers of the byte rewrite
 // (compact_back).  cs: the statistics this call fills (the caller's, so a live replay leaves
 // kvr_last_compact_stats alone).
+static int fold_launch(kvr_ctx *c, size_t nt, bool deferred);
 static int compact_front(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, kvr_error *err, size_t *nt_out,
-                         bool rewrite, kvr_compact_stats *cs) {
+                         bool rewrite, kvr_compact_stats *cs, bool deferred = false) {
     *nt_out = 0;
     c->c_staged = false;
     c->c_nt = 0;
@@ -709,77 +712,166 @@ static int compact_front(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t
     if (nt >= 0x7FFFFFFFull) return KVR_EINVAL;   // 32-bit tuple indices in the fold table
     c->c_nt = nt;
     hipStream_t st = c->stream;
-    // 2. the key's last tuple (open addressing over the key bytes, kvr_compact.hip).  The table
-    // is sized for the distinct keys (HyperLogLog estimate, load <= 0.63) rather than the tuples,
-    // so it stays in the caches; a table that fills up is redone at 2 n entries.
-    HIPCHK(hipEventRecord(c->ev[0], st));
-    uint64_t full_slots = 1;
-    while (full_slots < 2 * (uint64_t)nt) full_slots <<= 1;
-    uint64_t slots = full_slots;
-    if (nt >= 65536 || getenv("KVR_FOLD_TINY_TABLE")) {
-        const uint32_t hb = (uint32_t)std::min<uint64_t>((nt + HLL_T - 1) / HLL_T, (uint64_t)c->n_cu);
-        if (c->hpart.ensure((uint64_t)hb * HLL_M) || c->hreg.ensure(HLL_M)) return KVR_ENOMEM;
-        hipLaunchKernelGGL(k_hll, dim3(hb), dim3(HLL_T), 0, st, c->ctup.p, (uint64_t)nt, c->hpart.p);
-        hipLaunchKernelGGL(k_hll_merge, dim3(HLL_M / 16 / 16), dim3(HLL_MERGE_T), 0, st, c->hpart.p, hb, c->hreg.p);
-        HIPCHK(hipGetLastError());
-        std::vector<uint8_t> reg(HLL_M);
-        HIPCHK(hipMemcpyAsync(reg.data(), c->hreg.p, HLL_M, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        const double est = hll_estimate(reg.data());
-        c->fold_est = (uint64_t)est;
-        uint64_t want = 16;
-        while ((double)want < 1.6 * est + 1024.0) want <<= 1;
-        slots = std::min(want, full_slots);
-        if (getenv("KVR_FOLD_TINY_TABLE")) slots = 16;   // test knob: force the full-size redo
-    }
-    if (c->fent.ensure(full_slots) || c->cslot.ensure(nt) || c->cflag.ensure(nt) || c->cpos.ensure(nt) ||
-        c->csize.ensure(nt) || c->flist.ensure(2 * nt) || c->fcnt.ensure(2))
-        return KVR_ENOMEM;
+    if (c->cflag.ensure(nt) || c->cpos.ensure(nt) || c->csize.ensure(nt)) return KVR_ENOMEM;
     if (rewrite && (c->coff.ensure(nt) || c->l_src.ensure(nt) || c->l_off.ensure(nt + 1) || c->ctot.ensure(2)))
         return KVR_ENOMEM;
     size_t t1 = 0, t2 = 0;
     if (rewrite) HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, c->csize.p, c->coff.p, (int)nt, st));
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, c->cflag.p, c->cpos.p, (int)nt, st));
     if (c->ctmp.ensure(std::max(t1, t2))) return KVR_ENOMEM;
+    HIPCHK(hipEventRecord(c->ev[0], st));
+    return fold_launch(c, nt, deferred);
+}
+
+// the grid of the kernels that walk the fold table (grid-stride over its size on the device)
+static uint32_t fold_grid(const kvr_ctx *c) {
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((c->fent.n + 255) / 256, 4096));
+}
+
+// 2. the key's last tuple (open addressing over the key bytes, kvr_compact.hip) of c->ctup[0, nt).
+// The table is sized for the distinct keys (HyperLogLog estimate, load <= 0.63) rather than the
+// tuples, so it stays in the caches; the size is computed and used on the device (no host round
+// trip between the estimate and the claims); a table that fills up is redone at 2 n entries.
+// deferred: round 0 and FOLD_SPEC_ROUNDS - 1 further collision rounds (each of at most
+// FOLD_SPEC_CAP tuples, their sizes read on the device) are launched without a host sync; the
+// caller syncs once for everything and calls fold_settle, which redoes the fold synchronously in
+// the rare case that this was not enough.  Otherwise the rounds run with one sync each.
+constexpr uint32_t FOLD_SPEC_ROUNDS = 3, FOLD_SPEC_CAP = 65536, FOLD_CNT = 2;
+constexpr int FOLD_REDONE = 1000;   // internal (compact_back): the deferred fold was redone
+static int fold_launch(kvr_ctx *c, size_t nt, bool deferred) {
+    hipStream_t st = c->stream;
+    uint64_t full_slots = 1;
+    while (full_slots < 2 * (uint64_t)nt) full_slots <<= 1;
+    if (c->fent.ensure(full_slots) || c->cslot.ensure(nt) || c->flist.ensure(2 * nt) ||
+        c->fcnt.ensure(FOLD_CNT * FOLD_SPEC_ROUNDS) || c->fsz.ensure(4))
+        return KVR_ENOMEM;
+    c->fold_rounds = 0;
+    c->fold_redo = 0;
+    c->fold_est = 0;
+    c->fold_pending = false;
+    const bool tiny = getenv("KVR_FOLD_TINY_TABLE") != nullptr;   // test knob: force the full-size redo
+    if (tiny) {
+        hipLaunchKernelGGL(k_fold_setsize, dim3(1), dim3(1), 0, st, c->fsz.p, 15u);
+    } else if (nt >= 65536) {
+        const uint32_t hb = (uint32_t)std::min<uint64_t>((nt + HLL_T - 1) / HLL_T, (uint64_t)c->n_cu);
+        if (c->hpart.ensure((uint64_t)hb * HLL_M) || c->hreg.ensure(HLL_M)) return KVR_ENOMEM;
+        hipLaunchKernelGGL(k_hll, dim3(hb), dim3(HLL_T), 0, st, c->ctup.p, (uint64_t)nt, c->hpart.p);
+        hipLaunchKernelGGL(k_hll_merge, dim3(HLL_M / 16 / 16), dim3(HLL_MERGE_T), 0, st, c->hpart.p, hb, c->hreg.p);
+        hipLaunchKernelGGL(k_hll_size, dim3(1), dim3(HLL_SIZE_T), 0, st, c->hreg.p, full_slots, c->fsz.p);
+    } else {
+        hipLaunchKernelGGL(k_fold_setsize, dim3(1), dim3(1), 0, st, c->fsz.p, (uint32_t)(full_slots - 1));
+    }
+    HIPCHK(hipGetLastError());
+    static const bool pre = getenv("KVR_CLAIM_PRELOAD") && atoi(getenv("KVR_CLAIM_PRELOAD"));   // timing knob
+    // one probe round over m tuples (list: null = all, in round 0); counters cnt[0] tuples left for
+    // the next round, cnt[1] claims that found the table full
+    auto round = [&](uint64_t m, const uint32_t *n_dev, const uint32_t *list, uint32_t *next, uint32_t *cnt) {
+        const uint32_t g = (uint32_t)((m + 255) / 256);
+        if (pre)
+            hipLaunchKernelGGL(k_fold_claim<true>, dim3(g), dim3(256), 0, st, c->ctup.p, m, n_dev, list, c->segs.p,
+                               c->fent.p, c->fsz.p, c->cslot.p, cnt + 1);
+        else
+            hipLaunchKernelGGL(k_fold_claim<false>, dim3(g), dim3(256), 0, st, c->ctup.p, m, n_dev, list, c->segs.p,
+                               c->fent.p, c->fsz.p, c->cslot.p, cnt + 1);
+        hipLaunchKernelGGL(k_fold_verify, dim3(g), dim3(256), 0, st, c->ctup.p, m, n_dev, list, c->segs.p, c->fent.p,
+                           c->fsz.p, c->cslot.p, next, cnt);
+    };
 again:
-    HIPCHK(hipMemsetAsync(c->fent.p, 0xFF, slots * sizeof(FoldEnt), st));
-    c->fold_slots = slots;
-    const uint32_t mask = (uint32_t)(slots - 1);
-    const uint32_t *list = nullptr;   // round 0: every tuple
-    uint64_t m = nt;
+    hipLaunchKernelGGL(k_fent_clear, dim3(fold_grid(c)), dim3(256), 0, st, c->fent.p, c->fsz.p);
+    HIPCHK(hipMemsetAsync(c->fcnt.p, 0, FOLD_CNT * FOLD_SPEC_ROUNDS * sizeof(uint32_t), st));
+    round(nt, nullptr, nullptr, c->flist.p, c->fcnt.p);
+    HIPCHK(hipGetLastError());
+    if (deferred) {
+        for (uint32_t r = 1; r < FOLD_SPEC_ROUNDS; ++r)
+            round(FOLD_SPEC_CAP, c->fcnt.p + FOLD_CNT * (r - 1), c->flist.p + (uint64_t)((r - 1) & 1u) * nt,
+                  c->flist.p + (uint64_t)(r & 1u) * nt, c->fcnt.p + FOLD_CNT * r);
+        HIPCHK(hipGetLastError());
+        c->fold_pending = true;
+        return KVR_OK;
+    }
+    const uint32_t *list = c->flist.p;
+    uint64_t m = 0;
     for (uint32_t r = 0;; ++r) {
         uint32_t *next = c->flist.p + (uint64_t)(r & 1u) * nt;
-        const uint32_t g = (uint32_t)((m + 255) / 256);
-        HIPCHK(hipMemsetAsync(c->fcnt.p, 0, 8, st));
-        static const bool pre = getenv("KVR_CLAIM_PRELOAD") && atoi(getenv("KVR_CLAIM_PRELOAD"));   // timing knob
-        if (pre)
-            hipLaunchKernelGGL(k_fold_claim<true>, dim3(g), dim3(256), 0, st, c->ctup.p, m, list, c->segs.p, c->fent.p,
-                               mask, c->cslot.p, c->fcnt.p + 1);
-        else
-            hipLaunchKernelGGL(k_fold_claim<false>, dim3(g), dim3(256), 0, st, c->ctup.p, m, list, c->segs.p, c->fent.p,
-                               mask, c->cslot.p, c->fcnt.p + 1);
-        hipLaunchKernelGGL(k_fold_verify, dim3(g), dim3(256), 0, st, c->ctup.p, m, list, c->segs.p, c->fent.p, mask,
-                           c->cslot.p, next, c->fcnt.p);
-        HIPCHK(hipGetLastError());
+        if (r > 0) {
+            HIPCHK(hipMemsetAsync(c->fcnt.p, 0, FOLD_CNT * sizeof(uint32_t), st));
+            round(m, nullptr, list, next, c->fcnt.p);
+            HIPCHK(hipGetLastError());
+        }
         uint32_t cnt[2] = {0, 0};   // tuples left for the next round, claims that found the table full
+        uint32_t fs[4] = {0, 0, 0, 0};
         HIPCHK(hipMemcpyAsync(cnt, c->fcnt.p, 8, hipMemcpyDeviceToHost, st));
+        if (r == 0) HIPCHK(hipMemcpyAsync(fs, c->fsz.p, 16, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        const uint32_t left = cnt[0];
+        if (r == 0) {
+            c->fold_slots = (uint64_t)fs[0] + 1;
+            c->fold_est = (uint64_t)fs[2] | ((uint64_t)fs[3] << 32);
+        }
         c->fold_rounds = r + 1;
         if (cnt[1]) {
-            if (slots == full_slots) return KVR_EHIP;   // cannot happen: 2 n entries hold every tuple
-            slots = full_slots;
+            if (c->fold_slots == full_slots) return KVR_EHIP;   // cannot happen: 2 n entries hold every tuple
+            hipLaunchKernelGGL(k_fold_setsize, dim3(1), dim3(1), 0, st, c->fsz.p, (uint32_t)(full_slots - 1));
             ++c->fold_redo;
             goto again;
         }
-        if (left == 0) break;
+        if (cnt[0] == 0) break;
         // tuples whose tag another key holds: each round moves every one of them at least one
-        // entry on, so mask + 1 rounds bound the loop (a few in practice)
-        if (r > mask) return KVR_EHIP;
+        // entry on, so (table size) rounds bound the loop (a few in practice)
+        if (r > c->fold_slots) return KVR_EHIP;
         list = next;
-        m = left;
+        m = cnt[0];
     }
     return KVR_OK;
+}
+
+// the counters of deferred rounds, read back with the caller's own sync (fold_check_*)
+struct FoldCheck {
+    uint32_t cnt[FOLD_CNT * FOLD_SPEC_ROUNDS];
+    uint32_t fs[4];
+};
+static hipError_t fold_check_enqueue(kvr_ctx *c, FoldCheck *fc) {
+    if (!c->fold_pending) return hipSuccess;
+    hipError_t e = hipMemcpyAsync(fc->cnt, c->fcnt.p, sizeof(fc->cnt), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(fc->fs, c->fsz.p, sizeof(fc->fs), hipMemcpyDeviceToHost, c->stream);
+    return e;
+}
+// after that sync: true when the deferred rounds finished the fold (statistics filled in)
+static bool fold_check_eval(kvr_ctx *c, const FoldCheck &fc) {
+    if (!c->fold_pending) return true;
+    c->fold_pending = false;
+    c->fold_slots = (uint64_t)fc.fs[0] + 1;
+    c->fold_est = (uint64_t)fc.fs[2] | ((uint64_t)fc.fs[3] << 32);
+    bool ok = true;
+    uint32_t rounds = 1;
+    for (uint32_t r = 0; r < FOLD_SPEC_ROUNDS; ++r) {
+        const uint32_t left = fc.cnt[FOLD_CNT * r], full = fc.cnt[FOLD_CNT * r + 1];
+        if (full) ok = false;
+        if (left) {
+            if (r + 1 == FOLD_SPEC_ROUNDS || left > FOLD_SPEC_CAP) ok = false;
+            else rounds = r + 2;
+        }
+    }
+    c->fold_rounds = rounds;
+    return ok;
+}
+
+// after the caller's sync point: did the deferred rounds finish the fold?  Reads the counters
+// (and, when last2 is given, the live totals cpos[nt - 1], cflag[nt - 1]) with one sync; if the
+// fold was not complete it is redone synchronously and *redone is set (the caller then redoes
+// what it derived from the table).
+static int fold_settle(kvr_ctx *c, size_t nt, bool *redone, uint32_t *last2) {
+    *redone = false;
+    hipStream_t st = c->stream;
+    FoldCheck fc{};
+    HIPCHK(fold_check_enqueue(c, &fc));
+    if (last2) {
+        HIPCHK(hipMemcpyAsync(&last2[0], c->cpos.p + nt - 1, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(&last2[1], c->cflag.p + nt - 1, 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    if (fold_check_eval(c, fc)) return KVR_OK;
+    *redone = true;
+    return fold_launch(c, nt, false);
 }
 
 // live flags (and, for a rewrite, record sizes) of the tuples from the fold table
@@ -789,9 +881,8 @@ static hipError_t live_flags(kvr_ctx *c, size_t nt, bool sizes, bool keep_del = 
     hipError_t e = hipMemsetAsync(c->cflag.p, 0, nt * 4, st);
     if (e == hipSuccess && sizes) e = hipMemsetAsync(c->csize.p, 0, nt * 8, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_live_ent, dim3((uint32_t)((c->fold_slots + 255) / 256)), dim3(256), 0, st, c->fent.p,
-                       (uint64_t)c->fold_slots, c->ctup.p, sizes ? c->csize.p : nullptr, c->cflag.p,
-                       keep_del ? 1u : 0u);
+    hipLaunchKernelGGL(k_live_ent, dim3(fold_grid(c)), dim3(256), 0, st, c->fent.p, c->fsz.p, c->ctup.p,
+                       sizes ? c->csize.p : nullptr, c->cflag.p, keep_del ? 1u : 0u);
     return hipGetLastError();
 }
 
@@ -842,7 +933,13 @@ static int compact_back(kvr_ctx *c, uint32_t flags, uint64_t seg_target, uint8_t
     HIPCHK(hipMemcpyAsync(tot, c->ctot.p, sizeof(tot), hipMemcpyDeviceToHost, st));
     std::vector<uint64_t> cuts(seg_target ? max_cuts : 0);
     if (seg_target) HIPCHK(hipMemcpyAsync(cuts.data(), c->ccuts.p, max_cuts * 8, hipMemcpyDeviceToHost, st));
+    FoldCheck fc{};
+    HIPCHK(fold_check_enqueue(c, &fc));   // a deferred fold is checked with this same sync
     HIPCHK(hipStreamSynchronize(st));
+    if (!fold_check_eval(c, fc)) {        // rare: redo the fold with synced rounds, then the caller
+        const int rc = fold_launch(c, nt, false);   // redoes the rewrite
+        return rc == KVR_OK ? FOLD_REDONE : rc;
+    }
     c->cstats.ms_fold = ev_ms(c->ev[0], c->ev[1]);
     c->cstats.ms_gather = ev_ms(c->ev[1], c->ev[2]);
     const uint64_t total = tot[0], n_live = tot[1];
@@ -874,10 +971,15 @@ int kvr_compact(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, u
     *out_len = 0;
     *n_out_segs = 0;
     size_t nt = 0;
-    const int rc = compact_front(c, segs, n, flags, err, &nt, true, &c->cstats);
+    const int rc = compact_front(c, segs, n, flags, err, &nt, true, &c->cstats, true);   // deferred rounds
     if (rc != KVR_OK || nt == 0) return rc;
     HIPCHK(live_flags(c, nt, true));
-    return compact_back(c, flags, seg_target, out, out_cap, out_len, seg_ends, seg_cap, n_out_segs);
+    int rb = compact_back(c, flags, seg_target, out, out_cap, out_len, seg_ends, seg_cap, n_out_segs);
+    if (rb == FOLD_REDONE) {
+        HIPCHK(live_flags(c, nt, true));
+        rb = compact_back(c, flags, seg_target, out, out_cap, out_len, seg_ends, seg_cap, n_out_segs);
+    }
+    return rb;
 }
 
 int kvr_compact_stage(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, const uint32_t *gidx,

@@ -102,6 +102,10 @@ constexpr unsigned long long FE_EMPTY = ~0ull;   // the table is memset to 0xFF
 // into an unmapped page, whatever padding the caller's buffer has.  (Two aligned 16-B loads
 // measured slower: 401 vs 333 us for k_fold_verify on cfg2.)
 __device__ __forceinline__ void key_prefix16(const SegDesc &g, const kvr_tuple &t, uint32_t w[4]) {
+#ifdef KVR_FOLD_NOKEY   // timing diagnostic only (build.py variant foldnokey): no key reads, wrong results
+    w[0] = w[1] = w[2] = w[3] = t.key_tag;
+    return;
+#endif
     const uintptr_t p = reinterpret_cast<uintptr_t>(g.base) + t.rec_off + 5;
     const uintptr_t end = reinterpret_cast<uintptr_t>(g.base) + g.len;
     const uintptr_t pa = p & ~(uintptr_t)3;
@@ -171,15 +175,67 @@ __global__ void __launch_bounds__(HLL_MERGE_T) k_hll_merge(const uint8_t *__rest
     }
 }
 
+// the fold table's size on the device, so no host round trip sits between the estimate and the
+// claims: fsz[0] = entries - 1 (a power of two minus one), fsz[2..3] = the estimate (uint64).
+// The same arithmetic as the host's hll_estimate (kvr_api.hip), summed in a different order.
+constexpr int HLL_SIZE_T = 256;
+__global__ void __launch_bounds__(HLL_SIZE_T) k_hll_size(const uint8_t *__restrict__ reg, uint64_t full_slots,
+                                                         uint32_t *__restrict__ fsz) {
+    __shared__ double ss[HLL_SIZE_T];
+    __shared__ uint32_t sz[HLL_SIZE_T];
+    double sum = 0;
+    uint32_t zeros = 0;
+    for (int j = threadIdx.x; j < HLL_M; j += HLL_SIZE_T) {
+        sum += ldexp(1.0, -(int)reg[j]);
+        zeros += reg[j] == 0;
+    }
+    ss[threadIdx.x] = sum;
+    sz[threadIdx.x] = zeros;
+    __syncthreads();
+    for (int d = HLL_SIZE_T / 2; d > 0; d >>= 1) {
+        if ((int)threadIdx.x < d) { ss[threadIdx.x] += ss[threadIdx.x + d]; sz[threadIdx.x] += sz[threadIdx.x + d]; }
+        __syncthreads();
+    }
+    if (threadIdx.x) return;
+    const double m = HLL_M, alpha = 0.7213 / (1.0 + 1.079 / m);
+    double e = alpha * m * m / ss[0];
+    if (e <= 2.5 * m && sz[0]) e = m * log(m / sz[0]);
+    const double two32 = 4294967296.0;
+    if (e > two32 / 30.0) e = e < two32 ? -two32 * log(1.0 - e / two32) : two32;
+    uint64_t want = 16;
+    while ((double)want < 1.6 * e + 1024.0) want <<= 1;
+    const uint64_t slots = want < full_slots ? want : full_slots;
+    fsz[0] = (uint32_t)(slots - 1);
+    *reinterpret_cast<uint64_t *>(fsz + 2) = (uint64_t)e;
+}
+__global__ void k_fold_setsize(uint32_t *__restrict__ fsz, uint32_t mask) {
+    fsz[0] = mask;
+    *reinterpret_cast<uint64_t *>(fsz + 2) = 0;
+}
+// free entries (all ones) for the table size on the device; grid-stride
+__global__ void k_fent_clear(FoldEnt *__restrict__ ent, const uint32_t *__restrict__ fsz) {
+    const uint32_t mask = fsz[0];
+    const uint4 ff = make_uint4(~0u, ~0u, ~0u, ~0u);
+    for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h <= mask; h += (uint64_t)gridDim.x * blockDim.x) {
+        reinterpret_cast<uint4 *>(&ent[h])[0] = ff;
+        reinterpret_cast<uint4 *>(&ent[h])[1] = ff;
+    }
+}
+
 // one probe round: tuple i (all tuples in round 0, list[] afterwards) walks from its start entry
 // (the tag's home slot in round 0, slot[i] afterwards) to the first entry that is free (claimed
 // here) or holds its tag (verified by k_fold_verify)
+// (n_dev: a later round launched before the host knows its size reads it here; n caps it at the
+// grid, and the host checks afterwards that no round was larger)
 template <bool PRE>
-__global__ void k_fold_claim(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ list,
-                             const SegDesc *__restrict__ segs, FoldEnt *__restrict__ ent, uint32_t mask,
+__global__ void k_fold_claim(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ n_dev,
+                             const uint32_t *__restrict__ list, const SegDesc *__restrict__ segs,
+                             FoldEnt *__restrict__ ent, const uint32_t *__restrict__ fsz,
                              uint32_t *__restrict__ slot, uint32_t *__restrict__ full) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n_dev && *n_dev < n) n = *n_dev;
     if (g >= n) return;
+    const uint32_t mask = fsz[0];
     // latest tuples first (workgroups start in index order): a key's claimer is then usually its
     // last tuple, which k_fold_verify exploits
     const uint32_t i = list ? list[n - 1 - g] : (uint32_t)(n - 1 - g);
@@ -211,11 +267,14 @@ __global__ void k_fold_claim(const kvr_tuple *__restrict__ tup, uint64_t n, cons
 }
 
 // same key as the entry's representative: keep the last index; else on to the next round
-__global__ void k_fold_verify(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ list,
-                              const SegDesc *__restrict__ segs, FoldEnt *__restrict__ ent, uint32_t mask,
+__global__ void k_fold_verify(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ n_dev,
+                              const uint32_t *__restrict__ list, const SegDesc *__restrict__ segs,
+                              FoldEnt *__restrict__ ent, const uint32_t *__restrict__ fsz,
                               uint32_t *__restrict__ slot, uint32_t *__restrict__ next, uint32_t *__restrict__ n_next) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n_dev && *n_dev < n) n = *n_dev;
     if (g >= n) return;
+    const uint32_t mask = fsz[0];
     const uint32_t i = list ? list[n - 1 - g] : (uint32_t)(n - 1 - g);   // latest first
     const uint32_t h = slot[i];
     if (h == HT_EMPTY) return;
@@ -255,17 +314,20 @@ __device__ __forceinline__ bool is_last(const FoldEnt *ent, const uint32_t *slot
 // claimed entries' last tuples at random) instead of every tuple and its entry.
 // (keep_del: every key's last record, a DEL included — the per-GPU reduction of a sharded store,
 // whose tombstones may delete a key another GPU SET)
-__global__ void k_live_ent(const FoldEnt *__restrict__ ent, uint64_t n_slots, const kvr_tuple *__restrict__ tup,
-                           uint64_t *__restrict__ size, uint32_t *__restrict__ flag, uint32_t keep_del) {
-    const uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (h >= n_slots) return;
-    const uint4 a = reinterpret_cast<const uint4 *>(&ent[h])[0];
-    if (a.x == 0xFFFFFFFFu && a.y == 0xFFFFFFFFu) return;   // free
-    const uint32_t j = ~a.z;
-    const kvr_tuple t = tup[j];
-    if (t.op != 0 && !keep_del) return;
-    flag[j] = 1u;
-    if (size) size[j] = 9ull + t.key_len + t.val_len;   // SET framing, engine.rs:169-173
+// (grid-stride over the table size on the device)
+__global__ void k_live_ent(const FoldEnt *__restrict__ ent, const uint32_t *__restrict__ fsz,
+                           const kvr_tuple *__restrict__ tup, uint64_t *__restrict__ size,
+                           uint32_t *__restrict__ flag, uint32_t keep_del) {
+    const uint64_t n_slots = (uint64_t)fsz[0] + 1;
+    for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n_slots; h += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 a = reinterpret_cast<const uint4 *>(&ent[h])[0];
+        if (a.x == 0xFFFFFFFFu && a.y == 0xFFFFFFFFu) continue;   // free
+        const uint32_t j = ~a.z;
+        const kvr_tuple t = tup[j];
+        if (t.op != 0 && !keep_del) continue;
+        flag[j] = 1u;
+        if (size) size[j] = 9ull + t.key_len + t.val_len;   // SET framing, engine.rs:169-173
+    }
 }
 
 // totals: live bytes, live records, and the end sentinel of the dense offsets

@@ -31,17 +31,19 @@ constexpr uint32_t IX_DEAD = 0xFFFFFFFFu;   // a key whose last record is a DEL:
 // slots[h] from fold entry h: free -> 0, a live key -> 1 + its position in the live list, a
 // deleted key -> IX_DEAD (keeps the probe sequences of the keys behind it intact).  No atomics:
 // the fold already placed every key.
-__global__ void k_index_from_fold(const FoldEnt *__restrict__ ent, uint64_t n_slots, const uint32_t *__restrict__ flag,
-                                  const uint32_t *__restrict__ pos, uint32_t *__restrict__ slots) {
-    const uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (h >= n_slots) return;
-    const uint4 a = reinterpret_cast<const uint4 *>(&ent[h])[0];
-    uint32_t v = 0;
-    if (!(a.x == 0xFFFFFFFFu && a.y == 0xFFFFFFFFu)) {
-        const uint32_t j = ~a.z;
-        v = flag[j] ? pos[j] + 1u : IX_DEAD;
+__global__ void k_index_from_fold(const FoldEnt *__restrict__ ent, const uint32_t *__restrict__ fsz,
+                                  const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
+                                  uint32_t *__restrict__ slots) {
+    const uint64_t n_slots = (uint64_t)fsz[0] + 1;   // the fold table's size on the device; grid-stride
+    for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n_slots; h += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 a = reinterpret_cast<const uint4 *>(&ent[h])[0];
+        uint32_t v = 0;
+        if (!(a.x == 0xFFFFFFFFu && a.y == 0xFFFFFFFFu)) {
+            const uint32_t j = ~a.z;
+            v = flag[j] ? pos[j] + 1u : IX_DEAD;
+        }
+        slots[h] = v;
     }
-    slots[h] = v;
 }
 
 // key arena: live key i's bytes to keys[off[i] ..) — one thread per key (keys are short; a
@@ -66,26 +68,36 @@ uint64_t index_slots(uint64_t n_live) {
     return s;
 }
 
-// after compact_front: live flags, their scan and the dense live list in c->lout; *total = n_live
-// (keep_del: every key's last record instead, tombstones included)
-int live_list(kvr_ctx *c, size_t nt, uint64_t *total, bool keep_del = false) {
-    *total = 0;
-    if (nt == 0) return KVR_OK;
+// after compact_front: live flags, their scan and the dense live list in c->lout (room for every
+// tuple), and with index the key table in c->islots (room for the largest table); no host sync —
+// n_live = cpos[nt - 1] + cflag[nt - 1], read by fold_settle (keep_del: every key's last record
+// instead, tombstones included)
+int fold_derive(kvr_ctx *c, size_t nt, bool keep_del, bool index) {
     hipStream_t st = c->stream;
     const uint32_t g = (uint32_t)((nt + 255) / 256);
+    if (c->lout.ensure(nt) || (index && c->islots.ensure(c->fent.n))) return KVR_ENOMEM;
     HIPCHK(live_flags(c, nt, false, keep_del));
     size_t tb = c->ctmp.n;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->cflag.p, c->cpos.p, (int)nt, st));
-    uint32_t last[2] = {0, 0};
-    HIPCHK(hipMemcpyAsync(&last[0], c->cpos.p + nt - 1, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(&last[1], c->cflag.p + nt - 1, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    *total = (uint64_t)last[0] + last[1];
-    if (*total == 0) return KVR_OK;
-    if (c->lout.ensure(*total)) return KVR_ENOMEM;
     hipLaunchKernelGGL(k_live_tuples, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->cflag.p, c->cpos.p, c->lout.p);
+    if (index)
+        hipLaunchKernelGGL(k_index_from_fold, dim3(fold_grid(c)), dim3(256), 0, st, c->fent.p, c->fsz.p, c->cflag.p,
+                           c->cpos.p, c->islots.p);
     HIPCHK(hipGetLastError());
     return KVR_OK;
+}
+
+// fold_settle + fold_derive again if the deferred fold had to be redone; *total = n_live
+int derive_settle(kvr_ctx *c, size_t nt, bool keep_del, bool index, uint64_t *total) {
+    uint32_t last2[2] = {0, 0};
+    bool redone = false;
+    int rc = fold_settle(c, nt, &redone, last2);
+    if (rc == KVR_OK && redone) {
+        rc = fold_derive(c, nt, keep_del, index);
+        if (rc == KVR_OK) rc = fold_settle(c, nt, &redone, last2);   // (not pending: reads the totals)
+    }
+    *total = (uint64_t)last2[0] + last2[1];
+    return rc;
 }
 
 int index_copy_out(kvr_ctx *c, uint32_t flags, kvr_tuple *live, size_t live_cap, uint32_t *slots, uint64_t slot_cap) {
@@ -108,11 +120,14 @@ int replay_last(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, k
     c->ix_valid = false;
     size_t nt = 0;
     kvr_compact_stats cs{};
-    int rc = compact_front(c, segs, n, flags, err, &nt, false, &cs);   // replay + fold (kvr_compact.hip)
+    int rc = compact_front(c, segs, n, flags, err, &nt, false, &cs, true);   // replay + fold (kvr_compact.hip)
     if (rc != KVR_OK) return rc;
     uint64_t total = 0;
-    rc = live_list(c, nt, &total, keep_del);
-    if (rc != KVR_OK) return rc;
+    if (nt) {
+        rc = fold_derive(c, nt, keep_del, false);
+        if (rc == KVR_OK) rc = derive_settle(c, nt, keep_del, false, &total);
+        if (rc != KVR_OK) return rc;
+    }
     *n_out = total;
     c->ix_live = total;   // kvr_live_keys reads this live list
     c->ix_slots = 0;
@@ -154,29 +169,27 @@ int kvr_replay_index(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fla
     const auto t0 = std::chrono::steady_clock::now();
     size_t nt = 0;
     kvr_compact_stats cs{};
-    int rc = compact_front(c, segs, n, flags, err, &nt, false, &cs);
+    int rc = compact_front(c, segs, n, flags, err, &nt, false, &cs, true);   // deferred fold rounds
     c->istats.bytes_in = cs.bytes_in;
     c->istats.n_tuples = nt;
     c->istats.ms_replay = cs.ms_replay;
     if (rc != KVR_OK) return rc;
     uint64_t total = 0;
-    if (nt) {
-        rc = live_list(c, nt, &total);
-        if (rc != KVR_OK) return rc;
-    }
-    const uint64_t ns = nt ? c->fold_slots : 16;
-    if (c->islots.ensure(ns)) return KVR_ENOMEM;
     hipStream_t st = c->stream;
     if (nt) {
-        hipLaunchKernelGGL(k_index_from_fold, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, st, c->fent.p, ns,
-                           c->cflag.p, c->cpos.p, c->islots.p);
-        HIPCHK(hipGetLastError());
+        // the live list and the key table are launched behind the fold; one sync for all of it
+        rc = fold_derive(c, nt, false, true);
+        if (rc != KVR_OK) return rc;
+        HIPCHK(hipEventRecord(c->ev[4], st));
+        rc = derive_settle(c, nt, false, true, &total);
+        if (rc != KVR_OK) return rc;
+        c->istats.ms_fold = ev_ms(c->ev[0], c->ev[4]);   // fold rounds .. index table
     } else {
-        HIPCHK(hipMemsetAsync(c->islots.p, 0, ns * 4, st));
+        if (c->islots.ensure(16)) return KVR_ENOMEM;
+        HIPCHK(hipMemsetAsync(c->islots.p, 0, 16 * 4, st));
+        HIPCHK(hipStreamSynchronize(st));
     }
-    HIPCHK(hipEventRecord(c->ev[4], st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (nt) c->istats.ms_fold = ev_ms(c->ev[0], c->ev[4]);   // fold rounds .. index table
+    const uint64_t ns = nt ? c->fold_slots : 16;
     c->ix_live = total;
     c->ix_slots = ns;
     c->ix_valid = true;

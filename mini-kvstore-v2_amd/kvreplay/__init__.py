@@ -112,7 +112,11 @@ _host = None
 
 
 def lib_paths():
-    return os.path.join(_LIB, "libkvreplay.so"), os.path.join(_LIB, "libkvhost.so")
+    # KVREPLAY_VARIANT: a diagnostic build pair under lib/vpair (build.py build_variant_pair),
+    # timing tools only
+    v = os.environ.get("KVREPLAY_VARIANT")
+    d = os.path.join(_LIB, "vpair", v) if v else _LIB
+    return os.path.join(d, "libkvreplay.so"), os.path.join(d, "libkvhost.so")
 
 
 def _load():

@@ -66,6 +66,12 @@ for s in $STEPS; do
         timeout -k 10 120 python -u tools/ablate.py ${VCFG:-cfg2} 0 $v >> "$OUT/vars_${VCFG:-cfg2}.txt" 2>&1 || { echo "variant $v failed"; tail -20 "$OUT/vars_${VCFG:-cfg2}.txt"; exit 1; }
       done
       cat "$OUT/vars_${VCFG:-cfg2}.txt" ;;
+    foldv)    # tools/prof_index.py under each build pair named in $FOLDV (build.py build_variant_pair)
+      for v in ${FOLDV:-base}; do
+        echo "variant $v" >> "$OUT/foldv.txt"
+        KVREPLAY_VARIANT=$v timeout -k 10 120 python -u tools/prof_index.py ${VCFG:-cfg2} 6 >> "$OUT/foldv.txt" 2>&1 || { echo "foldv $v failed"; tail -20 "$OUT/foldv.txt"; exit 1; }
+      done
+      cat "$OUT/foldv.txt" ;;
     traffic)
       timeout -k 10 600 python -u tools/pmc_traffic.py > "$OUT/traffic.log" 2>&1 || { echo "traffic failed"; tail -20 "$OUT/traffic.log"; exit 1; }
       cp gpurun_out/pmc_traffic.json "$OUT/pmc_traffic.json" && tail -1 "$OUT/traffic.log" ;;
