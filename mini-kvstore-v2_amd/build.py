@@ -110,6 +110,9 @@ VARIANTS = {
     "nodefer": ["-DKVR_DEFER=0"],
     "foldnokey": ["-DKVR_FOLD_NOKEY"],
     "foldsplit": ["-DKVR_FOLD_MERGE=0"],   # every tag match verified by k_fold_verify   # fold kernels without key reads (timing bound only)   # long-value unit views updated in the hop loop   # unit loop with per-step register/data selects   # the hop loop with its separate range checks   # segmented scan with a multiply at every step   # slice-by-2 unit loop (two LDS round trips per word)
+    "pf": ["-DKVR_PF=1"],        # touch load of the next tile before the CRC phase (1.66 vs 1.64 ms, not kept)
+    "finr": ["-DKVR_FINR=1"],    # value-end tail bytes in one lookup round (A/B: 1.604 vs 1.589 ms, not kept)
+    "hop1": ["-DKVR_HOP2=0"],    # the single exact hop loop for every record (1.642 vs 1.604 ms)
     "base": [],
 }
 

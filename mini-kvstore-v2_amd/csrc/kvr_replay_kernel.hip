@@ -96,6 +96,12 @@ struct __align__(16) Smem {
 #ifndef KVR_DEFER   // 1: long-value unit views updated once per hop batch, not per hop
 #define KVR_DEFER 1
 #endif
+#ifndef KVR_HOP2   // 1: a fast hop loop for records read wholly from the registers, the exact loop after it
+#define KVR_HOP2 1
+#endif
+#ifndef KVR_FINR   // 1: a value end's last m & 3 bytes in one round of lookups (0: one round per byte)
+#define KVR_FINR 0
+#endif
 #ifndef KVR_XSCAN   // 1: pieces pushed to their consumer, XOR scan; 0: multiply at every scan step
 #define KVR_XSCAN 1
 #endif
@@ -547,6 +553,24 @@ __device__ __forceinline__ void load_unit(const uint8_t *abase, int64_t d0, uint
     }
 }
 
+// KVR_PF: one 4-B load per lane at its unit of tile k brings the tile's 128-B lines towards L2
+// while the CRC phase runs, so the unit load issued after it finds them on chip (the result is
+// only kept alive, never used)
+#ifndef KVR_PF
+#define KVR_PF 0
+#endif
+__device__ __forceinline__ uint32_t touch_unit(const uint8_t *abase, int64_t d0, uint64_t len, uint32_t k, int lane) {
+    const int64_t t0 = (int64_t)k * TILE;
+    const int64_t endw = (d0 + (int64_t)len + 15) & ~(int64_t)15;
+    int64_t nrec = endw - t0;
+    nrec = nrec < 0 ? 0 : (nrec > TILE ? TILE : nrec);
+    const uint64_t b = (uint64_t)(abase + t0);
+    const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)b), bhi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(((uint64_t)bhi << 32) | blo), (short)0, __builtin_amdgcn_readfirstlane((int)nrec), 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, lane * SC, 0, 0);
+}
+
 // the reads of tile k relative to its first byte (see TileSeg)
 __device__ __forceinline__ TileSeg tile_seg(const uint8_t *abase, const uint8_t *seg, int64_t d0, uint64_t len,
                                             uint32_t k) {
@@ -643,8 +667,10 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     unsigned long long prof_acc[16] = {};
 #endif
     if (KVR_BULK_LOWPRIO) __builtin_amdgcn_s_setprio(2);
+    uint32_t pf_sink = 0;   // KVR_PF: the touch load's result, kept alive until this wait
     for (;; ++k) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (KVR_PF) asm volatile("" ::"v"(pf_sink));
         KVR_STAMP(5);
         const bool in_stripe = k < sd.t_end;
         if (stop || (!in_stripe && !carry) || k >= sg.n_tiles) break;
@@ -906,11 +932,75 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     broke = brk != 0;
                     return q;
                 };
+#if KVR_HOP2
+                // KVR_HOP2: the fast loop takes only records whose header and value-length field sit
+                // in the registers and that pass every framing check; it stops before anything else
+                // (a field past the tile, a broken record), which the exact loop above then takes
+                // from the same position.  Nothing is written for a record before it is accepted, so
+                // each hop is two register reads, three range tests and the lane writes.
+                // the two words holding tile bytes [o, o + 8) (uniform o, o + 8 <= TILE): w[r] and
+                // w[r + 1] of lane o >> 7 moved under one register index, aligned in the vector unit
+                // (v_alignbyte takes the byte shift from o's low bits), then one readlane each; only
+                // a pair that wraps into the next lane (r = 31) goes through two separate reads
+                auto tpair = [&](int o, uint32_t &lo, uint32_t &hi) {
+                    const int r = (o >> 2) & 31, l = o >> 7;
+                    if (r != 31) {
+                        const uint32_t a = w[r], b = w[r + 1];
+                        lo = rl32(__builtin_amdgcn_alignbyte(b, a, (uint32_t)o), l);
+                        hi = rl32(b >> (8u * ((uint32_t)o & 3u)), l);
+                    } else {
+                        const uint64_t v = tu64(o);
+                        lo = (uint32_t)v;
+                        hi = (uint32_t)(v >> 32);
+                    }
+                };
+                auto hops_fast = [&](int32_t q) -> int32_t {
+                    const int32_t vhiT = (int32_t)vhi_r, remT = (int32_t)rem;
+                    const int32_t lim = remT < TILE - 4 ? remT : TILE - 4;   // e + 4 <= lim: vlen readable and inside the segment
+#pragma unroll 1
+                    for (;;) {
+                        if (((vhiT - 1 - q) | (63 - (int32_t)nb) | (TILE - 8 - q)) < 0) break;
+                        uint32_t x0, x1;
+                        tpair((int)q, x0, x1);
+                        const uint32_t op = x0 & 255u, klen = (uint32_t)((((uint64_t)x1 << 32) | x0) >> 8);
+                        // the value length is read for every record (a DEL ignores it), at a position
+                        // clamped into the registers: one exit test, no branch per record kind
+                        const uint32_t kk = __builtin_elementwise_min(klen, 0x40000000u);
+                        const uint32_t e = (uint32_t)q + 5u + kk, vb = e + 4u;
+                        uint32_t vraw, vhi_unused;
+                        tpair((int)__builtin_elementwise_min(e, (uint32_t)(TILE - 8)), vraw, vhi_unused);
+                        const uint32_t vlen = vraw & (op - 1u);   // (op 0: vraw, op 1: 0)
+                        // the tests as one sign: lim <= TILE - 4 and the key length clamped to 2^30
+                        // keep lim - vb inside int32; the value end is compared unsigned (vb < 2^31,
+                        // the value length clamped to 2^31 > remT, so a clamped length always fails)
+                        const uint32_t vv = __builtin_elementwise_min(vlen, 0x80000000u);
+                        const uint32_t vbad = vb + vv > (uint32_t)remT ? 0x80000000u : 0u;
+                        if ((int32_t)(((uint32_t)lim - vb) | vbad | (0u - (op >> 1))) < 0) break;
+                        const int32_t qn = (int32_t)(e + ((vlen + 4u) & (op - 1u)));
+                        if (vlen > (uint32_t)SMALL && ((vb ^ ((uint32_t)qn - 1u)) >> SC_LOG) != 0u) {   // vb < TILE here
+                            if (KVR_ABLATE & 32) any_long = true;
+                            else { lmark = wl32(lmark, nb + 1u, vb >> SC_LOG); bl = 1; }
+                        }
+                        myrec = (int32_t)wl32((uint32_t)myrec, (uint32_t)q, nb);
+                        my_op = wl32(my_op, op, nb);
+                        my_klen = wl32(my_klen, klen, nb);
+                        my_vlen = wl32(my_vlen, vlen, nb);
+                        ++nb;
+                        kmx = klen > kmx ? klen : kmx;
+                        q = qn;
+                    }
+                    return q;
+                };
+#endif
                 // the hop chain is the tile's serial critical path and shares the CU's scalar unit
                 // with 15 other waves: it issues at raised priority (KVR_HOP_PRIO)
                 if (KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
                 if (huge) p = hops((int64_t)p);
+#if KVR_HOP2
+                else p = hops((int32_t)hops_fast((int32_t)p));
+#else
                 else p = hops32((int32_t)p);
+#endif
                 if (KVR_DEFER && bl) {
                     // unit u's candidates: the batch's last long value starting in a unit <= u (it
                     // crosses u's end if it ends past ue) and the last one starting before u (it
@@ -1039,6 +1129,8 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             return is_abs ? ref : (ref < c1 ? b1 + ref : b2 + (ref - c1));
         };
         if (n_carry == 2u && !n_abs) n_ref = slot_of(n_ref, false);
+        if (KVR_PF && err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry))
+            pf_sink = touch_unit(abase, d0, len, k + 1, lane);
 
         KVR_STAMP(2);
         // ---- C. CRC of long values --------------------------------------------------------
@@ -1176,10 +1268,31 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             if (!(KVR_ABLATE & 16) && m != 0) {
                 const int r = m & 3;
                 uint32_t rp = snap, cf = kmul(sin, S.KQ + 128 * qm);
+#if KVR_FINR
+                // the last r < 4 bytes in one round of independent lookups: byte i of x = c ^ data
+                // goes through table r - 1 - i ("a byte then r - 1 - i zero bytes"), the rest of x
+                // is shifted past them
+                auto part = [&](uint32_t c, uint32_t d) -> uint32_t {
+                    const uint32_t x = c ^ (d & ((1u << (8 * r)) - 1u));
+                    uint32_t res = r ? x >> (8 * r) : x, tv[3];
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) {
+                        const int t = r - 1 - i;
+                        tv[i] = *reinterpret_cast<const uint32_t *>(
+                            K.t + ((((x >> (8 * i)) & 255u) << 8) | (32u * (uint32_t)(t < 0 ? 0 : t) + 4u * ((uint32_t)lane & 7u))));
+                    }
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) res ^= (r - 1 - i >= 0) ? tv[i] : 0u;
+                    return res;
+                };
+                rp = part(rp, wm);
+                cf = part(cf, 0u);
+#else
                 for (int b = 0; b < r; ++b) {
                     rp = crc1(rp, (wm >> (8 * b)) & 255u, K);
                     cf = crc1(cf, 0u, K);
                 }
+#endif
                 const uint64_t ms = slot_of(m_ref, m_abs);
                 if (ms < pool_cap) pool[ms].crc32 = ~(cf ^ rp);
             }
