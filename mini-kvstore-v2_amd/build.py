@@ -113,6 +113,7 @@ VARIANTS = {
     "pf": ["-DKVR_PF=1"],        # touch load of the next tile before the CRC phase (1.66 vs 1.64 ms, not kept)
     "finr": ["-DKVR_FINR=1"],    # value-end tail bytes in one lookup round (A/B: 1.604 vs 1.589 ms, not kept)
     "hop1": ["-DKVR_HOP2=0"],    # the single exact hop loop for every record (1.642 vs 1.604 ms)
+    "late": ["-DKVR_EARLY=0"],   # next tile loaded after the finalize
     "base": [],
 }
 

@@ -96,6 +96,9 @@ struct __align__(16) Smem {
 #ifndef KVR_DEFER   // 1: long-value unit views updated once per hop batch, not per hop
 #define KVR_DEFER 1
 #endif
+#ifndef KVR_EARLY   // 1: the next tile's load issued right after the unit loop (0: after the finalize)
+#define KVR_EARLY 1
+#endif
 #ifndef KVR_HOP2   // 1: a fast hop loop for records read wholly from the registers, the exact loop after it
 #define KVR_HOP2 1
 #endif
@@ -1132,6 +1135,8 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         if (KVR_PF && err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry))
             pf_sink = touch_unit(abase, d0, len, k + 1, lane);
 
+        // the stripe goes on past this tile (a value running past its end is carried on)
+        const bool need_next = err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry || out);
         KVR_STAMP(2);
         // ---- C. CRC of long values --------------------------------------------------------
         if (!(KVR_ABLATE & 2) && any_long) {
@@ -1180,6 +1185,12 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                 }
 #endif
                 sn = qm == UW ? cb : sn;
+            }
+            // KVR_EARLY: the unit loop was the tile registers' last reader, so the next tile's load
+            // is issued here and its latency runs under the scan and the finalize
+            if (KVR_EARLY && need_next) {
+                load_unit(abase, d0, len, k + 1, lane, w);
+                loaded = true;
             }
             // the piece of the value crossing the unit end: A pushed through B's bytes, then B
             // (A does not count when that value starts in B's half); the raw CRC of the first
@@ -1306,7 +1317,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
 
         if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(0);
         // the tile's registers are dead from here on: the next tile's load overlaps the rest
-        if (err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry)) {
+        if (!loaded && err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry)) {
             load_unit(abase, d0, len, k + 1, lane, w);
             loaded = true;
         }
