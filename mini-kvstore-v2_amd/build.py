@@ -114,6 +114,8 @@ VARIANTS = {
     "finr": ["-DKVR_FINR=1"],    # value-end tail bytes in one lookup round (A/B: 1.604 vs 1.589 ms, not kept)
     "hop1": ["-DKVR_HOP2=0"],    # the single exact hop loop for every record (1.642 vs 1.604 ms)
     "late": ["-DKVR_EARLY=0"],   # next tile loaded after the finalize
+    "rec1": ["-DKVR_LATEREC=1"],   # the last record batch after the unit loop (A/B 1.689 vs 1.601 ms: not kept)
+    "tres0": ["-DKVR_TRES_EARLY=0"],   # TileRes stored at the end of the tile
     "base": [],
 }
 

@@ -96,6 +96,12 @@ struct __align__(16) Smem {
 #ifndef KVR_DEFER   // 1: long-value unit views updated once per hop batch, not per hop
 #define KVR_DEFER 1
 #endif
+#ifndef KVR_LATEREC   // 1: the tile's last record batch emitted after the unit loop (key words loaded before it)
+#define KVR_LATEREC 0
+#endif
+#ifndef KVR_TRES_EARLY   // 1: the tile's TileRes stored before the CRC phase (0: at the end of the tile)
+#define KVR_TRES_EARLY 1
+#endif
 #ifndef KVR_EARLY   // 1: the next tile's load issued right after the unit loop (0: after the finalize)
 #define KVR_EARLY 1
 #endif
@@ -295,13 +301,21 @@ struct TileSeg {
 // raw CRC register (from ~0) over the n <= 4 NW bytes at offset o >= 0 (o + 4 NW + 4 <= lim),
 // and in *bad the 0x80 bits of those bytes; nw (wave-uniform) >= the words any lane needs
 template <int NW>
+__device__ __forceinline__ uint32_t crc_words(const uint32_t (&r)[NW + 1], const Crc &K, uint32_t sh, uint32_t n,
+                                              uint32_t nw, uint32_t *bad);
+template <int NW>
 __device__ __forceinline__ uint32_t crc_span(const TileSeg &ts, const Crc &K, int o, uint32_t n, uint32_t nw,
                                              uint32_t *bad) {
     const int a = o & ~3;
-    const uint32_t sh = (uint32_t)o & 3u;
     uint32_t r[NW + 1];
 #pragma unroll
     for (int i = 0; i <= NW; ++i) r[i] = (uint32_t)i <= nw ? ts.w32a(a + 4 * i) : 0u;
+    return crc_words<NW>(r, K, (uint32_t)o & 3u, n, nw, bad);
+}
+// the same over words already loaded: r[i] = the aligned word i of the span (sh = its start mod 4)
+template <int NW>
+__device__ __forceinline__ uint32_t crc_words(const uint32_t (&r)[NW + 1], const Crc &K, uint32_t sh, uint32_t n,
+                                              uint32_t nw, uint32_t *bad) {
     uint32_t c = ~0u, tail = 0, bd = 0;
 #pragma unroll
     for (int i = 0; i < NW; ++i) {
@@ -671,6 +685,13 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
 #endif
     if (KVR_BULK_LOWPRIO) __builtin_amdgcn_s_setprio(2);
     uint32_t pf_sink = 0;   // KVR_PF: the touch load's result, kept alive until this wait
+    // KVR_LATEREC: the tile's last record batch, emitted after the unit loop (its key words are
+    // loaded before it, so their latency runs under the loop)
+    bool pend = false;
+    int32_t pm_rec = -1;
+    uint32_t pm_op = 0, pm_klen = 0, pm_vlen = 0, pm_nw = 0, pm_nrec0 = 0;
+    uint64_t pm_slot = 0;
+    uint32_t kr[KEYW + 1];
     for (;; ++k) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (KVR_PF) asm volatile("" ::"v"(pf_sink));
@@ -1057,6 +1078,29 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                 uint32_t rerr = N32, rkind = 0;
                 uint64_t raux = 0;
                 const uint32_t j = nrec + (uint32_t)lane;
+#if KVR_LATEREC
+                // the tile's last batch, no broken record and no value the records phase must read
+                // (values in one unit or of at most SMALL bytes): its key words are loaded now and
+                // the records are emitted after the unit loop
+                const int32_t vb_ = myrec + 9 + (int32_t)my_klen;
+                const bool vmem = myrec >= 0 && my_op == 0u &&
+                                  (my_vlen <= (uint32_t)SMALL || (vb_ >> SC_LOG) == ((vb_ + (int32_t)my_vlen - 1) >> SC_LOG));
+                if (!(KVR_ABLATE & 1) && !huge && !broke && p >= vhi_r && !__ballot(vmem)) {
+                    pend = true;
+                    pm_rec = myrec; pm_op = my_op; pm_klen = my_klen; pm_vlen = my_vlen;
+                    pm_slot = slot; pm_nrec0 = nrec;
+                    const uint32_t kc = kmx > 4u * KEYW ? 4u * KEYW : kmx;
+                    pm_nw = (kc + 3u) >> 2;
+                    const int kb = myrec + 5;
+                    const bool kf = myrec >= 0 && my_klen <= 4u * KEYW && kb + 4 * KEYW + 8 <= ts.lim;
+                    const int ka = kf ? (kb & ~3) : 0;
+#pragma unroll
+                    for (int i = 0; i <= KEYW; ++i) kr[i] = (uint32_t)i <= pm_nw ? ts.w32a(ka + 4 * i) : 0u;
+                    nrec += nb;   // (an error found after the loop lowers it)
+                    if (KVR_REC_PRIO) __builtin_amdgcn_s_setprio(KVR_BULK_LOWPRIO ? 2 : 0);
+                    continue;
+                }
+#endif
                 if (!(KVR_ABLATE & 1) && myrec >= 0) {
                     if (broke && lane == (int)nb - 1) {   // the record that broke the chain: every check
                         const RecRes r = do_record(ts, K, myrec, j, slot, sd.seg, pool, pool_cap);
@@ -1127,6 +1171,17 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             tile_exit = broke ? ERRP : (uint64_t)(lo + p);
         }
         if (c1 == N32) c1 = nrec;
+        // the tile's result record; KVR_TRES_EARLY: stored here, ahead of the next tile's load, so
+        // that the wait for that load at the loop top does not also wait for this store's ack
+        auto store_tres = [&]() {
+            TileRes tr;
+            tr.pool_off = nrec ? b1 : 0ull;
+            tr.pool_off2 = b2;
+            tr.count = nrec;
+            tr.count1 = c1 < nrec ? c1 : nrec;
+            tres[sg.tile0 + k] = tr;
+        };
+        if (KVR_TRES_EARLY && !KVR_LATEREC && in_stripe && lane == 0) store_tres();
         // a record index of this tile -> its pool slot
         auto slot_of = [&](uint64_t ref, bool is_abs) -> uint64_t {
             return is_abs ? ref : (ref < c1 ? b1 + ref : b2 + (ref - c1));
@@ -1135,6 +1190,58 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         if (KVR_PF && err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry))
             pf_sink = touch_unit(abase, d0, len, k + 1, lane);
 
+        // KVR_LATEREC: the pending batch's records (key CRC from the preloaded words, tuples,
+        // the batch's first error), emitted before the finalize patches any of their crc32
+        auto rec2 = [&]() {
+            pend = false;
+            if (KVR_REC_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
+            uint32_t rerr = N32, rkind = 0;
+            uint64_t raux = 0;
+            const uint32_t j = pm_nrec0 + (uint32_t)lane;
+            if (pm_rec >= 0) {
+                const int kb = pm_rec + 5;
+                const uint32_t klen = pm_klen;
+                uint32_t c = ~0u, bad = 0x80u;
+                if (klen <= 4u * KEYW && kb + 4 * KEYW + 8 <= ts.lim) c = crc_words<KEYW>(kr, K, (uint32_t)kb & 3u, klen, pm_nw, &bad);
+                if (bad != 0u) {              // non-ASCII or long key: the full UTF-8 check
+                    uint64_t vu = 0;
+                    uint32_t el = 0;
+                    if (!utf8_check(ts, kb, klen, &vu, &el)) {   // engine.rs:114
+                        rerr = j; rkind = KVR_E_UTF8; raux = vu | ((uint64_t)el << 32);
+                    } else {
+                        c = crc_long(ts, ~0u, kb, klen, K);
+                    }
+                }
+                if (rerr == N32) {   // (a SET's value is long: its crc32 comes from the CRC phase)
+                    kvr_tuple t;
+                    t.rec_off = (uint64_t)(lo + pm_rec);
+                    t.seg_idx = sd.seg;
+                    t.key_len = klen;
+                    t.val_len = pm_op == 0u ? pm_vlen : 0u;
+                    t.crc32 = 0;
+                    t.key_tag = ~c;
+                    t.op = (uint8_t)pm_op;
+                    t.flags = 0;
+                    t.reserved = 0;
+                    if (pm_slot < pool_cap) pool[pm_slot] = t;
+                }
+            }
+            if (__ballot(rerr != N32)) {
+                uint32_t er = rerr;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) {
+                    const uint32_t o = __shfl_xor(er, d, 64);
+                    er = o < er ? o : er;
+                }
+                err_rec = uni32(er);
+                const int el = (int)(err_rec - pm_nrec0);
+                err_kind = rl32(rkind, el);
+                err_aux = rl64(raux, el);
+                err_pos = (uint64_t)(lo + (int64_t)(int32_t)rl32((uint32_t)pm_rec, el));
+                nrec = err_rec;
+            }
+            if (KVR_REC_PRIO) __builtin_amdgcn_s_setprio(0);
+        };
         // the stripe goes on past this tile (a value running past its end is carried on)
         const bool need_next = err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry || out);
         KVR_STAMP(2);
@@ -1192,6 +1299,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                 load_unit(abase, d0, len, k + 1, lane, w);
                 loaded = true;
             }
+            if (KVR_LATEREC && pend) rec2();
             // the piece of the value crossing the unit end: A pushed through B's bytes, then B
             // (A does not count when that value starts in B's half); the raw CRC of the first
             // 4 qm bytes: A's snapshot, or all of A pushed through 4 (qm - H) bytes, then B's
@@ -1315,6 +1423,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             }
         }
 
+        if (KVR_LATEREC && pend) rec2();   // (no long value touched the tile)
         if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(0);
         // the tile's registers are dead from here on: the next tile's load overlaps the rest
         if (!loaded && err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry)) {
@@ -1324,14 +1433,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         KVR_STAMP(3);
         // ---- bookkeeping ------------------------------------------------------------------
         if (in_stripe) {
-            if (lane == 0) {
-                TileRes tr;
-                tr.pool_off = nrec ? b1 : 0ull;
-                tr.pool_off2 = b2;
-                tr.count = nrec;
-                tr.count1 = c1 < nrec ? c1 : nrec;
-                tres[sg.tile0 + k] = tr;
-            }
+            if (!(KVR_TRES_EARLY && !KVR_LATEREC) && lane == 0) store_tres();
             total += nrec;
             if (walk) entry = tile_exit;
         }
