@@ -120,9 +120,13 @@ def main():
     if args.mode == "compact":
         return bench_compact(args, ctx, segs, seg_nos, seg_total, n_rec, desc, nseg, seg_bytes, world)
 
+    # the segment list is marshaled into the C ABI's kvr_segment array once (a native caller hands
+    # over its array; rebuilding 64 ctypes structs per call is harness time, not replay time)
+    seg_list = K.SegmentList(segs, seg_ids=seg_nos, on_device=True)
+
     def step():
-        r = ctx.replay(segs, seg_ids=seg_nos, expected=(manifest.data_ptr(), n_rec), expected_on_device=True,
-                       on_device=True, out_ptr=out.data_ptr(), cap=n_rec + 1024)
+        r = ctx.replay(seg_list, expected=(manifest.data_ptr(), n_rec), expected_on_device=True,
+                       out_ptr=out.data_ptr(), cap=n_rec + 1024)
         if r.status != 0:
             raise RuntimeError(f"replay failed: status {r.status} error {r.error and r.error.kind}")
         return r

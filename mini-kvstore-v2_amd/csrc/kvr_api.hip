@@ -64,6 +64,22 @@ struct DevBuf {
 };
 
 constexpr uint32_t REDO_GRID = 1024;
+constexpr size_t LC_CTR = 64;                     // Counters' offset in the link + counters block
+constexpr size_t LC_BYTES = 128;
+static_assert(sizeof(LinkResult) <= LC_CTR && LC_CTR + sizeof(Counters) <= LC_BYTES, "link + counters block");
+
+// wait for the work queued on st: a host spin on an event for up to 20 ms (a blocking wait wakes
+// tens of microseconds after a short pipeline ends), then a blocking wait
+hipError_t wait_stream(hipStream_t st, hipEvent_t ev) {
+    hipError_t e = hipEventRecord(ev, st);
+    if (e != hipSuccess) return e;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) return hipEventSynchronize(ev);
+    }
+}
 
 // k_replay keeps 32-bit pool slots in LDS; KVR_POOL_LIMIT lowers the limit (test knob)
 uint64_t pool_limit() {
@@ -123,8 +139,16 @@ struct kvr_ctx {
     DevBuf<uint64_t> r_best, r_hk;
     LinkResult *h_link = nullptr;
     Counters *h_ctr = nullptr;
+    // link result and counters share one device allocation (one memset, one copy back per call)
+    // and one pinned host block
+    DevBuf<uint8_t> lcbuf;
+    uint8_t *h_lc = nullptr;
     std::vector<SegDesc> h_segs;
     std::vector<StripeDesc> h_stripes;
+    // the descriptors last uploaded to segs / stripes: a call over the same segments skips the copy
+    std::vector<SegDesc> up_segs;
+    std::vector<StripeDesc> up_stripes;
+    const void *up_segs_p = nullptr, *up_stripes_p = nullptr;
     uint64_t pool_hint = 0;
     uint64_t pool_need = 0;                // > 0: the last replay needed more than 32-bit pool slots
     uint32_t tps_override = 0;
@@ -271,15 +295,20 @@ int kvr_ctx_create(int device, kvr_ctx **out) {
     if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return KVR_EHIP; }
     c->stream = c->own;
     for (auto &e : c->ev) if (hipEventCreate(&e) != hipSuccess) { delete c; return KVR_EHIP; }
-    if (hipHostMalloc(reinterpret_cast<void **>(&c->h_link), sizeof(LinkResult)) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void **>(&c->h_ctr), sizeof(Counters)) != hipSuccess) { delete c; return KVR_ENOMEM; }
+    if (hipHostMalloc(reinterpret_cast<void **>(&c->h_lc), LC_BYTES) != hipSuccess) { delete c; return KVR_ENOMEM; }
+    c->h_link = reinterpret_cast<LinkResult *>(c->h_lc);
+    c->h_ctr = reinterpret_cast<Counters *>(c->h_lc + LC_CTR);
     std::vector<uint32_t> crc, kmul, initx;
     build_tables(crc, kmul, initx);
     if (c->crc.ensure(crc.size()) || c->kmul.ensure(kmul.size()) || c->initx.ensure(initx.size()) ||
-        c->link.ensure(1) || c->ctr.ensure(1)) {
+        c->lcbuf.ensure(LC_BYTES)) {
         kvr_ctx_destroy(c);
         return KVR_ENOMEM;
     }
+    c->link.p = reinterpret_cast<LinkResult *>(c->lcbuf.p);
+    c->link.n = 1;
+    c->ctr.p = reinterpret_cast<Counters *>(c->lcbuf.p + LC_CTR);
+    c->ctr.n = 1;
     if (hipMemcpy(c->crc.p, crc.data(), crc.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->kmul.p, kmul.data(), kmul.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->initx.p, initx.data(), initx.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
@@ -295,7 +324,9 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->arena.release(); c->segs.release(); c->stripes.release(); c->sres.release(); c->tres.release();
-    c->pool.release(); c->dense.release(); c->redo.release(); c->link.release(); c->ctr.release();
+    c->pool.release(); c->dense.release(); c->redo.release();
+    c->link.p = nullptr; c->ctr.p = nullptr;   // (inside lcbuf)
+    c->lcbuf.release();
     c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->bsum.release();
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
     c->ctup.release(); c->lout.release(); c->fent.release(); c->flist.release(); c->fcnt.release(); c->fsz.release();
@@ -315,8 +346,7 @@ void kvr_ctx_destroy(kvr_ctx *c) {
         if (c->ev_copy[i]) (void)hipEventDestroy(c->ev_copy[i]);
     }
     if (c->copy) (void)hipStreamDestroy(c->copy);
-    if (c->h_link) (void)hipHostFree(c->h_link);
-    if (c->h_ctr) (void)hipHostFree(c->h_ctr);
+    if (c->h_lc) (void)hipHostFree(c->h_lc);
     for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -481,8 +511,19 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         c->tres.ensure(n_tiles) || c->redo.ensure(std::max<uint32_t>(n_stripes, REDO_GRID)) ||
         c->seg_bad.ensure(n) || c->seg_err.ensure(n))
         return KVR_ENOMEM;
-    HIPCHK(hipMemcpyAsync(c->segs.p, c->h_segs.data(), n * sizeof(SegDesc), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(c->stripes.p, c->h_stripes.data(), n_stripes * sizeof(StripeDesc), hipMemcpyHostToDevice, st));
+    // (the same segments as the last call: the descriptors on the device are still these)
+    if (c->up_segs_p != c->segs.p || c->up_segs.size() != n ||
+        memcmp(c->up_segs.data(), c->h_segs.data(), n * sizeof(SegDesc)) != 0) {
+        HIPCHK(hipMemcpyAsync(c->segs.p, c->h_segs.data(), n * sizeof(SegDesc), hipMemcpyHostToDevice, st));
+        c->up_segs = c->h_segs;
+        c->up_segs_p = c->segs.p;
+    }
+    if (c->up_stripes_p != c->stripes.p || c->up_stripes.size() != n_stripes ||
+        memcmp(c->up_stripes.data(), c->h_stripes.data(), n_stripes * sizeof(StripeDesc)) != 0) {
+        HIPCHK(hipMemcpyAsync(c->stripes.p, c->h_stripes.data(), n_stripes * sizeof(StripeDesc), hipMemcpyHostToDevice, st));
+        c->up_stripes = c->h_stripes;
+        c->up_stripes_p = c->stripes.p;
+    }
 
     const uint32_t nb = (n_tiles + CB - 1) / CB;
     if (c->bsum.ensure(nb)) return KVR_ENOMEM;
@@ -520,8 +561,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             d_out = c->dense.p;
             out_cap = pool_cap;
         }
-        HIPCHK(hipMemsetAsync(c->ctr.p, 0, sizeof(Counters), st));
-        HIPCHK(hipMemsetAsync(c->link.p, 0, sizeof(LinkResult), st));
+        HIPCHK(hipMemsetAsync(c->lcbuf.p, 0, LC_BYTES, st));   // counters and link result
         HIPCHK(hipEventRecord(c->ev[0], st));
         hipLaunchKernelGGL(KR_KERNEL, dim3((n_stripes + KR_WPB - 1) / KR_WPB), dim3(KR_RT), 0, st, c->segs.p, c->stripes.p, n_stripes,
                            c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, c->redo.p, c->link.p, 0, pool_chunk);
@@ -539,9 +579,8 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
                            d_out, out_cap, d_exp, (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[3], st));
-        HIPCHK(hipMemcpyAsync(c->h_link, c->link.p, sizeof(LinkResult), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
+        HIPCHK(hipMemcpyAsync(c->h_lc, c->lcbuf.p, LC_BYTES, hipMemcpyDeviceToHost, st));   // link result + counters
+        HIPCHK(wait_stream(st, c->ev[5]));
         c->stats.ms_replay = ev_ms(c->ev[0], c->ev[1]);
         c->stats.ms_link = ev_ms(c->ev[1], c->ev[2]);
         c->stats.ms_compact = ev_ms(c->ev[2], c->ev[3]);

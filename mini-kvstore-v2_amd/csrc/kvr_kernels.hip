@@ -144,6 +144,9 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
 // ---------------------------------------------------------------------------------------
 // Scan of per-tile counts and the ordered gather pool -> out.
 // ---------------------------------------------------------------------------------------
+#ifndef KVR_COMPACT16   // 1: k_compact moves 16-B halves of tuples (0: one 32-B tuple per thread)
+#define KVR_COMPACT16 1
+#endif
 constexpr int CT = 256;           // threads per compaction block
 constexpr int CPT = 1;            // tiles per thread
 constexpr int CB = CT * CPT;      // tiles per compaction block
@@ -223,6 +226,31 @@ __global__ __launch_bounds__(CT) void k_compact(const TileRes *__restrict__ tres
     const uint32_t nt = min((uint32_t)CB, n_tiles - tb);
     const uint64_t btotal = (tb + nt - 1 < n_tiles ? off[nt - 1] + tres[tb + nt - 1].count : b0) - b0;
     uint32_t fails = 0;
+#if KVR_COMPACT16
+    // 16-B items: thread k2 moves half k2 & 1 of tuple k2 >> 1, so a wave's loads and stores are
+    // 1 KiB contiguous; the second half holds val_len, crc32, key_tag, op and flags, so its thread
+    // also does the expected-CRC check
+    for (uint64_t k2 = threadIdx.x; k2 < 2 * btotal; k2 += CT) {
+        const uint64_t k = k2 >> 1;
+        const uint32_t half = (uint32_t)k2 & 1u;
+        uint32_t lo_i = 0, hi_i = nt - 1;       // last tile i with off[i] - b0 <= k
+        while (lo_i < hi_i) {
+            const uint32_t mid = (lo_i + hi_i + 1) >> 1;
+            if (off[mid] - b0 <= k) lo_i = mid; else hi_i = mid - 1;
+        }
+        const uint64_t o = b0 + k;
+        const TileRes &tr = tres[tb + lo_i];
+        const uint64_t r = o - off[lo_i];
+        const uint64_t src = r < tr.count1 ? tr.pool_off + r : tr.pool_off2 + (r - tr.count1);
+        if (src >= pool_cap) continue;
+        uint4 v = reinterpret_cast<const uint4 *>(pool + src)[half];
+        if (half && expected && o < n_expected && (v.w & 255u) == 0u) {   // a SET: op in byte 0 of w
+            v.w |= KVR_TF_VERIFIED << 8;
+            if (expected[o] != v.y) { v.w |= KVR_TF_CRC_FAIL << 8; ++fails; }
+        }
+        if (o < out_cap) reinterpret_cast<uint4 *>(out + o)[half] = v;
+    }
+#else
     for (uint64_t k = threadIdx.x; k < btotal; k += CT) {
         uint32_t lo_i = 0, hi_i = nt - 1;       // last tile i with off[i] - b0 <= k
         while (lo_i < hi_i) {
@@ -241,6 +269,7 @@ __global__ __launch_bounds__(CT) void k_compact(const TileRes *__restrict__ tres
         }
         if (o < out_cap) out[o] = tp;
     }
+#endif
     for (int d = 32; d >= 1; d >>= 1) fails += __shfl_xor(fails, d, 64);
     if (lane == 0 && fails) atomicAdd(&ctr->crc_fail, (unsigned long long)fails);
 }

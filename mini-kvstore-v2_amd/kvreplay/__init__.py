@@ -425,6 +425,32 @@ class MultiContext:
         return ReplayResult(rc, tuples, n_out.value, err if rc == CORRUPTED else None, self.last_stats())
 
 
+class SegmentList:
+    """A segment list marshaled once into the kvr_segment array of the C ABI, for callers that
+    replay the same segments repeatedly (Context.replay accepts it in place of a list; the
+    segment bytes must stay alive and unchanged).  on_device: (ptr, len) pairs in HBM."""
+
+    def __init__(self, segments, seg_ids=None, on_device=False):
+        self.n = len(segments)
+        self.on_device = on_device
+        self.keep = []
+        self.arr = (Segment * max(self.n, 1))()
+        self.total = 0
+        for i, s in enumerate(segments):
+            sid = seg_ids[i] if seg_ids is not None else i
+            if on_device:
+                ptr, ln = s
+            else:
+                a = np.frombuffer(s, dtype=np.uint8) if isinstance(s, (bytes, bytearray)) else np.ascontiguousarray(s)
+                self.keep.append(a)
+                ptr, ln = (a.ctypes.data if a.size else None), a.size
+            self.arr[i] = Segment(sid, ptr, ln)
+            self.total += ln
+
+    def __len__(self):
+        return self.n
+
+
 class Context:
     """One kvr_ctx on one HIP device."""
 
@@ -464,21 +490,12 @@ class Context:
                expected_on_device=False):
         """Replay host segments (list of bytes / uint8 arrays), or device segments given as
         (ptr, len) pairs with on_device=True.  Returns ReplayResult; tuples is a numpy
-        TUPLE_DTYPE array unless out_ptr (device memory) is given."""
-        n = len(segments)
-        keep = []
-        segs = (Segment * max(n, 1))()
-        total = 0
-        for i, s in enumerate(segments):
-            sid = seg_ids[i] if seg_ids is not None else i
-            if on_device:
-                ptr, ln = s
-            else:
-                a = np.frombuffer(s, dtype=np.uint8) if isinstance(s, (bytes, bytearray)) else np.ascontiguousarray(s)
-                keep.append(a)
-                ptr, ln = (a.ctypes.data if a.size else None), a.size
-            segs[i] = Segment(sid, ptr, ln)
-            total += ln
+        TUPLE_DTYPE array unless out_ptr (device memory) is given.  segments may be a
+        SegmentList (marshaled once; its on_device flag applies)."""
+        if not isinstance(segments, SegmentList):
+            segments = SegmentList(segments, seg_ids, on_device)
+        n, segs, total, on_device = segments.n, segments.arr, segments.total, segments.on_device
+        keep = [segments]
         flags = (SEGS_ON_DEVICE if on_device else 0)
         exp_ptr, n_exp = None, 0
         if expected is not None:
