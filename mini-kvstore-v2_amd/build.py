@@ -116,7 +116,8 @@ VARIANTS = {
     "late": ["-DKVR_EARLY=0"],   # next tile loaded after the finalize
     "rec1": ["-DKVR_LATEREC=1"],   # the last record batch after the unit loop (A/B 1.689 vs 1.601 ms: not kept)
     "tres0": ["-DKVR_TRES_EARLY=0"],   # TileRes stored at the end of the tile
-    "cmp32": ["-DKVR_COMPACT16=0"],   # k_compact with one 32-B tuple per thread
+    "cmp32": ["-DKVR_COMPACT16=0", "-DKVR_CSTRIPE=0"],   # k_compact with one 32-B tuple per thread
+    "ctile": ["-DKVR_CSTRIPE=0"],   # compaction by 256-tile blocks after a scan of tile counts
     "base": [],
 }
 

@@ -64,6 +64,9 @@ struct DevBuf {
 };
 
 constexpr uint32_t REDO_GRID = 1024;
+#ifndef KVR_CSTRIPE   // 1: compaction per stripe from k_link's stripe offsets (0: k_tsum + k_tscan + k_compact)
+#define KVR_CSTRIPE 1
+#endif
 constexpr size_t LC_CTR = 64;                     // Counters' offset in the link + counters block
 constexpr size_t LC_BYTES = 128;
 static_assert(sizeof(LinkResult) <= LC_CTR && LC_CTR + sizeof(Counters) <= LC_BYTES, "link + counters block");
@@ -111,6 +114,7 @@ struct kvr_ctx {
     DevBuf<Counters> ctr;
     DevBuf<uint32_t> seg_bad, seg_err, expected;
     DevBuf<uint64_t> bsum;
+    DevBuf<uint64_t> soff;                 // each stripe's output offset (k_link, for k_compact_s)
     DevBuf<uint32_t> crc, kmul, initx;
     DevBuf<GenRecDev> gen;
     // compaction (kvr_compact)
@@ -327,7 +331,7 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->pool.release(); c->dense.release(); c->redo.release();
     c->link.p = nullptr; c->ctr.p = nullptr;   // (inside lcbuf)
     c->lcbuf.release();
-    c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->bsum.release();
+    c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->bsum.release(); c->soff.release();
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
     c->ctup.release(); c->lout.release(); c->fent.release(); c->flist.release(); c->fcnt.release(); c->fsz.release();
     c->cslot.release(); c->cflag.release(); c->islots.release(); c->ing.release(); c->hpart.release(); c->hreg.release();
@@ -509,7 +513,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
 
     if (c->segs.ensure(n) || c->stripes.ensure(n_stripes) || c->sres.ensure(n_stripes) ||
         c->tres.ensure(n_tiles) || c->redo.ensure(std::max<uint32_t>(n_stripes, REDO_GRID)) ||
-        c->seg_bad.ensure(n) || c->seg_err.ensure(n))
+        c->seg_bad.ensure(n) || c->seg_err.ensure(n) || c->soff.ensure(n_stripes))
         return KVR_ENOMEM;
     // (the same segments as the last call: the descriptors on the device are still these)
     if (c->up_segs_p != c->segs.p || c->up_segs.size() != n ||
@@ -561,6 +565,20 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             d_out = c->dense.p;
             out_cap = pool_cap;
         }
+        // the ordered gather pool -> output: one workgroup per stripe from the stripe offsets k_link
+        // computes (KVR_CSTRIPE), or the scan of per-tile counts then a workgroup per 256 tiles
+        auto launch_compact = [&]() {
+            if (KVR_CSTRIPE) {
+                hipLaunchKernelGGL(k_compact_s, dim3(n_stripes), dim3(CT), 0, st, c->segs.p, c->stripes.p, c->soff.p,
+                                   c->tres.p, c->pool.p, pool_cap, d_out, out_cap, d_exp,
+                                   (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p);
+            } else {
+                hipLaunchKernelGGL(k_tsum, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->link.p);
+                hipLaunchKernelGGL(k_tscan, dim3(1), dim3(1024), 0, st, c->bsum.p, nb, c->ctr.p, c->link.p);
+                hipLaunchKernelGGL(k_compact, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->pool.p, pool_cap,
+                                   d_out, out_cap, d_exp, (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p);
+            }
+        };
         HIPCHK(hipMemsetAsync(c->lcbuf.p, 0, LC_BYTES, st));   // counters and link result
         HIPCHK(hipEventRecord(c->ev[0], st));
         hipLaunchKernelGGL(KR_KERNEL, dim3((n_stripes + KR_WPB - 1) / KR_WPB), dim3(KR_RT), 0, st, c->segs.p, c->stripes.p, n_stripes,
@@ -568,15 +586,13 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[1], st));
         hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
-                           c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p, (uint32_t)KR_TILE);
+                           c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p, (uint32_t)KR_TILE,
+                           c->soff.p, c->ctr.p);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[2], st));
         // compaction is launched right away: it does nothing unless linking succeeded (status 0),
         // which is the common case; otherwise the host re-walks and compacts again below
-        hipLaunchKernelGGL(k_tsum, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->link.p);
-        hipLaunchKernelGGL(k_tscan, dim3(1), dim3(1024), 0, st, c->bsum.p, nb, c->ctr.p, c->link.p);
-        hipLaunchKernelGGL(k_compact, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->pool.p, pool_cap,
-                           d_out, out_cap, d_exp, (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p);
+        launch_compact();
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[3], st));
         HIPCHK(hipMemcpyAsync(c->h_lc, c->lcbuf.p, LC_BYTES, hipMemcpyDeviceToHost, st));   // link result + counters
@@ -616,7 +632,8 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
                                0, st, c->segs.p, c->stripes.p, n_stripes, c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p,
                                tb, c->redo.p, c->link.p, 1, pool_chunk);
             hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes,
-                               c->sres.p, c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p, (uint32_t)KR_TILE);
+                               c->sres.p, c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p, (uint32_t)KR_TILE,
+                               c->soff.p, c->ctr.p);
             HIPCHK(hipGetLastError());
             HIPCHK(hipMemcpyAsync(c->h_link, c->link.p, sizeof(LinkResult), hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, st));
@@ -651,10 +668,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             return KVR_EHIP;
         }
         if (recompact && c->h_link->status == 0 && !c->h_ctr->overflow) {
-            hipLaunchKernelGGL(k_tsum, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->link.p);
-            hipLaunchKernelGGL(k_tscan, dim3(1), dim3(1024), 0, st, c->bsum.p, nb, c->ctr.p, c->link.p);
-            hipLaunchKernelGGL(k_compact, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->pool.p, pool_cap,
-                               d_out, out_cap, d_exp, (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p);
+            launch_compact();
             HIPCHK(hipGetLastError());
             HIPCHK(hipMemcpyAsync(c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));

@@ -34,25 +34,48 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
                                              const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
                                              const StripeRes *__restrict__ sres, RedoEnt *__restrict__ redo,
                                              uint32_t redo_cap, LinkResult *res, uint32_t *seg_bad,
-                                             uint32_t *seg_err, uint32_t tile) {
-    __shared__ int32_t cm[LT];
+                                             uint32_t *seg_err, uint32_t tile, uint64_t *__restrict__ soff,
+                                             Counters *ctr) {
+    __shared__ int32_t wm[LT / 64];
+    __shared__ unsigned long long wsum[LT / 64];
     __shared__ uint32_t first_problem, nredo;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (uint32_t g = tid; g < n_segs; g += LT) { seg_bad[g] = ~0u; seg_err[g] = ~0u; }
     if (tid == 0) { first_problem = ~0u; nredo = 0; }
     const uint32_t per = (n_stripes + LT - 1) / LT;
     const uint32_t b = tid * per, e = min(b + per, n_stripes);
+    // this thread's chunk: its last stripe with a record start, and its stripes' records (the
+    // output offsets k_compact_s writes from); exclusive scans over the chunks, a max and a sum,
+    // by wave shuffles and then the 16 wave totals
     int32_t m = -1;
-    for (uint32_t s = b; s < e; ++s) if (sres[s].entry != NONE) m = (int32_t)s;
-    cm[tid] = m;
-    __syncthreads();
-    for (int d = 1; d < LT; d <<= 1) {   // inclusive max-scan of chunk maxima
-        const int32_t o = tid >= d ? cm[tid - d] : -1;
-        __syncthreads();
-        if (o > cm[tid]) cm[tid] = o;
-        __syncthreads();
+    unsigned long long mine = 0;
+    for (uint32_t s = b; s < e; ++s) {
+        if (sres[s].entry != NONE) m = (int32_t)s;
+        mine += sres[s].count;
     }
-    const int32_t run0 = tid ? cm[tid - 1] : -1;
+    int32_t im = m;
+    unsigned long long is = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int32_t om = __shfl_up(im, d, 64);
+        const unsigned long long os = __shfl_up(is, d, 64);
+        if (lane >= d) { im = om > im ? om : im; is += os; }
+    }
+    if (lane == 63) { wm[wv] = im; wsum[wv] = is; }
+    __syncthreads();
+    int32_t pm = -1;
+    unsigned long long ps = 0, all_recs = 0;
+    for (int i = 0; i < LT / 64; ++i) {
+        if (i < wv) { pm = wm[i] > pm ? wm[i] : pm; ps += wsum[i]; }
+        all_recs += wsum[i];
+    }
+    const int32_t xm = __shfl_up(im, 1, 64);
+    const unsigned long long xs = __shfl_up(is, 1, 64);
+    const int32_t run0 = lane ? (xm > pm ? xm : pm) : pm;   // the last stripe with records before the chunk
+    if (soff) {
+        unsigned long long at = (lane ? xs : 0ull) + ps;
+        for (uint32_t s = b; s < e; ++s) { soff[s] = at; at += sres[s].count; }
+    }
 
     // pass 1: consistency of every stripe with its predecessor's exit
     int32_t run = run0;
@@ -129,6 +152,7 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
             L.status = 3;
         } else if (fe == ~0u) {
             L.status = 0;
+            if (soff) ctr->total_tuples = all_recs;
         } else {
             const StripeRes r = sres[__hip_atomic_load(&seg_err[fe], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)];
             L.status = 1;
@@ -272,6 +296,66 @@ __global__ __launch_bounds__(CT) void k_compact(const TileRes *__restrict__ tres
 #endif
     for (int d = 32; d >= 1; d >>= 1) fails += __shfl_xor(fails, d, 64);
     if (lane == 0 && fails) atomicAdd(&ctr->crc_fail, (unsigned long long)fails);
+}
+
+// One workgroup per stripe (the stripe's output offset from k_link, so no separate scan of the
+// tile counts): the stripe's tiles in chunks of CB, each chunk's tile offsets scanned in LDS,
+// its tuples moved as 16-B halves (see k_compact) with the expected-CRC check.
+__global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ segs, const StripeDesc *__restrict__ stripes,
+                                                  const uint64_t *__restrict__ soff, const TileRes *__restrict__ tres,
+                                                  const kvr_tuple *__restrict__ pool, uint64_t pool_cap,
+                                                  kvr_tuple *__restrict__ out, uint64_t out_cap,
+                                                  const uint32_t *__restrict__ expected, uint64_t n_expected,
+                                                  Counters *ctr, const LinkResult *__restrict__ link) {
+    if (link->status != 0 || ctr->overflow) return;
+    __shared__ uint64_t off[CB + 1];
+    __shared__ uint64_t part[CT];
+    const StripeDesc sd = stripes[blockIdx.x];
+    const uint32_t tile0 = segs[sd.seg].tile0;
+    const uint32_t t_end = tile0 + sd.t_end;
+    uint64_t carry = soff[blockIdx.x];
+    uint32_t fails = 0;
+    for (uint32_t tb = tile0 + sd.t_begin; tb < t_end; tb += CB) {
+        const uint32_t nt = min((uint32_t)CB, t_end - tb);
+        const uint32_t t = tb + threadIdx.x;
+        const uint64_t cnt = threadIdx.x < nt ? tres[t].count : 0u;
+        part[threadIdx.x] = cnt;
+        __syncthreads();
+        for (int d = 1; d < CT; d <<= 1) {
+            const uint64_t o = threadIdx.x >= (uint32_t)d ? part[threadIdx.x - d] : 0ull;
+            __syncthreads();
+            part[threadIdx.x] += o;
+            __syncthreads();
+        }
+        off[threadIdx.x] = carry + part[threadIdx.x] - cnt;
+        const uint64_t ctotal = part[CT - 1];
+        __syncthreads();
+        const uint64_t b0 = carry;
+        for (uint64_t k2 = threadIdx.x; k2 < 2 * ctotal; k2 += CT) {
+            const uint64_t k = k2 >> 1;
+            const uint32_t half = (uint32_t)k2 & 1u;
+            uint32_t lo_i = 0, hi_i = nt - 1;       // last tile i with off[i] - b0 <= k
+            while (lo_i < hi_i) {
+                const uint32_t mid = (lo_i + hi_i + 1) >> 1;
+                if (off[mid] - b0 <= k) lo_i = mid; else hi_i = mid - 1;
+            }
+            const uint64_t o = b0 + k;
+            const TileRes &tr = tres[tb + lo_i];
+            const uint64_t r = o - off[lo_i];
+            const uint64_t src = r < tr.count1 ? tr.pool_off + r : tr.pool_off2 + (r - tr.count1);
+            if (src >= pool_cap) continue;
+            uint4 v = reinterpret_cast<const uint4 *>(pool + src)[half];
+            if (half && expected && o < n_expected && (v.w & 255u) == 0u) {   // a SET: op in byte 0 of w
+                v.w |= KVR_TF_VERIFIED << 8;
+                if (expected[o] != v.y) { v.w |= KVR_TF_CRC_FAIL << 8; ++fails; }
+            }
+            if (o < out_cap) reinterpret_cast<uint4 *>(out + o)[half] = v;
+        }
+        carry += ctotal;
+        __syncthreads();   // (off and part are rewritten by the next chunk)
+    }
+    for (int d = 32; d >= 1; d >>= 1) fails += __shfl_xor(fails, d, 64);
+    if ((threadIdx.x & 63) == 0 && fails) atomicAdd(&ctr->crc_fail, (unsigned long long)fails);
 }
 
 // ---------------------------------------------------------------------------------------
