@@ -102,7 +102,9 @@ VARIANTS = {
     "v8": ["-DKVR_KERNEL_V8"],
     "prio0": ["-DKVR_HOP_PRIO=0", "-DKVR_REC_PRIO=0"],   # wave priority off
     "bulklow": ["-DKVR_BULK_LOWPRIO=1"],
-    "fin1": ["-DKVR_FIN_PRIO=1"],
+    "fin0": ["-DKVR_FIN_PRIO=0"],
+    "fin2": ["-DKVR_FIN_PRIO=2"],
+    "fin1rp2": ["-DKVR_REC_PRIO=2"],
     "s2": ["-DKVR_S4=0"],
     "kscan": ["-DKVR_XSCAN=0"],
     "hopold": ["-DKVR_HOPFAST=0"],
@@ -118,6 +120,9 @@ VARIANTS = {
     "tres0": ["-DKVR_TRES_EARLY=0"],   # TileRes stored at the end of the tile
     "cmp32": ["-DKVR_COMPACT16=0", "-DKVR_CSTRIPE=0"],   # k_compact with one 32-B tuple per thread
     "ctile": ["-DKVR_CSTRIPE=0"],   # compaction by 256-tile blocks after a scan of tile counts
+    "rp2": ["-DKVR_REC_PRIO=2"],
+    "rp0": ["-DKVR_REC_PRIO=0"],
+    "hp3": ["-DKVR_HOP_PRIO=3", "-DKVR_REC_PRIO=2"],
     "base": [],
 }
 

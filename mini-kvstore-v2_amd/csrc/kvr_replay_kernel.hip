@@ -81,8 +81,8 @@ struct __align__(16) Smem {
 #ifndef KVR_REC_PRIO
 #define KVR_REC_PRIO 1
 #endif
-#ifndef KVR_FIN_PRIO       // experiment: the scan + finalize chain raised too
-#define KVR_FIN_PRIO 0
+#ifndef KVR_FIN_PRIO       // the scan + finalize chain raised too (with the next tile's load issued before it:
+#define KVR_FIN_PRIO 1     // cfg2 1.552 vs 1.580 ms A/B)
 #endif
 #ifndef KVR_BULK_LOWPRIO   // experiment: every phase raised except the unit CRC loop
 #define KVR_BULK_LOWPRIO 0
