@@ -120,9 +120,7 @@ VARIANTS = {
     "tres0": ["-DKVR_TRES_EARLY=0"],   # TileRes stored at the end of the tile
     "cmp32": ["-DKVR_COMPACT16=0", "-DKVR_CSTRIPE=0"],   # k_compact with one 32-B tuple per thread
     "ctile": ["-DKVR_CSTRIPE=0"],   # compaction by 256-tile blocks after a scan of tile counts
-    "rp2": ["-DKVR_REC_PRIO=2"],
-    "rp0": ["-DKVR_REC_PRIO=0"],
-    "hp3": ["-DKVR_HOP_PRIO=3", "-DKVR_REC_PRIO=2"],
+    "xf1": ["-DKVR_XFUSE=1"],   # unit-loop registers as two XOR terms (A/B 1.661 vs 1.579 ms: not kept)
     "base": [],
 }
 

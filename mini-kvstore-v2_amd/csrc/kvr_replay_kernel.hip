@@ -105,6 +105,9 @@ struct __align__(16) Smem {
 #ifndef KVR_EARLY   // 1: the next tile's load issued right after the unit loop (0: after the finalize)
 #define KVR_EARLY 1
 #endif
+#ifndef KVR_XFUSE   // 1: unit-loop registers as two XOR terms, the next input one v_bitop3 (0: materialized;
+#define KVR_XFUSE 0  // A/B: cfg2 1.661 vs 1.579 ms, cfg3 2.073 vs 2.089: not kept)
+#endif
 #ifndef KVR_HOP2   // 1: a fast hop loop for records read wholly from the registers, the exact loop after it
 #define KVR_HOP2 1
 #endif
@@ -236,6 +239,20 @@ __device__ __forceinline__ void crc4x2(uint32_t &ca, uint32_t wa, uint32_t &cb, 
     ca = xa;
     cb = xb;
 #endif
+}
+// KVR_XFUSE: two chains' slice-by-4 step from their inputs x = register ^ data, each new register
+// kept as two terms t ^ u (three lookups XORed, the fourth alone), so the next step's input
+// t ^ u ^ data is one v_bitop3 instead of two XORs
+__device__ __forceinline__ void step4x2(uint32_t xa, uint32_t xb, const Crc &k, uint32_t &ta, uint32_t &ua,
+                                        uint32_t &tb, uint32_t &ub) {
+    const uint32_t ra = __builtin_amdgcn_alignbit(xa, xa, k.rot), rb = __builtin_amdgcn_alignbit(xb, xb, k.rot);
+    uint32_t a0 = s4get(k, ra, 0), a1 = s4get(k, ra, 1), a2 = s4get(k, ra, 2), a3 = s4get(k, ra, 3);
+    uint32_t b0 = s4get(k, rb, 0), b1 = s4get(k, rb, 1), b2 = s4get(k, rb, 2), b3 = s4get(k, rb, 3);
+    asm("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
+    ta = xor3(a0, a1, a2);
+    ua = a3;
+    tb = xor3(b0, b1, b2);
+    ub = b3;
 }
 __device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
     const uint32_t x = c ^ b;
@@ -1263,10 +1280,35 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             if (KVR_ABLATE & 8) {
                 ca = w[0]; cb = w[1];
             } else if (!__ballot(m != 0 || qa >= 0)) {
+#if KVR_XFUSE && KVR_S4
+                uint32_t ta = 0, ua = 0, tb = 0, ub = 0;
+#pragma unroll
+                for (int kk = 0; kk < H; ++kk) step4x2(xor3(ta, ua, w[kk]), xor3(tb, ub, w[kk + H]), K, ta, ua, tb, ub);
+                ca = ta ^ ua;
+                cb = tb ^ ub;
+#else
 #pragma unroll
                 for (int kk = 0; kk < H; ++kk) crc4x2(ca, w[kk], cb, w[kk + H], K);
+#endif
             } else {
-#if KVR_UNITLITE
+#if KVR_XFUSE && KVR_S4 && KVR_UNITLITE
+                // the snapshot is taken of the step's input x = c ^ w[qm] (no restart can fall on
+                // that step: a value starts at least 9 bytes after the one ending here) and the
+                // register recovered after the loop with the word at qm, which is loaded anyway
+                if (m != 0 && qm < UW) wm = ts.w32a(us + 4 * qm);
+                uint32_t ta = 0, ua = 0, tb = 0, ub = 0, snx = 0;
+#pragma unroll
+                for (int kk = 0; kk < H; ++kk) {
+                    const bool r = kk == qah, ra = r && !ab, rb = r && ab;
+                    const uint32_t xa = ra ? (w[kk] & amask) : xor3(ta, ua, w[kk]);
+                    const uint32_t xb = rb ? (w[kk + H] & amask) : xor3(tb, ub, w[kk + H]);
+                    snx = kk == qh ? (mb ? xb : xa) : snx;
+                    step4x2(xa, xb, K, ta, ua, tb, ub);
+                }
+                ca = ta ^ ua;
+                cb = tb ^ ub;
+                sn = snx ^ wm;
+#elif KVR_UNITLITE
                 // the word at qm comes from memory (issued here, used after the scan), and a restart
                 // is one select of the step's input: x = restart ? (w & amask) : (c ^ w)
                 if (m & 3) wm = ts.w32a(us + 4 * qm);
