@@ -188,3 +188,17 @@ def test_format_error_messages():
     assert K.format_error(5, 0, 0, 0, p) == "Failed to read val len in db/segment-1.dat: failed to fill whole buffer"
     assert K.format_error(6, 0, 0, 0, p) == "Failed to read val in db/segment-1.dat: failed to fill whole buffer"
     assert K.format_error(7, 0, 0, 9, p) == "Unknown opcode 9 in segment db/segment-1.dat"
+
+
+def test_segment_list_marshals_like_a_list():
+    """kvreplay.SegmentList (the kvr_segment array marshaled once, bench.py's replay step) holds
+    the same ids, pointers and lengths Context.replay builds from a plain list."""
+    segs = [b"\x00\x01\x00\x00\x00k\x01\x00\x00\x00v", bytearray(b""), np.arange(7, dtype=np.uint8)]
+    sl = K.SegmentList(segs, seg_ids=[3, 5, 9])
+    assert len(sl) == 3 and sl.total == 11 + 0 + 7 and not sl.on_device
+    assert [sl.arr[i].seg_id for i in range(3)] == [3, 5, 9]
+    assert [sl.arr[i].len for i in range(3)] == [11, 0, 7]
+    assert sl.arr[0].bytes == sl.keep[0].ctypes.data and not sl.arr[1].bytes
+    dev = K.SegmentList([(0x1000, 64), (0x2000, 0)], on_device=True)
+    assert dev.on_device and [dev.arr[i].seg_id for i in range(2)] == [0, 1]
+    assert [(dev.arr[i].bytes, dev.arr[i].len) for i in range(2)] == [(0x1000, 64), (0x2000, 0)]
