@@ -64,6 +64,9 @@ struct DevBuf {
 };
 
 constexpr uint32_t REDO_GRID = 1024;
+#ifndef KVR_GATHER_REC   // 1: the compaction's gather one wave per live record (0: one wave per 512-B block)
+#define KVR_GATHER_REC 1
+#endif
 #ifndef KVR_CSTRIPE   // 1: compaction per stripe from k_link's stripe offsets (0: k_tsum + k_tscan + k_compact)
 #define KVR_CSTRIPE 1
 #endif
@@ -978,8 +981,12 @@ static int compact_back(kvr_ctx *c, uint32_t flags, uint64_t seg_target, uint8_t
     }
     const uint32_t gw = (uint32_t)std::min<uint64_t>((max_blocks + CT_GATHER / 64 - 1) / (CT_GATHER / 64),
                                                      (uint64_t)c->n_cu * 16);
-    hipLaunchKernelGGL(k_gather, dim3(std::max(gw, 1u)), dim3(CT_GATHER), 0, st, c->l_src.p, c->l_off.p, c->cfirst.p,
-                       c->ctot.p, d_out, d_cap);
+    if (KVR_GATHER_REC)
+        hipLaunchKernelGGL(k_gather_r, dim3((uint32_t)c->n_cu * 16), dim3(CT_GATHER), 0, st, c->l_src.p, c->l_off.p,
+                           c->ctot.p, d_out, d_cap);
+    else
+        hipLaunchKernelGGL(k_gather, dim3(std::max(gw, 1u)), dim3(CT_GATHER), 0, st, c->l_src.p, c->l_off.p, c->cfirst.p,
+                           c->ctot.p, d_out, d_cap);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[2], st));
     uint64_t tot[2] = {0, 0};

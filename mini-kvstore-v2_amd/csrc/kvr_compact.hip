@@ -426,6 +426,69 @@ __global__ void __launch_bounds__(CT_GATHER) k_gather(const uint64_t *__restrict
     }
 }
 
+// KVR_GATHER_REC: one wave per live record (grid-stride over records): the record's source and
+// output range come straight from the dense live list (two dependent loads instead of the block
+// search's four); the output's 16-B aligned body moves as 16 B per lane (five source dwords
+// funnel-shifted), the unaligned head and tail bytes one per lane.  A long record loops 4 KiB at
+// a time with all its loads issued first.
+__global__ void __launch_bounds__(CT_GATHER) k_gather_r(const uint64_t *__restrict__ l_src, const uint64_t *__restrict__ l_off,
+                                                        const uint64_t *__restrict__ totals, uint8_t *__restrict__ out,
+                                                        uint64_t cap) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t total = totals[0];
+    const uint64_t n_live = totals[1];
+    const uint64_t lim = total < cap ? total : cap;
+    const uint64_t waves = (uint64_t)gridDim.x * (CT_GATHER / 64);
+    const uint64_t w0 = (uint64_t)blockIdx.x * (CT_GATHER / 64) + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint64_t j = w0; j < n_live; j += waves) {
+        const uint64_t src = l_src[j], s0 = l_off[j];
+        uint64_t s1 = l_off[j + 1];
+        if (s0 >= lim) continue;
+        s1 = s1 < lim ? s1 : lim;
+        const uint8_t *sp = reinterpret_cast<const uint8_t *>(src);
+        const uint64_t oa = reinterpret_cast<uint64_t>(out);
+        // body [a0, a1): output offsets whose absolute address is 16-B aligned
+        uint64_t a0 = ((oa + s0 + 15) & ~15ull) - oa, a1 = ((oa + s1) & ~15ull) - oa;
+        if (a0 >= a1) { a0 = s1; a1 = s1; }   // no whole 16-B word: all bytes go one by one
+        // head [s0, a0) and tail [a1, s1): fewer than 16 bytes each, or the whole record when it
+        // has no body (then fewer than 32)
+        {
+            const uint64_t nh = a0 - s0, nt = s1 - a1;
+            if ((uint64_t)lane < nh) out[s0 + lane] = sp[lane];
+            if ((uint64_t)lane < nt) out[a1 + lane] = sp[a1 - s0 + lane];
+        }
+        for (uint64_t xb = a0; xb < a1; xb += 4 * 1024) {
+            uint32_t d[4][5];
+            uint32_t sh[4];
+            bool on[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint64_t x = xb + (uint64_t)u * 1024 + 16u * (uint32_t)lane;
+                on[u] = x < a1;
+                const uint64_t sa = src + (on[u] ? x - s0 : 0);
+                const uint32_t *b = reinterpret_cast<const uint32_t *>(sa & ~3ull);
+                sh[u] = (uint32_t)sa & 3u;
+                if (on[u]) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) d[u][q] = b[q];
+                    d[u][4] = sh[u] ? b[4] : 0u;   // b[4] holds byte sa + 15 when sh != 0
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (!on[u]) continue;
+                const uint64_t x = xb + (uint64_t)u * 1024 + 16u * (uint32_t)lane;
+                uint4 v;
+                v.x = __builtin_amdgcn_alignbyte(d[u][1], d[u][0], sh[u]);
+                v.y = __builtin_amdgcn_alignbyte(d[u][2], d[u][1], sh[u]);
+                v.z = __builtin_amdgcn_alignbyte(d[u][3], d[u][2], sh[u]);
+                v.w = __builtin_amdgcn_alignbyte(d[u][4], d[u][3], sh[u]);
+                *reinterpret_cast<uint4 *>(out + x) = v;
+            }
+        }
+    }
+}
+
 // cut k (k = 1 .. (total - 1) / target): the output offset of the first live record at or after
 // k * target (grid-stride; the count comes from the device totals, cuts has room for it)
 __global__ void k_cuts(const uint64_t *__restrict__ l_off, const uint64_t *__restrict__ totals, uint64_t target,
