@@ -156,6 +156,9 @@ struct kvr_ctx {
     std::vector<SegDesc> up_segs;
     std::vector<StripeDesc> up_stripes;
     const void *up_segs_p = nullptr, *up_stripes_p = nullptr;
+    uint64_t up_tps = 0;                   // the tiles per stripe of the uploaded stripes
+    bool h_stripes_up = false;             // h_stripes holds exactly the uploaded stripes
+    bool lc_zero = false;                  // lcbuf is known to be zero (cleared at the end of the last call)
     uint64_t pool_hint = 0;
     uint64_t pool_need = 0;                // > 0: the last replay needed more than 32-bit pool slots
     uint32_t tps_override = 0;
@@ -497,15 +500,30 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
     // between whole rounds leave a ragged tail
     const uint64_t target = (uint64_t)c->n_cu * (uint64_t)c->wg_per_cu * KR_WPB;
     const uint64_t tps = c->tps_override ? c->tps_override : std::max<uint64_t>(1, (total_tiles + target - 1) / target);
-    c->h_stripes.clear();
-    for (size_t i = 0; i < n; ++i) {
-        SegDesc &g = c->h_segs[i];
-        g.stripe0 = (uint32_t)c->h_stripes.size();
-        const uint64_t ns = g.n_tiles ? (g.n_tiles + tps - 1) / tps : 0;
-        for (uint64_t j = 0; j < ns; ++j)
-            c->h_stripes.push_back(StripeDesc{(uint32_t)i, (uint32_t)(j * g.n_tiles / ns),
-                                              (uint32_t)((j + 1) * g.n_tiles / ns), 0u});
-        g.n_stripes = (uint32_t)ns;
+    // the same segment layout and stripe length as the last uploaded call: the stripes are the
+    // uploaded ones (h_stripes still holds them), only their per-segment indices are copied
+    bool same_layout = c->h_stripes_up && c->up_tps == tps && c->up_segs.size() == n && c->up_stripes_p != nullptr;
+    for (size_t i = 0; same_layout && i < n; ++i) {
+        const SegDesc &a = c->h_segs[i], &b = c->up_segs[i];
+        same_layout = a.base == b.base && a.len == b.len && a.d0 == b.d0 && a.n_tiles == b.n_tiles && a.tile0 == b.tile0;
+    }
+    if (same_layout) {
+        for (size_t i = 0; i < n; ++i) {
+            c->h_segs[i].stripe0 = c->up_segs[i].stripe0;
+            c->h_segs[i].n_stripes = c->up_segs[i].n_stripes;
+        }
+    } else {
+        c->h_stripes_up = false;
+        c->h_stripes.clear();
+        for (size_t i = 0; i < n; ++i) {
+            SegDesc &g = c->h_segs[i];
+            g.stripe0 = (uint32_t)c->h_stripes.size();
+            const uint64_t ns = g.n_tiles ? (g.n_tiles + tps - 1) / tps : 0;
+            for (uint64_t j = 0; j < ns; ++j)
+                c->h_stripes.push_back(StripeDesc{(uint32_t)i, (uint32_t)(j * g.n_tiles / ns),
+                                                  (uint32_t)((j + 1) * g.n_tiles / ns), 0u});
+            g.n_stripes = (uint32_t)ns;
+        }
     }
     const uint32_t n_stripes = (uint32_t)c->h_stripes.size();
     const uint32_t n_tiles = (uint32_t)total_tiles;
@@ -526,11 +544,14 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         c->up_segs_p = c->segs.p;
     }
     if (c->up_stripes_p != c->stripes.p || c->up_stripes.size() != n_stripes ||
-        memcmp(c->up_stripes.data(), c->h_stripes.data(), n_stripes * sizeof(StripeDesc)) != 0) {
+        (!same_layout && memcmp(c->up_stripes.data(), c->h_stripes.data(), n_stripes * sizeof(StripeDesc)) != 0)) {
+        c->up_stripes_p = nullptr;   // (invalid until the copy is queued)
         HIPCHK(hipMemcpyAsync(c->stripes.p, c->h_stripes.data(), n_stripes * sizeof(StripeDesc), hipMemcpyHostToDevice, st));
         c->up_stripes = c->h_stripes;
         c->up_stripes_p = c->stripes.p;
     }
+    c->up_tps = tps;
+    c->h_stripes_up = true;
 
     const uint32_t nb = (n_tiles + CB - 1) / CB;
     if (c->bsum.ensure(nb)) return KVR_ENOMEM;
@@ -582,7 +603,10 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
                                    d_out, out_cap, d_exp, (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p);
             }
         };
-        HIPCHK(hipMemsetAsync(c->lcbuf.p, 0, LC_BYTES, st));   // counters and link result
+        // counters and link result start at zero (the last successful call cleared them behind its
+        // results, so this memset usually runs only on a context's first call or after an error)
+        if (!c->lc_zero || attempt) HIPCHK(hipMemsetAsync(c->lcbuf.p, 0, LC_BYTES, st));
+        c->lc_zero = false;
         HIPCHK(hipEventRecord(c->ev[0], st));
         hipLaunchKernelGGL(KR_KERNEL, dim3((n_stripes + KR_WPB - 1) / KR_WPB), dim3(KR_RT), 0, st, c->segs.p, c->stripes.p, n_stripes,
                            c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, c->redo.p, c->link.p, 0, pool_chunk);
@@ -698,6 +722,8 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         c->stats.n_records = total;
         c->stats.n_crc_fail = c->h_ctr->crc_fail;
         *n_out = total;
+        // clear the counters for the next call now, behind this call's work on the stream
+        if (hipMemsetAsync(c->lcbuf.p, 0, LC_BYTES, st) == hipSuccess) c->lc_zero = true;
         if (!(flags & KVR_OUT_ON_DEVICE) && cap) {
             const uint64_t m = std::min<uint64_t>(total, cap);
             if (m) {
