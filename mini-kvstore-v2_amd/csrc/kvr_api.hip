@@ -835,7 +835,7 @@ static int fold_launch(kvr_ctx *c, size_t nt, bool deferred) {
     if (tiny) {
         hipLaunchKernelGGL(k_fold_setsize, dim3(1), dim3(1), 0, st, c->fsz.p, 15u);
     } else if (nt >= 65536) {
-        const uint32_t hb = (uint32_t)std::min<uint64_t>((nt + HLL_T - 1) / HLL_T, (uint64_t)c->n_cu);
+        const uint32_t hb = (uint32_t)std::min<uint64_t>((nt + HLL_T - 1) / HLL_T, 2ull * (uint64_t)c->n_cu);
         if (c->hpart.ensure((uint64_t)hb * HLL_M) || c->hreg.ensure(HLL_M)) return KVR_ENOMEM;
         hipLaunchKernelGGL(k_hll, dim3(hb), dim3(HLL_T), 0, st, c->ctup.p, (uint64_t)nt, c->hpart.p);
         hipLaunchKernelGGL(k_hll_merge, dim3(HLL_M / 16 / 16), dim3(HLL_MERGE_T), 0, st, c->hpart.p, hb, c->hreg.p);
@@ -1480,7 +1480,7 @@ int kvr_etag_batch(kvr_ctx *c, const uint8_t *data, uint64_t data_len, const uin
     uint64_t fails = 0;
     HIPCHK(hipMemcpyAsync(&fails, c->e_fail.p, 8, hipMemcpyDeviceToHost, st));
     if (!(flags & KVR_OUT_ON_DEVICE)) HIPCHK(hipMemcpyAsync(crc_out, d_out, n * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(wait_stream(st, c->ev[5]));
     float a = 0.f, b = 0.f;
     (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
     (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
