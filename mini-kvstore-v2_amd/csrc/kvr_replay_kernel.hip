@@ -120,7 +120,7 @@ struct __align__(16) Smem {
 #ifndef KVR_ABLATE
 #define KVR_ABLATE 0   // diagnostic builds only: 1 skip records, 2 skip value CRC, 4 skip hops,
 #endif                 // 8 skip the unit loop, 16 skip scan + finalize, 32 skip long-value folding,
-                       // 64 loads only
+                       // 64 loads only, 128 records without key loads
 
 #ifdef KVR_PROF
 __device__ unsigned long long g_prof[16];
@@ -1129,6 +1129,13 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                         const int kb = myrec + 5;
                         const uint32_t klen = my_klen;
                         uint32_t c = ~0u, bad = 0x80u;
+                        if (KVR_ABLATE & 128) {   // timing only: the key CRC over register words, no key loads
+                            uint32_t r_[KEYW + 1];
+#pragma unroll
+                            for (int i = 0; i <= KEYW; ++i) r_[i] = (uint32_t)kb * 0x9E3779B9u + (uint32_t)i;
+                            c = crc_words<KEYW>(r_, K, (uint32_t)kb & 3u, klen, nw, &bad);
+                            bad = 0u;
+                        } else
                         if (klen <= 4u * KEYW && kb + 4 * KEYW + 8 <= ts.lim) c = crc_span<KEYW>(ts, K, kb, klen, nw, &bad);
                         if (bad != 0u) {              // non-ASCII or long key: the full UTF-8 check
                             uint64_t vu = 0;
