@@ -838,7 +838,7 @@ static int fold_launch(kvr_ctx *c, size_t nt, bool deferred) {
         const uint32_t hb = (uint32_t)std::min<uint64_t>((nt + HLL_T - 1) / HLL_T, 2ull * (uint64_t)c->n_cu);
         if (c->hpart.ensure((uint64_t)hb * HLL_M) || c->hreg.ensure(HLL_M)) return KVR_ENOMEM;
         hipLaunchKernelGGL(k_hll, dim3(hb), dim3(HLL_T), 0, st, c->ctup.p, (uint64_t)nt, c->hpart.p);
-        hipLaunchKernelGGL(k_hll_merge, dim3(HLL_M / 16 / 16), dim3(HLL_MERGE_T), 0, st, c->hpart.p, hb, c->hreg.p);
+        hipLaunchKernelGGL(k_hll_merge, dim3(HLL_M / 16 / HLL_MG), dim3(HLL_MERGE_T), 0, st, c->hpart.p, hb, c->hreg.p);
         hipLaunchKernelGGL(k_hll_size, dim3(1), dim3(HLL_SIZE_T), 0, st, c->hreg.p, full_slots, c->fsz.p);
     } else {
         hipLaunchKernelGGL(k_fold_setsize, dim3(1), dim3(1), 0, st, c->fsz.p, (uint32_t)(full_slots - 1));

@@ -151,43 +151,53 @@ __device__ __forceinline__ uint32_t max4u8(uint32_t a, uint32_t b) {
     return r;
 }
 
-// 16 workgroups' worth of registers per thread-row: thread (g, s) takes register group g (16
-// registers, one 16-B load per partition) over partitions s, s + 16, ...; LDS folds the 16 rows
-constexpr int HLL_MERGE_T = 256;
+// thread (g, s) takes register group g (16 registers, one 16-B load per partition) over
+// partitions s, s + HLL_MR, ...; 4 groups per workgroup, so HLL_M / 64 workgroups share the
+// partitions; an LDS tree folds the HLL_MR rows
+constexpr int HLL_MERGE_T = 256, HLL_MG = 4, HLL_MR = HLL_MERGE_T / HLL_MG;
 __global__ void __launch_bounds__(HLL_MERGE_T) k_hll_merge(const uint8_t *__restrict__ part, uint32_t n_parts,
                                                            uint8_t *__restrict__ out) {
-    __shared__ uint4 acc[16][16];
-    const uint32_t gl = threadIdx.x & 15u, sl = threadIdx.x >> 4;
-    const uint32_t g = blockIdx.x * 16u + gl;   // register group: registers 16 g .. 16 g + 15
+    __shared__ uint4 acc[HLL_MR][HLL_MG];
+    const uint32_t gl = threadIdx.x % HLL_MG, sl = threadIdx.x / HLL_MG;
+    const uint32_t g = blockIdx.x * HLL_MG + gl;   // register group: registers 16 g .. 16 g + 15
     uint4 m = make_uint4(0u, 0u, 0u, 0u);
-    for (uint32_t b = sl; b < n_parts; b += 16) {
+#pragma unroll 4
+    for (uint32_t b = sl; b < n_parts; b += HLL_MR) {
         const uint4 v = reinterpret_cast<const uint4 *>(part + (uint64_t)b * HLL_M)[g];
         m = make_uint4(max4u8(m.x, v.x), max4u8(m.y, v.y), max4u8(m.z, v.z), max4u8(m.w, v.w));
     }
     acc[sl][gl] = m;
     __syncthreads();
-    if (sl == 0) {
-        for (int r = 1; r < 16; ++r) {
-            const uint4 v = acc[r][gl];
-            m = make_uint4(max4u8(m.x, v.x), max4u8(m.y, v.y), max4u8(m.z, v.z), max4u8(m.w, v.w));
+    for (uint32_t d = HLL_MR / 2; d > 0; d >>= 1) {
+        if (sl < d) {
+            const uint4 v = acc[sl + d][gl], a = acc[sl][gl];
+            acc[sl][gl] = make_uint4(max4u8(a.x, v.x), max4u8(a.y, v.y), max4u8(a.z, v.z), max4u8(a.w, v.w));
         }
-        reinterpret_cast<uint4 *>(out)[g] = m;
+        __syncthreads();
     }
+    if (sl == 0) reinterpret_cast<uint4 *>(out)[g] = acc[0][gl];
 }
 
 // the fold table's size on the device, so no host round trip sits between the estimate and the
 // claims: fsz[0] = entries - 1 (a power of two minus one), fsz[2..3] = the estimate (uint64).
 // The same arithmetic as the host's hll_estimate (kvr_api.hip), summed in a different order.
-constexpr int HLL_SIZE_T = 256;
+constexpr int HLL_SIZE_T = 1024;   // 16 registers per thread, one 16-B load each
+static_assert(HLL_M == 16 * HLL_SIZE_T, "k_hll_size: one 16-B word of registers per thread");
 __global__ void __launch_bounds__(HLL_SIZE_T) k_hll_size(const uint8_t *__restrict__ reg, uint64_t full_slots,
                                                          uint32_t *__restrict__ fsz) {
     __shared__ double ss[HLL_SIZE_T];
     __shared__ uint32_t sz[HLL_SIZE_T];
     double sum = 0;
     uint32_t zeros = 0;
-    for (int j = threadIdx.x; j < HLL_M; j += HLL_SIZE_T) {
-        sum += ldexp(1.0, -(int)reg[j]);
-        zeros += reg[j] == 0;
+    {
+        const uint4 q = reinterpret_cast<const uint4 *>(reg)[threadIdx.x];
+        const uint32_t wds[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t r = (wds[i >> 2] >> (8 * (i & 3))) & 255u;
+            sum += ldexp(1.0, -(int)r);
+            zeros += r == 0u;
+        }
     }
     ss[threadIdx.x] = sum;
     sz[threadIdx.x] = zeros;
