@@ -47,11 +47,38 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
     // this thread's chunk: its last stripe with a record start, and its stripes' records (the
     // output offsets k_compact_s writes from); exclusive scans over the chunks, a max and a sum,
     // by wave shuffles and then the 16 wave totals
+    // (up to KL stripes per thread, the common case: their results and descriptors are loaded
+    // once, all together, and kept in registers for the passes below)
+    constexpr int KL = 4;
+    const bool cached = per <= (uint32_t)KL;
+    uint64_t c_entry[KL], c_exit[KL];
+    uint32_t c_kind[KL], c_count[KL], c_seg[KL], c_tb[KL], c_te[KL];
+    if (cached) {
+#pragma unroll
+        for (int i = 0; i < KL; ++i) {
+            const uint32_t s = b + i;
+            c_entry[i] = NONE; c_exit[i] = NONE; c_kind[i] = 0; c_count[i] = 0; c_seg[i] = 0; c_tb[i] = 0; c_te[i] = 0;
+            if (s < e) {
+                c_entry[i] = sres[s].entry; c_exit[i] = sres[s].exit; c_kind[i] = sres[s].err_kind;
+                c_count[i] = sres[s].count;
+                const StripeDesc d = stripes[s];
+                c_seg[i] = d.seg; c_tb[i] = d.t_begin; c_te[i] = d.t_end;
+            }
+        }
+    }
     int32_t m = -1;
     unsigned long long mine = 0;
-    for (uint32_t s = b; s < e; ++s) {
-        if (sres[s].entry != NONE) m = (int32_t)s;
-        mine += sres[s].count;
+    if (cached) {
+#pragma unroll
+        for (int i = 0; i < KL; ++i) {
+            if (b + i < e && c_entry[i] != NONE) m = (int32_t)(b + i);
+            mine += c_count[i];
+        }
+    } else {
+        for (uint32_t s = b; s < e; ++s) {
+            if (sres[s].entry != NONE) m = (int32_t)s;
+            mine += sres[s].count;
+        }
     }
     int32_t im = m;
     unsigned long long is = mine;
@@ -74,11 +101,41 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
     const int32_t run0 = lane ? (xm > pm ? xm : pm) : pm;   // the last stripe with records before the chunk
     if (soff) {
         unsigned long long at = (lane ? xs : 0ull) + ps;
-        for (uint32_t s = b; s < e; ++s) { soff[s] = at; at += sres[s].count; }
+        if (cached) {
+#pragma unroll
+            for (int i = 0; i < KL; ++i) if (b + i < e) { soff[b + i] = at; at += c_count[i]; }
+        } else {
+            for (uint32_t s = b; s < e; ++s) { soff[s] = at; at += sres[s].count; }
+        }
     }
 
     // pass 1: consistency of every stripe with its predecessor's exit
     int32_t run = run0;
+    if (cached) {
+        SegDesc gc[KL];
+#pragma unroll
+        for (int i = 0; i < KL; ++i) if (b + i < e) gc[i] = segs[c_seg[i]];
+        uint64_t xrun = run0 >= 0 ? sres[run0].exit : NONE;   // the exit of stripe `run`
+#pragma unroll
+        for (int i = 0; i < KL; ++i) {
+            const uint32_t s = b + i;
+            if (s >= e) break;
+            StripeDesc d;
+            d.seg = c_seg[i]; d.t_begin = c_tb[i]; d.t_end = c_te[i]; d.pad = 0;
+            const SegDesc &g = gc[i];
+            const bool first = (s == g.stripe0);
+            bool bad = false, after_err = false;
+            if (!first) {
+                const uint64_t xp = run >= 0 ? xrun : NONE;
+                if (xp == ERRP) after_err = true;
+                else if (c_entry[i] == NONE) bad = xp < stripe_hi(d, g, tile);
+                else bad = (c_entry[i] != xp);
+            }
+            if (bad && !after_err) atomicMin(&seg_bad[d.seg], s);
+            if (c_kind[i] != 0 && !after_err && !bad) atomicMin(&seg_err[d.seg], s);
+            if (c_entry[i] != NONE) { run = (int32_t)s; xrun = c_exit[i]; }
+        }
+    } else
     for (uint32_t s = b; s < e; ++s) {
         const StripeRes r = sres[s];
         const StripeDesc d = stripes[s];
