@@ -290,3 +290,15 @@ def test_segment_over_2gib(gctx):
     cut = seg[: len(head) + len(hdr) + big // 2]      # the big value is truncated: engine.rs:130
     rg = check_parity(gctx, [cut])
     assert rg.error.kind == KIND["VAL"]
+
+
+def test_repeated_calls_reuse_and_refresh_descriptors(gctx):
+    """Calls over the same segments reuse the uploaded descriptors and stripe layout; a call over
+    other segments (same count, other lengths), a corrupted call (its counters are not cleared
+    behind it) and the calls after it must still match the oracle bit for bit."""
+    spec_a, spec_b = SPECS["cfg2_1k"], SPECS["cfg4_del"]
+    a = [K.gen_segment_cpu(spec_a, s)[0].tobytes() for s in range(3)]
+    b = [K.gen_segment_cpu(spec_b, s)[0].tobytes() for s in range(3)]
+    bad = a[:2] + [a[2][: len(a[2]) // 2 + 7]]
+    for segs in (a, a, b, a, bad, bad, a, b, b):
+        check_parity(gctx, segs)
