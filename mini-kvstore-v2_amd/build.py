@@ -92,35 +92,12 @@ def build_ablate(masks=(0, 1, 2, 3, 7, 8, 16, 32, 64)):
     return out
 
 
-# experimental k_replay variants (tools/ablate.py <cfg> 0 <name>): timing only, not shipped
+# experimental k_replay variants (tools/ablate.py <cfg> 0 <name>): timing only, never shipped.
+# Each entry is the -D flags of one build; the kernel's own comments say what each macro does.
 VARIANTS = {
-    "rt768": ["-DKVR_RT=768"],
-    "rt512": ["-DKVR_RT=512"],
-    "v9": ["-DKVR_KERNEL_V9"],
-    "v9a3": ["-DKVR_KERNEL_V9", "-DKVR_ABLATE=3"],
-    "v9a64": ["-DKVR_KERNEL_V9", "-DKVR_ABLATE=64"],
-    "v8": ["-DKVR_KERNEL_V8"],
-    "prio0": ["-DKVR_HOP_PRIO=0", "-DKVR_REC_PRIO=0"],   # wave priority off
-    "bulklow": ["-DKVR_BULK_LOWPRIO=1"],
-    "fin0": ["-DKVR_FIN_PRIO=0"],
-    "fin2": ["-DKVR_FIN_PRIO=2"],
-    "fin1rp2": ["-DKVR_REC_PRIO=2"],
-    "s2": ["-DKVR_S4=0"],
-    "kscan": ["-DKVR_XSCAN=0"],
-    "hopold": ["-DKVR_HOPFAST=0"],
-    "unitsel": ["-DKVR_UNITLITE=0"],
-    "nodefer": ["-DKVR_DEFER=0"],
-    "foldnokey": ["-DKVR_FOLD_NOKEY"],
-    "foldsplit": ["-DKVR_FOLD_MERGE=0"],   # every tag match verified by k_fold_verify   # fold kernels without key reads (timing bound only)   # long-value unit views updated in the hop loop   # unit loop with per-step register/data selects   # the hop loop with its separate range checks   # segmented scan with a multiply at every step   # slice-by-2 unit loop (two LDS round trips per word)
-    "pf": ["-DKVR_PF=1"],        # touch load of the next tile before the CRC phase (1.66 vs 1.64 ms, not kept)
-    "finr": ["-DKVR_FINR=1"],    # value-end tail bytes in one lookup round (A/B: 1.604 vs 1.589 ms, not kept)
-    "hop1": ["-DKVR_HOP2=0"],    # the single exact hop loop for every record (1.642 vs 1.604 ms)
-    "late": ["-DKVR_EARLY=0"],   # next tile loaded after the finalize
-    "rec1": ["-DKVR_LATEREC=1"],   # the last record batch after the unit loop (A/B 1.689 vs 1.601 ms: not kept)
-    "tres0": ["-DKVR_TRES_EARLY=0"],   # TileRes stored at the end of the tile
-    "cmp32": ["-DKVR_COMPACT16=0", "-DKVR_CSTRIPE=0"],   # k_compact with one 32-B tuple per thread
-    "ctile": ["-DKVR_CSTRIPE=0"],   # compaction by 256-tile blocks after a scan of tile counts
-    "xf1": ["-DKVR_XFUSE=1"],   # unit-loop registers as two XOR terms (A/B 1.661 vs 1.579 ms: not kept)
+    "rt768": ["-DKVR_RT=768"],     # 12 stripes per workgroup
+    "prio0": ["-DKVR_HOP_PRIO=0", "-DKVR_REC_PRIO=0"],   # no raised wave priority
+    "fin0": ["-DKVR_FIN_PRIO=0"],  # the scan + finalize chain at priority 0
     "base": [],
 }
 

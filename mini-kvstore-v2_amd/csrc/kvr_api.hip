@@ -22,27 +22,16 @@
 #include <hipcub/hipcub.hpp>
 
 #include "kvr_replay_kernel.hip"
-#include "kvr_replay8.hip"
-#include "kvr_replay9.hip"
 #include "kvr_kernels.hip"
 #include "kvr_compact.hip"
 #include "kvr_etag.hip"
 
 using namespace kvr;
 
-// the replay kernel: V7 (kvr_replay_kernel.hip, the fastest measured: DESIGN.md §7);
-// -DKVR_KERNEL_V8 / -DKVR_KERNEL_V9 build the experimental kernels (timing only).
-// KR_WPB = stripes per workgroup, KR_TILE = tile bytes.
-#if defined(KVR_KERNEL_V9)
-#define KR_KERNEL v9::k_replay9
-static constexpr int KR_RT = v9::RT, KR_WPB = v9::WPB * v9::QPW, KR_TILE = v9::TILE;
-#elif defined(KVR_KERNEL_V8)
-#define KR_KERNEL v8::k_replay8
-static constexpr int KR_RT = v8::RT, KR_WPB = v8::WPB, KR_TILE = TILE;
-#else
+// the replay kernel (kvr_replay_kernel.hip): KR_WPB = stripes per workgroup,
+// KR_TILE = tile bytes
 #define KR_KERNEL k_replay
 static constexpr int KR_RT = RT, KR_WPB = WPB, KR_TILE = TILE;
-#endif
 
 namespace {
 
@@ -455,6 +444,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
     if (err) memset(err, 0, sizeof(*err));
     *n_out = 0;
     memset(&c->stats, 0, sizeof(c->stats));
+    c->ix_valid = false;   // the segment descriptors and the pool change: an earlier live list is stale
     if (n == 0) return KVR_OK;
     if (n >= 0xFFFFFFFFull) return KVR_EINVAL;
     for (size_t i = 0; i < n; ++i) {
@@ -766,6 +756,7 @@ static int fold_launch(kvr_ctx *c, size_t nt, bool deferred);
 static int compact_front(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, kvr_error *err, size_t *nt_out,
                          bool rewrite, kvr_compact_stats *cs, bool deferred = false) {
     *nt_out = 0;
+    c->ix_valid = false;
     c->c_staged = false;
     c->c_nt = 0;
     c->fold_rounds = 0;

@@ -430,11 +430,14 @@ struct Loader {
 };
 
 // mmap path: every file mapped read-only and populated from the page cache (no copy; about 1 ms
-// for 4 GiB when cached), one file per task over the threads in store order.  Each mapping is
-// its own registration (a transfer must lie inside one).  false: a mapping failed (the pread
-// path takes over; nothing is left mapped).
-bool load_mmap(kvs_store *s, const std::vector<int> &fds, const std::vector<uint64_t> &sizes, uint32_t n_threads,
-               Loader &L) {
+// for 4 GiB when cached), one file per task over the threads in store order.  Each file is opened,
+// mapped and closed at once (a mapping outlives its descriptor), so at most one descriptor per
+// thread is open whatever the segment count.  Each mapping is its own registration (a transfer
+// must lie inside one).  false: a mapping failed (the pread path takes over; nothing is left
+// mapped).  The files must not be truncated while the store is open: a mapped page past a new
+// end of file faults (SIGBUS) when touched.
+bool load_mmap(kvs_store *s, const std::vector<std::string> &paths, const std::vector<uint64_t> &sizes,
+               uint32_t n_threads, Loader &L) {
     const size_t n = L.n;
     std::vector<void *> mp(n, nullptr);
     std::atomic<size_t> next{0};
@@ -445,7 +448,9 @@ bool load_mmap(kvs_store *s, const std::vector<int> &fds, const std::vector<uint
                 const size_t i = next.fetch_add(1);
                 if (i >= n) return;
                 if (sizes[i] && !failed) {
-                    void *p = mmap(nullptr, sizes[i], PROT_READ, MAP_PRIVATE | MAP_POPULATE, fds[i], 0);
+                    const int fd = open(paths[i].c_str(), O_RDONLY);
+                    void *p = fd < 0 ? MAP_FAILED : mmap(nullptr, sizes[i], PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+                    if (fd >= 0) close(fd);
                     if (p == MAP_FAILED) failed = true;
                     else mp[i] = p;
                 }
@@ -469,18 +474,21 @@ bool load_mmap(kvs_store *s, const std::vector<int> &fds, const std::vector<uint
 
 // pread path: one anonymous arena on 2-MiB pages (page-aligned segment starts), 8-MiB pieces in
 // store order over the threads (they fault the arena in parallel); consecutive segments form
-// registration groups of >= 256 MiB, each ready when all its pieces are in
-void load_pread(kvs_store *s, const std::vector<int> &fds, const std::vector<uint64_t> &sizes, uint32_t n_threads,
-                Loader &L) {
+// registration groups of >= 256 MiB, each ready when all its pieces are in.  Each piece opens its
+// file, reads and closes it (one descriptor per thread at most).  Returns KVR_OK, KVR_ENOMEM when
+// the arena cannot be mapped (never an empty store in its place: a later compaction would remove
+// the files), or KVR_EIO when a file that opened at discovery no longer does (*io_failed).
+int load_pread(kvs_store *s, const std::vector<std::string> &paths, const std::vector<uint64_t> &sizes,
+               uint32_t n_threads, Loader &L, std::atomic<bool> *io_failed) {
     const size_t n = L.n;
     std::vector<uint64_t> offs(n);
     uint64_t arena = 0;
     for (size_t i = 0; i < n; ++i) { offs[i] = arena; arena += page_up(sizes[i]); }
     const uint64_t map_len = ((arena + HUGE_PAGE - 1) & ~(HUGE_PAGE - 1)) + HUGE_PAGE;
     void *m = mmap(nullptr, map_len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-    if (m == MAP_FAILED) {   // nothing to read into: every segment empty, the replay sees no bytes
+    if (m == MAP_FAILED) {
         for (size_t i = 0; i < n; ++i) { L.len[i] = 0; L.left[i] = 0; }
-        return;
+        return KVR_ENOMEM;
     }
     s->maps.emplace_back(m, map_len);
     uint8_t *base = reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(m) + HUGE_PAGE - 1) & ~(HUGE_PAGE - 1));
@@ -503,7 +511,7 @@ void load_pread(kvs_store *s, const std::vector<int> &fds, const std::vector<uin
     auto next = std::make_shared<std::atomic<uint64_t>>(0);
     const uint64_t n_pieces = (*pstart)[n];
     for (uint32_t w = 0; w < n_threads && n; ++w) {
-        L.th.emplace_back([&L, &fds, &sizes, base, offs, pstart, next, n_pieces]() {
+        L.th.emplace_back([&L, &paths, &sizes, base, offs, pstart, next, n_pieces, io_failed]() {
             for (;;) {
                 const uint64_t p = next->fetch_add(1);
                 if (p >= n_pieces) return;
@@ -511,12 +519,15 @@ void load_pread(kvs_store *s, const std::vector<int> &fds, const std::vector<uin
                 const uint64_t o = (p - (*pstart)[i]) * PIECE;
                 const uint64_t want = o < sizes[i] ? std::min(PIECE, sizes[i] - o) : 0;
                 uint64_t r = 0;
-                while (r < want) {   // a short read (EOF, error) ends the segment there (engine.rs:88)
-                    const ssize_t k = pread(fds[i], base + offs[i] + o + r, (size_t)(want - r), (off_t)(o + r));
+                const int fd = want ? open(paths[i].c_str(), O_RDONLY) : -1;
+                if (want && fd < 0) *io_failed = true;
+                while (fd >= 0 && r < want) {   // a short read (EOF, error) ends the segment there (engine.rs:88)
+                    const ssize_t k = pread(fd, base + offs[i] + o + r, (size_t)(want - r), (off_t)(o + r));
                     if (k < 0 && errno == EINTR) continue;
                     if (k <= 0) break;
                     r += (uint64_t)k;
                 }
+                if (fd >= 0) close(fd);
                 if (r < want) {
                     uint64_t cur = L.len[i].load();
                     while (o + r < cur && !L.len[i].compare_exchange_weak(cur, o + r)) {}
@@ -525,6 +536,20 @@ void load_pread(kvs_store *s, const std::vector<int> &fds, const std::vector<uin
             }
         });
     }
+    return KVR_OK;
+}
+
+// create a directory and its missing parents (std::fs::create_dir_all, engine.rs:26-28)
+int mkdir_all(const std::string &dir) {
+    struct stat st;
+    if (stat(dir.c_str(), &st) == 0) return S_ISDIR(st.st_mode) ? 0 : -1;
+    const size_t cut = dir.find_last_of('/');
+    if (cut != std::string::npos && cut > 0) {
+        const std::string parent = dir.substr(0, cut);
+        if (mkdir_all(parent) != 0) return -1;
+    }
+    if (mkdir(dir.c_str(), 0777) != 0 && errno != EEXIST) return -1;
+    return 0;
 }
 
 }  // namespace
@@ -557,8 +582,7 @@ int kvs_open_ex(const char *dir, kvr_ctx *ctx, uint32_t flags, kvs_store **out, 
     if (err) memset(err, 0, sizeof(*err));
     if (msg && msg_cap) msg[0] = 0;
     const auto t0 = std::chrono::steady_clock::now();
-    struct stat st;
-    if (stat(dir, &st) != 0 && mkdir(dir, 0777) != 0 && errno != EEXIST) return KVR_EIO;   // engine.rs:26-28
+    if (mkdir_all(dir) != 0) return KVR_EIO;   // engine.rs:26-28 (create_dir_all)
     size_t n = 0;
     int rc = kvh_discover(dir, nullptr, 0, nullptr, 0, &n);
     if (rc != KVR_OK && rc != KVR_CAPACITY) return rc;
@@ -571,20 +595,24 @@ int kvs_open_ex(const char *dir, kvr_ctx *ctx, uint32_t flags, kvs_store **out, 
     for (size_t i = 0; i < n; ++i) { paths[i] = std::string(pbuf.data() + po); po += paths[i].size() + 1; }
 
     // engine.rs:55-57 opens segment k only after segments 0 .. k-1 replayed: an unopenable file
-    // ends the list, and its error stands only if the segments before it replay cleanly
-    std::vector<int> fds;
+    // ends the list, and its error stands only if the segments before it replay cleanly.  Each
+    // file is opened, measured and closed here (the loaders open it again), so the descriptors
+    // in use never grow with the segment count; running out of descriptors (EMFILE / ENFILE) is a
+    // resource failure of this process, not an unopenable segment.
     std::vector<uint64_t> sizes;
     size_t n_ok = n;
     int open_errno = 0;
     for (size_t i = 0; i < n; ++i) {
         const int fd = open(paths[i].c_str(), O_RDONLY);
-        if (fd < 0) { n_ok = i; open_errno = errno; break; }   // engine.rs:80-82
+        if (fd < 0) {
+            if (errno == EMFILE || errno == ENFILE) return KVR_EIO;
+            n_ok = i; open_errno = errno; break;   // engine.rs:80-82
+        }
         struct stat fs;
         const bool dir_like = fstat(fd, &fs) != 0 || S_ISDIR(fs.st_mode);   // read() fails -> EOF (engine.rs:88)
-        fds.push_back(fd);
+        close(fd);
         sizes.push_back(dir_like ? 0 : (uint64_t)fs.st_size);
     }
-    auto close_all = [&]() { for (int fd : fds) close(fd); fds.clear(); };
 
     std::unique_ptr<kvs_store> s(new kvs_store());
     s->dir = dir;
@@ -603,8 +631,12 @@ int kvs_open_ex(const char *dir, kvr_ctx *ctx, uint32_t flags, kvs_store **out, 
     // the segments' host bytes: the files mapped (page cache, no copy) or read into an arena;
     // the loader threads make segment i ready in store order as far as they can, and the push
     // loop below registers and transfers each one as soon as it is
-    bool mapped = !(flags & KVS_OPEN_PREAD) && load_mmap(s.get(), fds, sizes, n_threads, L);
-    if (!mapped) load_pread(s.get(), fds, sizes, n_threads, L);
+    bool mapped = !(flags & KVS_OPEN_PREAD) && load_mmap(s.get(), paths, sizes, n_threads, L);
+    std::atomic<bool> io_failed{false};
+    if (!mapped) {
+        const int lr = load_pread(s.get(), paths, sizes, n_threads, L, &io_failed);
+        if (lr != KVR_OK) return lr;
+    }
     s->ost.mode = mapped ? KVS_LOAD_MMAP : KVS_LOAD_PREAD;
     bool all_reg = reg;
     double ms_reg = 0, ms_push = 0;
@@ -632,7 +664,7 @@ int kvs_open_ex(const char *dir, kvr_ctx *ctx, uint32_t flags, kvs_store **out, 
     s->ost.ms_register = ms_reg;
     s->ost.ms_push = ms_push;
     s->pinned = all_reg;
-    close_all();
+    if (io_failed) return KVR_EIO;   // a segment file vanished between discovery and the read
     uint64_t bytes = 0;
     for (const kvr_segment &g : s->segs) bytes += g.len;
     s->ost.bytes = bytes;
@@ -665,7 +697,8 @@ int kvs_open_ex(const char *dir, kvr_ctx *ctx, uint32_t flags, kvs_store **out, 
     s->active_id = (n ? ids[n - 1] : 0) + 1;
     const std::string ap = std::string(dir) + "/segment-" + std::to_string(s->active_id) + ".dat";
     const int fd = open(ap.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
-    if (fd >= 0) close(fd);
+    if (fd < 0) return KVR_EIO;   // engine.rs:63-67: the create error is StoreError::Io
+    close(fd);
     s->ost.ms_total = ms_since(t0);
     *out = s.release();
     return KVR_OK;

@@ -118,6 +118,7 @@ int replay_last(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, k
     if (flags & ~(KVR_SEGS_ON_DEVICE | KVR_OUT_ON_DEVICE)) return KVR_EINVAL;
     *n_out = 0;
     c->ix_valid = false;
+    HIPCHK(hipSetDevice(c->device));
     size_t nt = 0;
     kvr_compact_stats cs{};
     int rc = compact_front(c, segs, n, flags, err, &nt, false, &cs, true);   // replay + fold (kvr_compact.hip)
@@ -165,6 +166,7 @@ int kvr_replay_index(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fla
     *n_slots = 0;
     c->ix_valid = false;
     c->ix_live = c->ix_slots = 0;
+    HIPCHK(hipSetDevice(c->device));
     memset(&c->istats, 0, sizeof(c->istats));
     const auto t0 = std::chrono::steady_clock::now();
     size_t nt = 0;
@@ -209,6 +211,7 @@ int kvr_replay_index(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fla
 int kvr_index_fetch(kvr_ctx *c, uint32_t flags, kvr_tuple *live, size_t live_cap, uint32_t *slots, uint64_t slot_cap) {
     if (!c || !c->ix_valid || (live_cap && !live) || (slot_cap && !slots)) return KVR_EINVAL;
     if (flags & ~KVR_OUT_ON_DEVICE) return KVR_EINVAL;
+    HIPCHK(hipSetDevice(c->device));
     return index_copy_out(c, flags, live, live_cap, slots, slot_cap);
 }
 
@@ -216,7 +219,8 @@ int kvr_live_keys(kvr_ctx *c, uint32_t flags, uint8_t *keys, uint64_t keys_cap, 
                   uint64_t *key_bytes) {
     if (!c || !key_bytes || (keys_cap && !keys) || (off_cap && !key_off)) return KVR_EINVAL;
     if (flags & ~KVR_OUT_ON_DEVICE) return KVR_EINVAL;
-    if (!c->ix_valid) return KVR_EINVAL;   // no live list (or a later call replaced it)
+    if (!c->ix_valid) return KVR_EINVAL;   // no live list (or a later call replaced it: every replay clears it)
+    HIPCHK(hipSetDevice(c->device));
     const uint64_t n = c->ix_live;
     hipStream_t st = c->stream;
     *key_bytes = 0;

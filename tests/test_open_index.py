@@ -414,3 +414,48 @@ def test_live_replay_ends_a_staged_compaction(gctx):
     gctx.replay_live(segs)
     with pytest.raises(K.NativeError, match="-1"):
         gctx.compact_export(hdr.data_ptr(), keys.data_ptr())
+
+
+@pytest.mark.gpu
+def test_live_keys_invalid_after_a_later_replay(gctx):
+    """kvr_live_keys reads the live list of the last replay_live / replay_index; a later
+    kvr_replay or kvr_compact on the same context replaces the segment descriptors and the pool,
+    so the key arena must answer KVR_EINVAL rather than read stale tuples."""
+    spec = K.GenSpec(seed=106, seg_bytes=200_000, key_space_log2=9, val_min=0, val_max=100, del_permille=200)
+    segs = [K.gen_segment_cpu(spec, s)[0] for s in range(3)]
+    idx = gctx.replay_index(segs)
+    keys, offs = gctx.live_keys(len(idx.live))
+    assert len(offs) == len(idx.live) + 1
+    gctx.replay(segs[:1])
+    with pytest.raises(K.NativeError, match="-1"):
+        gctx.live_keys(len(idx.live))
+    idx = gctx.replay_index(segs)
+    gctx.compact(segs)
+    with pytest.raises(K.NativeError, match="-1"):
+        gctx.live_keys(len(idx.live))
+
+
+@pytest.mark.gpu
+def test_kvs_open_more_segments_than_descriptors(gctx, tmp_path):
+    """A store with more segment files than the process may hold descriptors (one per reopen
+    over a long life, or after compactions) opens: kvs_open_ex closes each file before the next
+    (engine.rs:80 opens one at a time), on the mmap and the pread path."""
+    import resource
+    spec = K.GenSpec(seed=107, seg_bytes=3000, key_space_log2=8, val_min=0, val_max=60, del_permille=200)
+    n = 300
+    segs = [K.gen_segment_cpu(spec, s)[0] for s in range(n)]
+    ids = list(range(1, n + 1))
+    d = tmp_path / "db"
+    _write_store(d, segs, ids)
+    want, nk, tb = expect(segs, ids)
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    in_use = len(os.listdir("/proc/self/fd"))
+    resource.setrlimit(resource.RLIMIT_NOFILE, (in_use + 64, hard))
+    try:
+        for flags in (0, K.OPEN_PREAD):
+            s = K.KVStore.open(str(d), gctx, flags=flags)
+            assert (s.stats().num_keys, s.stats().total_bytes, s.stats().active_segment_id) == (nk, tb, n + 1)
+            s.close()
+            os.unlink(d / f"segment-{n + 1}.dat")
+    finally:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (soft, hard))
