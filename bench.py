@@ -56,7 +56,8 @@ def main():
     ap.add_argument("--config", default=None, choices=list(CONFIGS))
     ap.add_argument("--mode", default="replay", choices=["replay", "compact", "etag"])
     ap.add_argument("--segments", type=int, default=0, help="override segments per GPU")
-    ap.add_argument("--cpu-segs", type=int, default=32, help="CPU baseline sample (segments)")
+    ap.add_argument("--cpu-segs", type=int, default=0,
+                    help="CPU baseline sample in segments (default: about 2 GiB of the shard)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stream", action="store_true", help="skip the pinned-host streamed (H2D-inclusive) leg")
     ap.add_argument("--no-open", action="store_true", help="skip the kvs_open-from-files leg")
@@ -163,10 +164,12 @@ def main():
     alg_bytes = seg_total + 32 * n_rec          # segment bytes read once + 32-B tuple writes
     achieved = alg_bytes / (ms_replay / 1e3) / 1e9
 
-    cpu = e2e = cpu_par = None
+    cpu = e2e = cpu_par = cpu_all = None
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle_py as O   # the checker / CPU baseline only
-        cs = min(args.cpu_segs, nseg)
+        # the faithful port runs about 0.5 GiB/s on one core: a sample of about 2 GiB (32 of cfg2's
+        # 64 segments, 4 of cfg5's 512-MiB segments, 2 of cfg3's 1-GiB segments) keeps it near 5 s
+        cs = min(args.cpu_segs or max(1, (2 << 30) // seg_bytes), nseg)
         hall = data[:tot].cpu().numpy()   # the shard's bytes (byte-identical to kvh_gen_segment's)
         all_segs = [hall[o:o + ln] for (ln, _), o in zip(sizes, offs)]
         host_segs = all_segs[:cs]
@@ -190,21 +193,30 @@ def main():
         # owning map) over the whole shard, one segment per thread on every core this process may use
         from concurrent.futures import ThreadPoolExecutor
         host = host_cpu_info()
-        pts = []
-        for _ in range(3):
-            t3 = time.perf_counter()
-            with ThreadPoolExecutor(host["threads"]) as ex:
-                pr = list(ex.map(lambda h: O.replay_s16([h]), all_segs))
-            pts.append(time.perf_counter() - t3)
-            assert all(r[0] == 0 for r in pr) and sum(len(r[1]) for r in pr) == n_rec
-        pt = min(pts)
-        del hall, all_segs, host_segs, pr
-        cpu_par = {"value": round(seg_total / pt / 2 ** 30, 4), "unit": "GiB/s", "cores": host["threads"], "kind": "port",
-                   "records_per_s": round(n_rec / pt, 1), "nproc": host["nproc"], "affinity": host["affinity"],
-                   "cpu_model": host["model"],
-                   "sample": f"all {nseg} segments ({seg_total / 2**30:.2f} GiB): oracle_replay_s16 (framing walk, "
-                             f"UTF-8 check, slice-by-16 CRC-32 of every key and value, 32-B tuples; no owning map), "
-                             f"one segment per thread, {host['threads']} threads, best of 3"}
+
+        def strong(threads):
+            pts = []
+            for _ in range(3):
+                t3 = time.perf_counter()
+                with ThreadPoolExecutor(threads) as ex:
+                    pr = list(ex.map(lambda h: O.replay_s16([h]), all_segs))
+                pts.append(time.perf_counter() - t3)
+                assert all(r[0] == 0 for r in pr) and sum(len(r[1]) for r in pr) == n_rec
+            return min(pts)
+
+        def strong_line(pt, threads, what):
+            return {"value": round(seg_total / pt / 2 ** 30, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+                    "records_per_s": round(n_rec / pt, 1), "nproc": host["nproc"], "affinity": host["affinity"],
+                    "cpu_model": host["model"],
+                    "sample": f"all {nseg} segments ({seg_total / 2**30:.2f} GiB): oracle_replay_s16 (framing walk, "
+                              f"UTF-8 check, slice-by-16 CRC-32 of every key and value, 32-B tuples; no owning map), "
+                              f"one segment per thread (the framing is serial within a segment, engine.rs:85), "
+                              f"{threads} threads = {what}, best of 3"}
+        cpu_par = strong_line(strong(host["threads"]), host["threads"], "this job's CPU share per GPU")
+        all_threads = min(host["affinity"], nseg)
+        cpu_all = strong_line(strong(all_threads), all_threads,
+                              f"every core of the affinity set ({host['affinity']}) the {nseg} segments can use")
+        del hall, all_segs, host_segs
         cpu = {"value": round(sb / ct / 2 ** 30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
                "records_per_s": round(nr / ct, 1), "nproc": host["nproc"], "cpu_model": host["model"],
                "sample": f"{cs} of the {nseg} segments ({sb / 2**30:.2f} GiB), oracle_replay_faithful: "
@@ -349,6 +361,7 @@ def main():
                      "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": cpu,
         "cpu_baseline_parallel": cpu_par,
+        "cpu_baseline_allcores": cpu_all,
         "e2e_host": e2e,
         "e2e_stream_pinned": stream,
         "live_index_device": live_idx,
@@ -397,8 +410,13 @@ def bench_compact(args, ctx, segs, seg_nos, seg_total, n_rec, desc, nseg, seg_by
     dt = time.perf_counter() - t0
     ms_rep, ms_fold, ms_gat = (float(np.mean([x[i] for x in st])) for i in range(3))
     live_bytes, n_live = r.stats.bytes_out, r.stats.n_live
-    gather_bytes = 2 * live_bytes                       # live records read once + written once
-    achieved = gather_bytes / (ms_gat / 1e3) / 1e9
+    # the pipeline's algorithmic HBM bytes per step: every segment byte read once by
+    # the replay, its 32-B tuples written once and read once by the fold, the live records read once
+    # and written once by the gather
+    alg = seg_total + 2 * 32 * n_rec + 2 * live_bytes
+    ms_dev = ms_rep + ms_fold + ms_gat
+    achieved = alg / (ms_dev / 1e3) / 1e9
+    phases = {"replay": round(ms_rep, 4), "fold": round(ms_fold, 4), "gather": round(ms_gat, 4)}
     res = {
         "metric": "device-resident compaction live-record rewrite GiB/s (segment bytes in)",
         "value": round(seg_total * args.steps / dt / 2 ** 30, 3), "unit": "GiB/s", "n_gpus": world,
@@ -410,9 +428,12 @@ def bench_compact(args, ctx, segs, seg_nos, seg_total, n_rec, desc, nseg, seg_by
                    "records_per_gpu": n_rec, "live_records": n_live, "live_bytes": live_bytes,
                    "new_segments": len(r.seg_ends), "parallelism": "1 GPU"},
         "ms_replay": round(ms_rep, 4), "ms_fold": round(ms_fold, 4), "ms_gather": round(ms_gat, 4),
-        "roofline": {"bound": "hbm", "kernel": "k_gather", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+        "roofline": {"bound": "hbm", "kernel": "compaction pipeline (k_replay, fold kernels, k_gather_r)",
+                     "dominant_kernel": "k_replay" if ms_rep >= max(ms_fold, ms_gat) else
+                                        ("fold" if ms_fold >= ms_gat else "k_gather_r"),
+                     "ms_by_phase": phases, "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-                     "alg_bytes_per_launch": gather_bytes},
+                     "alg_bytes_per_step": alg},
     }
     print(json.dumps(res))
     ctx.close()

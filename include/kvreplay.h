@@ -255,7 +255,8 @@ int  kvr_last_stream_stats(const kvr_ctx *ctx, kvr_stream_stats *out);
  * shards.  Output, errors, expected_crc and return codes are exactly those of kvr_replay over the
  * same segs on one GPU: tuples in (segment, offset) order with seg_idx into segs[], the first
  * error = the minimum (segment, offset) error over the shards.  devices may repeat an id (several
- * contexts on one GPU).  Host segments and host output only (flags: 0). */
+ * contexts on one GPU).  flags: KVR_SEGS_ON_DEVICE (segment i resident on the device of context
+ * i mod N: a sharded store generated or kept in HBM); output to host memory. */
 typedef struct kvr_mctx kvr_mctx;
 typedef struct kvr_multi_stats {
     double   ms_wall;         /* host wall time of the call: shard threads + merge                 */
@@ -277,9 +278,19 @@ int  kvr_last_multi_stats(const kvr_mctx *m, kvr_multi_stats *out);
 /* kvr_replay_live over several GPUs: each GPU reduces its shard to every key's
  * last record, tombstones included (a DEL on one GPU may delete a key another GPU SET), only
  * those come back, and the host keeps each key's last record over all shards if it is a SET —
- * exactly kvr_replay_live's output for the whole store.  Keys are compared in segs[] (host). */
+ * exactly kvr_replay_live's output for the whole store.  Every shard exports the key bytes of
+ * its last records (kvr_live_keys) and the merge compares those, so the segments may stay on
+ * their devices (KVR_SEGS_ON_DEVICE) with no key byte read from host segments.  Replaces the
+ * loop of engine.rs:55-57 + the map of engine.rs:137 / :141 on N GPUs. */
 int  kvr_replay_live_multi(kvr_mctx *m, const kvr_segment *segs, size_t n_segs, uint32_t flags,
                            kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err);
+/* The key bytes of the last kvr_replay_live_multi output, packed in its order: key i is
+ * keys[key_off[i] .. key_off[i + 1]), key_off has n_out + 1 entries, *key_bytes = the total.
+ * With the live tuples it is the String-keyed map of engine.rs:114 / index.rs:7 for a store whose
+ * bytes live in HBM.  KVR_CAPACITY (*key_bytes set) when a buffer is short, KVR_EINVAL when m
+ * holds no live output. */
+int  kvr_multi_live_keys(const kvr_mctx *m, uint8_t *keys, uint64_t keys_cap, uint64_t *key_off, size_t off_cap,
+                         uint64_t *key_bytes);
 
 /* Host helpers. */
 const char *kvr_strerror(int code);

@@ -98,6 +98,9 @@ VARIANTS = {
     "rt768": ["-DKVR_RT=768"],     # 12 stripes per workgroup
     "prio0": ["-DKVR_HOP_PRIO=0", "-DKVR_REC_PRIO=0"],   # no raised wave priority
     "fin0": ["-DKVR_FIN_PRIO=0"],  # the scan + finalize chain at priority 0
+    "pf1": ["-DKVR_PREFETCH=1"],   # a prefetch wave per workgroup (cfg2 1.540 vs 1.396 ms: not kept)
+    "lf0": ["-DKVR_LANEFRAME=0"],  # the scalar hop loop for every record
+    "a7": ["-DKVR_ABLATE=7"],      # loads + per-tile bookkeeping only (the memory floor at 16 waves/CU)
     "base": [],
 }
 

@@ -179,9 +179,15 @@ struct kvr_ctx {
     std::vector<kvr_segment> ing_segs;     // device pointers into ing, in push order
 };
 
-#define HIPCHK(x)                                   \
-    do {                                            \
-        if ((x) != hipSuccess) return KVR_EHIP;     \
+// a HIP failure returns KVR_EHIP and says which call failed on stderr (KVR_QUIET=1 silences it)
+#define HIPCHK(x)                                                                              \
+    do {                                                                                       \
+        const hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) {                                                                \
+            if (!getenv("KVR_QUIET")) fprintf(stderr, "kvr: %s failed: %s (%s:%d)\n", #x,      \
+                                              hipGetErrorName(e_), __FILE__, __LINE__);        \
+            return KVR_EHIP;                                                                   \
+        }                                                                                      \
     } while (0)
 
 // ---------------------------------------------------------------------------------------

@@ -11,18 +11,17 @@
  *   - errors: the store's first error is the minimum (segment, offset) error over the shards
  *     (engine.rs:56 stops at the first one; what other shards found after it is never reached);
  *   - expected CRCs (the caller's manifest in store tuple order) are checked on the merged order.
+ * Segments may be host bytes or resident in HBM (KVR_SEGS_ON_DEVICE: segment i on the device of
+ * context i mod N, as a sharded store generated or kept in HBM holds them).  The live-index form
+ * never reads key bytes on the host side from the segments: every shard exports the key bytes of
+ * its per-key last records (kvr_live_keys), and the merge compares those.
  */
 #include <thread>
 
-// key bytes of tuple t in the caller's host segments ([op][klen u32][key], engine.rs:169-171)
-static inline const uint8_t *mkey(const kvr_segment *segs, const kvr_tuple &t) {
-    return segs[t.seg_idx].bytes + t.rec_off + 5;
-}
-
-// the last record of each key over t[0, n) (in (segment, offset) order, keys read from host
-// segments): live[i] = 1 iff t[i] is its key's last record and a SET.  Keys split by tag into one
+// the last record of each key over t[0, n) (in (segment, offset) order; key i is kp[i], t[i].key_len
+// bytes): live[i] = 1 iff t[i] is its key's last record and a SET.  Keys split by tag into one
 // partition per thread; each partition keeps an open-addressing table of (tag << 32 | index).
-static void fold_last_parallel(const kvr_segment *segs, const kvr_tuple *t, size_t n, std::vector<uint8_t> &live) {
+static void fold_last_parallel(const uint8_t *const *kp, const kvr_tuple *t, size_t n, std::vector<uint8_t> &live) {
     live.assign(n, 0);
     if (n == 0) return;
     const uint32_t P = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -47,7 +46,7 @@ static void fold_last_parallel(const kvr_segment *segs, const kvr_tuple *t, size
                     if (sl == EMPTY) { sl = tag | i; break; }
                     if ((sl & 0xFFFFFFFF00000000ull) != tag) continue;
                     const kvr_tuple &y = t[(uint32_t)sl];
-                    if (y.key_len == x.key_len && memcmp(mkey(segs, y), mkey(segs, x), x.key_len) == 0) {
+                    if (y.key_len == x.key_len && memcmp(kp[(uint32_t)sl], kp[i], x.key_len) == 0) {
                         sl = tag | i;   // later record wins (engine.rs:137, :141)
                         break;
                     }
@@ -63,6 +62,10 @@ static void fold_last_parallel(const kvr_segment *segs, const kvr_tuple *t, size
 struct kvr_mctx {
     std::vector<kvr_ctx *> c;
     kvr_multi_stats st{};
+    // the key bytes of the last kvr_replay_live_multi output, packed in its order (kvr_multi_live_keys)
+    std::vector<uint8_t> keys;
+    std::vector<uint64_t> koff;
+    bool keys_valid = false;
 };
 
 extern "C" {
@@ -111,6 +114,17 @@ int kvr_replay_live_multi(kvr_mctx *m, const kvr_segment *segs, size_t n, uint32
     return replay_multi(m, segs, n, flags, nullptr, 0, out, cap, n_out, err, true);
 }
 
+int kvr_multi_live_keys(const kvr_mctx *m, uint8_t *keys, uint64_t keys_cap, uint64_t *key_off, size_t off_cap,
+                        uint64_t *key_bytes) {
+    if (!m || !key_bytes || (keys_cap && !keys) || (off_cap && !key_off)) return KVR_EINVAL;
+    if (!m->keys_valid) return KVR_EINVAL;
+    *key_bytes = m->keys.size();
+    if (m->keys.size() > keys_cap || m->koff.size() > off_cap) return KVR_CAPACITY;
+    if (!m->keys.empty()) memcpy(keys, m->keys.data(), m->keys.size());
+    memcpy(key_off, m->koff.data(), m->koff.size() * sizeof(uint64_t));
+    return KVR_OK;
+}
+
 }  // extern "C"
 
 // last: each shard reduces its tuples to every key's last record, tombstones included
@@ -119,10 +133,14 @@ int kvr_replay_live_multi(kvr_mctx *m, const kvr_segment *segs, size_t n, uint32
 static int replay_multi(kvr_mctx *m, const kvr_segment *segs, size_t n, uint32_t flags, const uint32_t *expected,
                         size_t n_expected, kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err, bool last) {
     if (!m || m->c.empty() || (!segs && n) || !n_out || (cap && !out)) return KVR_EINVAL;
-    if (flags & (KVR_SEGS_ON_DEVICE | KVR_OUT_ON_DEVICE | KVR_EXPECTED_ON_DEVICE)) return KVR_EINVAL;   // host in, host out
+    if (flags & ~KVR_SEGS_ON_DEVICE) return KVR_EINVAL;   // host output; segments on the host or on their shard's device
     if (err) memset(err, 0, sizeof(*err));
     *n_out = 0;
     memset(&m->st, 0, sizeof(m->st));
+    m->keys_valid = false;
+    m->keys.clear();
+    m->koff.assign(1, 0);
+    const uint32_t sflags = flags & KVR_SEGS_ON_DEVICE;
     for (size_t i = 1; i < n; ++i)
         if (segs[i].seg_id < segs[i - 1].seg_id) return KVR_EINVAL;   // caller sorts (engine.rs:51)
     const size_t N = m->c.size();
@@ -136,6 +154,8 @@ static int replay_multi(kvr_mctx *m, const kvr_segment *segs, size_t n, uint32_t
         m->st.bytes_in += segs[i].len;
     }
     std::vector<std::vector<kvr_tuple>> tv(N);
+    std::vector<std::vector<uint8_t>> kb(N);     // last: each shard's exported key bytes ...
+    std::vector<std::vector<uint64_t>> ko(N);    // ... and their offsets (kvr_live_keys)
     std::vector<int> rc(N, KVR_OK);
     std::vector<kvr_error> er(N);
     std::vector<size_t> nn(N, 0);
@@ -149,14 +169,23 @@ static int replay_multi(kvr_mctx *m, const kvr_segment *segs, size_t n, uint32_t
             size_t c = (size_t)(bytes / 256) + 4096 + sh[r].size();
             tv[r].resize(c);
             auto run = [&](size_t cc) {
-                return last ? kvr_replay_last(m->c[r], sh[r].data(), sh[r].size(), 0, tv[r].data(), cc, &nn[r], &er[r])
-                            : kvr_replay(m->c[r], sh[r].data(), sh[r].size(), 0, nullptr, 0, tv[r].data(), cc, &nn[r], &er[r]);
+                return last ? kvr_replay_last(m->c[r], sh[r].data(), sh[r].size(), sflags, tv[r].data(), cc, &nn[r], &er[r])
+                            : kvr_replay(m->c[r], sh[r].data(), sh[r].size(), sflags, nullptr, 0, tv[r].data(), cc, &nn[r], &er[r]);
             };
             int x = run(c);
             if (x == KVR_CAPACITY) {   // rare: denser than one record per 256 B; replay again into the exact size
                 c = nn[r];
                 tv[r].resize(c);
                 x = run(c);
+            }
+            if (last && x == KVR_OK) {   // the key bytes of the shard's per-key last records
+                uint64_t nb = 0;
+                ko[r].assign(nn[r] + 1, 0);
+                x = kvr_live_keys(m->c[r], 0, nullptr, 0, ko[r].data(), ko[r].size(), &nb);
+                if (x == KVR_CAPACITY || x == KVR_OK) {
+                    kb[r].resize(nb + 1);
+                    x = kvr_live_keys(m->c[r], 0, kb[r].data(), kb[r].size(), ko[r].data(), ko[r].size(), &nb);
+                }
             }
             kvr_stats s;
             kvr_last_stats(m->c[r], &s);
@@ -194,24 +223,30 @@ static int replay_multi(kvr_mctx *m, const kvr_segment *segs, size_t n, uint32_t
         size_t tot = 0;
         for (size_t r = 0; r < N; ++r) tot += nn[r];
         std::vector<kvr_tuple> mt;
+        std::vector<const uint8_t *> kp;
         mt.reserve(tot);
+        kp.reserve(tot);
         for (size_t i = 0; i < n; ++i) {
             const size_t r = i % N;
             const uint32_t j = (uint32_t)(i / N);
             size_t &p = pos[r];
             while (p < nn[r] && tv[r][p].seg_idx == j) {
+                kp.push_back(kb[r].data() + ko[r][p]);
                 kvr_tuple x = tv[r][p++];
                 x.seg_idx = (uint32_t)i;
                 mt.push_back(x);
             }
         }
         std::vector<uint8_t> live;
-        fold_last_parallel(segs, mt.data(), mt.size(), live);
+        fold_last_parallel(kp.data(), mt.data(), mt.size(), live);
         for (size_t i = 0; i < mt.size(); ++i) {
             if (!live[i]) continue;
             if (o < cap) out[o] = mt[i];
+            m->keys.insert(m->keys.end(), kp[i], kp[i] + mt[i].key_len);
+            m->koff.push_back(m->keys.size());
             ++o;
         }
+        m->keys_valid = true;
         *n_out = o;
         m->st.n_records = o;
         m->st.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

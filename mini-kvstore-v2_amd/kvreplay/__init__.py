@@ -143,6 +143,7 @@ def _load():
     rep.kvr_mctx_size.argtypes = [P]
     rep.kvr_replay_multi.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
     rep.kvr_replay_live_multi.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
+    rep.kvr_multi_live_keys.argtypes = [P, P, U64, P, SZ, C.POINTER(U64)]
     rep.kvr_replay_last.argtypes = [P, C.POINTER(Segment), SZ, U32, P, SZ, C.POINTER(SZ), C.POINTER(Error)]
     rep.kvr_last_multi_stats.argtypes = [P, C.POINTER(MultiStats)]
     rep.kvr_replay_stream.argtypes = [P, C.POINTER(Segment), SZ, U32, U64, P, SZ, P, SZ, C.POINTER(SZ),
@@ -388,19 +389,25 @@ class MultiContext:
         self._rep.kvr_last_multi_stats(self.h, C.byref(s))
         return s
 
-    def replay(self, segments, seg_ids=None, expected=None, cap=None, live=False):
-        """Same contract as Context.replay over host segments; returns ReplayResult (stats:
-        MultiStats).  live=True: kvr_replay_live_multi (each GPU reduces its shard to every key's
-        last record, tombstones included; the host keeps the live keys' final SETs)."""
+    def replay(self, segments, seg_ids=None, expected=None, cap=None, live=False, on_device=False):
+        """Same contract as Context.replay; returns ReplayResult (stats: MultiStats).
+        live=True: kvr_replay_live_multi (each GPU reduces its shard to every key's last record,
+        tombstones included; the host keeps the live keys' final SETs).  on_device: segments are
+        (ptr, len) pairs, segment i resident on the device of context i mod N."""
         keep = []
         n = len(segments)
         segs = (Segment * max(n, 1))()
         total = 0
         for i, s in enumerate(segments):
-            a = np.frombuffer(s, dtype=np.uint8) if isinstance(s, (bytes, bytearray)) else np.ascontiguousarray(s)
-            keep.append(a)
-            segs[i] = Segment(seg_ids[i] if seg_ids is not None else i, a.ctypes.data if a.size else None, a.size)
-            total += a.size
+            sid = seg_ids[i] if seg_ids is not None else i
+            if on_device:
+                ptr, ln = s
+            else:
+                a = np.frombuffer(s, dtype=np.uint8) if isinstance(s, (bytes, bytearray)) else np.ascontiguousarray(s)
+                keep.append(a)
+                ptr, ln = (a.ctypes.data if a.size else None), a.size
+            segs[i] = Segment(sid, ptr, ln)
+            total += ln
         exp_ptr, n_exp = None, 0
         if expected is not None:
             e = np.ascontiguousarray(expected, dtype=np.uint32)
@@ -411,18 +418,34 @@ class MultiContext:
         out_arr = np.zeros(max(cap, 1), dtype=TUPLE_DTYPE)
         n_out = C.c_size_t()
         err = Error()
+        fl = SEGS_ON_DEVICE if on_device else 0
         if live:
-            rc = self._rep.kvr_replay_live_multi(self.h, segs, n, 0, out_arr.ctypes.data, cap, C.byref(n_out),
+            rc = self._rep.kvr_replay_live_multi(self.h, segs, n, fl, out_arr.ctypes.data, cap, C.byref(n_out),
                                                  C.byref(err))
         else:
-            rc = self._rep.kvr_replay_multi(self.h, segs, n, 0, exp_ptr, n_exp, out_arr.ctypes.data, cap,
+            rc = self._rep.kvr_replay_multi(self.h, segs, n, fl, exp_ptr, n_exp, out_arr.ctypes.data, cap,
                                             C.byref(n_out), C.byref(err))
         if rc == CAPACITY:
-            return self.replay(segments, seg_ids, expected, cap=n_out.value + 16, live=live)
+            return self.replay(segments, seg_ids, expected, cap=n_out.value + 16, live=live, on_device=on_device)
         if rc < 0:
             raise NativeError(f"kvr_replay_multi: {self._rep.kvr_strerror(rc).decode()} ({rc})")
         tuples = out_arr[: n_out.value] if rc == OK else None
         return ReplayResult(rc, tuples, n_out.value, err if rc == CORRUPTED else None, self.last_stats())
+
+    def live_keys(self, n_live):
+        """Key bytes of the last replay(live=True) output of n_live tuples (kvr_multi_live_keys)
+        -> (packed key bytes uint8 array, offsets: n_live + 1 uint64)."""
+        kb = C.c_uint64()
+        offs = np.zeros(n_live + 1, dtype=np.uint64)
+        rc = self._rep.kvr_multi_live_keys(self.h, None, 0, offs.ctypes.data, offs.size, C.byref(kb))
+        if rc not in (OK, CAPACITY):
+            raise NativeError(f"kvr_multi_live_keys: {rc}")
+        keys = np.zeros(max(kb.value, 1), dtype=np.uint8)
+        rc = self._rep.kvr_multi_live_keys(self.h, keys.ctypes.data, keys.size, offs.ctypes.data, offs.size,
+                                           C.byref(kb))
+        if rc != OK:
+            raise NativeError(f"kvr_multi_live_keys: {rc}")
+        return keys[: kb.value], offs
 
 
 class SegmentList:

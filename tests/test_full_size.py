@@ -3,6 +3,8 @@ in HBM by the device generator exactly as bench.py does, replayed through the C 
 
   cfg2  64 x 64 MiB, 1 KiB values          tuple for tuple against the oracle (one segment per host
   cfg3  8 x 1 GiB, 64 KiB values           thread over the D2H copy of the same bytes) + manifest
+  cfg4  64 x 64 MiB, 50 % DEL (one GPU's   the compaction (kvr_compact) output byte for byte against
+        shard of the compaction config)    oracle_compact, and its replay against the oracle's
   cfg5  64 x 512 MiB (one GPU's 32 GiB     size-independent properties: records = generator count,
         shard of the 256 GiB store)        every CRC verified against the manifest with 0 failures,
                                            stripe re-walks reported; two segments against the oracle
@@ -19,6 +21,7 @@ pytestmark = pytest.mark.gpu
 SPECS = {   # bench.py CONFIGS (seed = 0x6B767265706C6179 + config number)
     "cfg2": (64, 64 << 20, dict(val_min=1024, val_max=1024, key_space_log2=20)),
     "cfg3": (8, 1 << 30, dict(val_min=65536, val_max=65536, key_space_log2=20)),
+    "cfg4": (64, 64 << 20, dict(val_min=1024, val_max=1024, key_space_log2=20, del_permille=500)),
     "cfg5": (64, 512 << 20, dict(val_min=16, val_max=1 << 20, key_space_log2=24, key_dist=1, del_permille=100)),
 }
 
@@ -89,3 +92,34 @@ def test_cfg5_shard_properties(gctx):
         got["seg_idx"] = 0
         got["flags"] = 0
         assert rc == 0 and np.array_equal(got, ref)
+
+
+def test_full_size_cfg4_compaction(gctx):
+    """BASELINE config 4's compaction at one GPU's full shard (64 x 64 MiB, 1 KiB values, 50 % DEL
+    of earlier-SET keys): kvr_compact with input and output in HBM, exactly as bench.py --mode
+    compact runs it.  The output bytes and the new segment boundaries equal oracle_compact's
+    (compaction.rs:9-29 with the intended live rewrite, README.md:283-287), and a replay of the new
+    segments on the GPU equals the oracle's replay of them, tuple for tuple (the pre-compaction
+    map, tests/store_integration.rs:20-31, now across a reopen)."""
+    data, offs, sizes, man, n_rec = _generate(gctx, "cfg4")
+    segs = [(data.data_ptr() + o, ln) for (ln, _), o in zip(sizes, offs)]
+    total = sum(ln for ln, _ in sizes)
+    target = 64 << 20
+    out = torch.empty(total + 4096, dtype=torch.uint8, device="cuda")
+    r = gctx.compact(segs, target, on_device=True, out_ptr=out.data_ptr(), out_cap=out.numel())
+    assert r.status == 0 and r.out_len == r.stats.bytes_out
+    torch.cuda.synchronize()
+    got = out[: r.out_len].cpu().numpy().tobytes()
+    host = data.cpu().numpy()
+    hsegs = [host[o: o + ln] for (ln, _), o in zip(sizes, offs)]
+    del data, out
+    rc, want, ends, _ = O.compact(hsegs, seg_target=target)
+    assert rc == 0
+    assert len(got) == len(want) and got == want
+    assert r.seg_ends == ends
+    news = O.split_segments(want, ends)
+    rco, ro, _ = O.replay(news)
+    rg = gctx.replay(news)
+    assert rco == rg.status == 0 and np.array_equal(rg.tuples, ro)
+    # every record of the new segments is a SET, and there is exactly one per live key
+    assert (ro["op"] == 0).all() and len(ro) == r.stats.n_live

@@ -90,3 +90,51 @@ def test_live_multi_matches_oracle_fold(n_ctx):
         assert r.status == 1 and (r.error.kind, r.error.seg_idx, r.error.rec_off) == (err.kind, err.seg_idx, err.rec_off)
     finally:
         m.close()
+
+
+@pytest.mark.parametrize("n_ctx", [2, 3])
+def test_live_multi_device_resident_with_keys(n_ctx):
+    """The sharded index of a store that lives in HBM (BASELINE cfg4/cfg5 shape: generated on the
+    device, never on the host): kvr_replay_live_multi with KVR_SEGS_ON_DEVICE, segment i on
+    context i mod N.  Keys repeat across segments and 35 % of records are DELs, so tombstones cross
+    shards.  The live tuples equal the oracle's fold of the whole store (engine.rs:137 / :141) and
+    the exported key bytes (kvr_multi_live_keys) equal the oracle's keys of those records."""
+    torch = pytest.importorskip("torch")
+    spec = K.GenSpec(seed=108, seg_bytes=250_000, key_space_log2=9, val_min=0, val_max=300, del_permille=350)
+    n = 7
+    ids = [1, 4, 9, 16, 25, 36, 49]
+    host = [K.gen_segment_cpu(spec, s)[0] for s in range(n)]   # byte-identical to the device generator
+    rc, t, _ = O.replay(host, seg_ids=ids)
+    live, nk, _ = O.fold_live(host, t)
+    want = t[live]
+    wkeys = [bytes(host[x["seg_idx"]][x["rec_off"] + 5: x["rec_off"] + 5 + x["key_len"]]) for x in want]
+    gctx = K.Context(0)
+    m = K.MultiContext([0] * n_ctx)
+    try:
+        sizes = [len(h) for h in host]
+        buf = torch.zeros(sum(s + 256 for s in sizes) + 256, dtype=torch.uint8, device="cuda")
+        ptrs, off = [], 16
+        for s, ln in enumerate(sizes):
+            got = gctx.gen_segment_device(spec, s, buf.data_ptr() + off, ln)
+            assert got[0] == ln
+            ptrs.append((buf.data_ptr() + off, ln))
+            off += ln + 256 + (s % 5)            # odd device alignments
+        torch.cuda.synchronize()
+        r = m.replay(ptrs, seg_ids=ids, live=True, on_device=True)
+        assert r.status == 0 and r.n == nk and np.array_equal(r.tuples, want)
+        keys, offs = m.live_keys(r.n)
+        assert offs[0] == 0 and int(offs[-1]) == len(keys)
+        assert [bytes(keys[offs[i]: offs[i + 1]]) for i in range(r.n)] == wkeys
+        # the plain (all tuples) multi replay from device shards too
+        r2 = m.replay(ptrs, seg_ids=ids, on_device=True)
+        assert r2.status == 0 and np.array_equal(r2.tuples, t)
+        # a torn device segment: the store's first error, as from host bytes
+        bad = list(ptrs)
+        bad[4] = (ptrs[4][0], ptrs[4][1] - 3)
+        rcb, _, err = O.replay(host[:4] + [host[4][:-3]] + host[5:], seg_ids=ids)
+        r3 = m.replay(bad, seg_ids=ids, live=True, on_device=True)
+        assert r3.status == rcb == 1
+        assert (r3.error.kind, r3.error.seg_idx, r3.error.rec_off) == (err.kind, err.seg_idx, err.rec_off)
+    finally:
+        m.close()
+        gctx.close()

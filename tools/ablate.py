@@ -66,6 +66,6 @@ for mask in masks:
         st = K.Stats()
         lib.kvr_last_stats(h, C.byref(st))
         ms.append(st.ms_replay)
-    t = min(ms[1:])
+    t = max(min(ms[1:]), 1e-9)
     print(f"{cfg} ablate={mask!s:>6} (1 records, 2 value CRC, 4 hops): rc={rc} n={n.value}/{nrec} k_replay {t:.3f} ms"
           f"  {tot / t / 1e6:.1f} GB/s  seg_bytes={sum(ln for ln, _ in sizes)}", flush=True)

@@ -1,60 +1,54 @@
 /*
- * kvr_replay_kernel.hip — k_replay, the hot path (gfx950).
+ * kvr_replay_kernel.hip — k_replay (V7), the hot path (gfx950).
  *
  * One WAVE replays one stripe (consecutive 8-KiB tiles of one segment) exactly as
  * src/store/engine.rs:79-154 walks a segment file, and emits one 32-B kvr_tuple per record with
  * the CRC-32 of its key and of its value (crc32fast::hash semantics, src/volume/storage.rs:27).
- * A workgroup holds 16 independent stripes that share the CRC tables; after the tables are staged
- * there is no workgroup barrier.
+ * A workgroup holds 12 independent stripes that share the CRC tables (the only LDS use); after
+ * the tables are staged there is no workgroup barrier.
  *
- * Per tile, lane l owns the 128-B unit [128 l, 128 l + 128), held in 32 registers; the next tile's
- * load goes into the same registers as soon as the CRC phase is done with them.
- *   F  framing, lane-parallel: stride prediction, verified.  Lane j decodes the
- *      record that would start at entry + j L (L = the last record's length) from a window of
- *      the segment bytes: opcode, key length, value length, every engine.rs framing check, and
- *      where its successor starts.  The first lane whose record is broken or whose successor is
- *      not the next prediction ends the round; the records before it and its own are the exact
- *      chain.  Equal-sized records (the benchmark shapes) take one round per tile; a broken
- *      record, varying lengths or a segment more than 2 GiB past the tile continue in the exact
- *      scalar hop loop (on the CU's scalar unit), which also reports the error of a broken
- *      record with every engine.rs check in engine.rs order.
+ * Per tile, lane l owns the 128-B unit [128 l, 128 l + 128), held in 32 registers and prefetched
+ * one tile ahead with 16-B buffer loads.  The tile is never copied anywhere else:
+ *   F  framing, exact from the tile entry (the previous tile's exit).  The wave hops header to
+ *      header in scalar registers, reading the header words straight out of the lanes'
+ *      registers (uniform register index + readlane).  Each SET value longer than 64 B that
+ *      crosses a unit boundary is folded on the spot into every unit's view: "which value
+ *      crosses my end, and where does it start" / "which value ends inside me, and where".
+ *      Records are taken in batches of 64.
  *      Only a stripe's first tile guesses: it takes its first plausible record start, which
  *      k_link checks against the previous stripe's exit (a wrong guess is re-walked).
- *   R  records: the lanes on the chain emit their record in parallel: the UTF-8 check of the key
- *      (engine.rs:114), the key CRC and the CRC of a value of at most 64 B or lying inside one
- *      unit, from the window the decode already holds.
+ *   R  records: lane j emits record j of the batch with the engine.rs check the hops did not
+ *      make (UTF-8 of the key), the key CRC and the CRC of a value of at most 64 B or lying
+ *      inside one unit, reading key
+ *      and value bytes through a range-checked buffer resource (they are L2-hot: this wave just
+ *      streamed them).  The record that broke the chain takes the general path (every check in
+ *      engine.rs order).
  *   C  long values: each lane CRCs its unit from registers in two independent chains, with a
- *      snapshot where a value ends and a restart where one starts; a segmented XOR scan across
- *      the wave (DPP only, each piece first pushed to its consumer with x^(8*128*d) from a
- *      per-lane column of nibble tables) gives the CRC register at every unit boundary; the lane
+ *      snapshot where a value ends and a restart where one starts; a segmented scan across the
+ *      wave (DPP row shifts, then row broadcasts; the multipliers x^(8*128*d) come from
+ *      conflict-free nibble tables) gives the CRC register at every unit boundary; the lane
  *      holding a value's last byte finishes that CRC.  A value running past the tile hands its
  *      register to the next tile of the stripe, so no variable GF(2) multiply is needed.
  *
- * CRC tables: slice-by-4 byte tables replicated per LDS bank group (see Crc), so no lookup of a
- * wave ever conflicts and its address is a single v_perm_b32 of the register byte and a lane
- * constant.
+ * CRC tables: the slice-by-2 byte tables (T0: one byte, T1: a byte followed by a zero byte) are
+ * replicated once per LDS bank: the entry for byte b of table t in lane l's copy sits at byte
+ * address b*256 + t*128 + 4 (l & 31), in bank (l & 31), so no lookup of a wave ever conflicts,
+ * and its address is a single v_perm_b32 of the register byte and the lane's constant.
  */
 #include "kvr_device.h"
 #include <type_traits>
 
 namespace kvr {
 
-// threads per workgroup: 16 stripes, one per wave.  The 32 tile registers leave room for four
-// waves per SIMD (under 128 VGPRs) when the next tile is loaded into the same registers once the
-// current one is done with (no separate prefetch buffer)
+// threads per workgroup: 16 stripes, one per wave.  The 32 tile registers leave room for four waves
+// per SIMD (under 128 VGPRs) when the next tile is loaded into the same registers once the current one is
+// done with (no separate prefetch buffer); that occupancy hides the load better than a full-tile
+// register prefetch at three waves (RT=768: 7% slower on cfg2)
 #ifndef KVR_RT
 #define KVR_RT 1024
 #endif
 constexpr int RT = KVR_RT;
-#ifndef KVR_PREFETCH   // 1: one wave per workgroup prefetches the workers' next tiles into the caches
-#define KVR_PREFETCH 0
-#endif
-#ifndef KVR_PF_DIST    // tiles ahead of its worker the prefetch wave runs
-#define KVR_PF_DIST 1
-#endif
-constexpr int NWAVE = RT / 64;            // waves per workgroup
-constexpr int WPB = NWAVE - (KVR_PREFETCH ? 1 : 0);   // stripes (worker waves) per workgroup
-constexpr uint32_t PDONE = 0xFFFFFFFFu;   // a worker's progress word once its stripe is done
+constexpr int WPB = RT / 64;              // stripes (waves) per workgroup
 constexpr int UW = SC / 4;                // dwords of a lane's unit
 constexpr int SC_LOG = 7;
 static_assert(SC == 1 << SC_LOG, "unit size");
@@ -67,7 +61,6 @@ static_assert(POOL_CHUNK >= TILE_RECS, "the rest of a tile's records fits in one
 constexpr int32_t FAR = 1 << 30;          // "ends beyond the tile" (tile-relative clamp)
 constexpr int KEYW = 6;                   // key words the record fast path reads at once (<= 24 B)
 constexpr int VALW = SMALL / 4;           // value words of a short value
-constexpr int WINW = KEYW + 3;            // decode window: dwords from the candidate's aligned word
 
 // The small tables come first: every table address is a lane-dependent VGPR plus a constant
 // below 64 KiB, which the ds_read instruction carries as its immediate offset.
@@ -76,34 +69,58 @@ struct __align__(16) Smem {
     uint32_t KT[4 * 8 * 16];              // [j][i][n]: (n << 4i) * x^(8*SC*2^j), j < 4
     uint32_t KQ[NQ * 8 * 16];             // [q][i][n]: (n << 4i) * x^(8*4q), q <= SC/4
     uint32_t IX[NIX + 3];                 // 0xFFFFFFFF * x^(8j): initial register pushed through j bytes
-    uint32_t MK[NWAVE][64];               // per wave: long-value marks by unit (framing)
-    uint32_t PROG[NWAVE];                 // per worker: the tile it is on (PDONE: finished)
-    uint32_t PSINK[64];                   // the prefetch wave's loads land here (never read)
     uint32_t C2[256 * 64];                // byte tables, row b = 256 B (64 KiB), see Crc
 };
 
-// wave priority (s_setprio) of the serial phases: the framing and the records phase are the
-// tile's critical path and share the CU with 15 other waves, so they issue ahead of waves in
-// their bulk CRC; the scan + finalize chain is raised too
+// wave priority (s_setprio) of the serial phases: the hop chain and the records phase are the
+// tile's critical path and share the CU's scalar unit with 15 other waves, so they issue ahead
+// of waves in their bulk CRC (cfg2: 1.90 -> 1.77 ms; cfg3 / cfg5 unchanged)
 #ifndef KVR_HOP_PRIO
 #define KVR_HOP_PRIO 2
 #endif
 #ifndef KVR_REC_PRIO
 #define KVR_REC_PRIO 1
 #endif
-#ifndef KVR_FIN_PRIO
-#define KVR_FIN_PRIO 1
+#ifndef KVR_FIN_PRIO       // the scan + finalize chain raised too (with the next tile's load issued before it:
+#define KVR_FIN_PRIO 1     // cfg2 1.552 vs 1.580 ms A/B)
 #endif
-#ifndef KVR_LANEFRAME   // 1: lane-parallel framing (0: the exact scalar hop loop for every record)
-#define KVR_LANEFRAME 1
+#ifndef KVR_BULK_LOWPRIO   // experiment: every phase raised except the unit CRC loop
+#define KVR_BULK_LOWPRIO 0
 #endif
-#ifndef KVR_FAST_BACKOFF   // tiles the scalar hop loop keeps after a lane-parallel round found < 3 records
-#define KVR_FAST_BACKOFF 4
+#ifndef KVR_HOPFAST   // 1: one compare per hop-loop check
+#define KVR_HOPFAST 1
+#endif
+#ifndef KVR_UNITLITE   // 1: unit-loop restarts as one input select, the word at qm loaded from memory
+#define KVR_UNITLITE 1
+#endif
+#ifndef KVR_DEFER   // 1: long-value unit views updated once per hop batch, not per hop
+#define KVR_DEFER 1
+#endif
+#ifndef KVR_LATEREC   // 1: the tile's last record batch emitted after the unit loop (key words loaded before it)
+#define KVR_LATEREC 0
+#endif
+#ifndef KVR_TRES_EARLY   // 1: the tile's TileRes stored before the CRC phase (0: at the end of the tile)
+#define KVR_TRES_EARLY 1
+#endif
+#ifndef KVR_EARLY   // 1: the next tile's load issued right after the unit loop (0: after the finalize)
+#define KVR_EARLY 1
+#endif
+#ifndef KVR_XFUSE   // 1: unit-loop registers as two XOR terms, the next input one v_bitop3 (0: materialized;
+#define KVR_XFUSE 0  // A/B: cfg2 1.661 vs 1.579 ms, cfg3 2.073 vs 2.089: not kept)
+#endif
+#ifndef KVR_HOP2   // 1: a fast hop loop for records read wholly from the registers, the exact loop after it
+#define KVR_HOP2 1
+#endif
+#ifndef KVR_FINR   // 1: a value end's last m & 3 bytes in one round of lookups (0: one round per byte)
+#define KVR_FINR 0
+#endif
+#ifndef KVR_XSCAN   // 1: pieces pushed to their consumer, XOR scan; 0: multiply at every scan step
+#define KVR_XSCAN 1
 #endif
 #ifndef KVR_ABLATE
-#define KVR_ABLATE 0   // diagnostic builds only: 1 skip records, 2 skip value CRC, 4 skip framing,
+#define KVR_ABLATE 0   // diagnostic builds only: 1 skip records, 2 skip value CRC, 4 skip hops,
 #endif                 // 8 skip the unit loop, 16 skip scan + finalize, 32 skip long-value folding,
-                       // 64 loads only
+                       // 64 loads only, 128 records without key loads
 
 #ifdef KVR_PROF
 __device__ unsigned long long g_prof[16];
@@ -130,25 +147,15 @@ __device__ __forceinline__ uint32_t wl32(uint32_t old, uint32_t val, uint32_t l)
     asm("v_writelane_b32 %0, %1, %2" : "+v"(old) : "s"(val), "{m0}"(l));   // lane select through m0
     return old;
 }
-__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {   // (readlane returns int: widen as unsigned)
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
-           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+    return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
 }
 
 // DPP move (no LDS): CTRL = row_shr:d (0x110 + d), row_bcast:15 (0x142), row_bcast:31 (0x143),
-// wave_shr:1 (0x138), wave_shl:1 (0x130); lanes without a source read 0
+// wave_shr:1 (0x138); lanes without a source read 0
 template <int CTRL, int ROWS = 0xF, bool BC = true>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xF, BC);
-}
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {   // (every lane gets the maximum)
-    v = __builtin_elementwise_max(v, dpp<0x111>(v));
-    v = __builtin_elementwise_max(v, dpp<0x112>(v));
-    v = __builtin_elementwise_max(v, dpp<0x114>(v));
-    v = __builtin_elementwise_max(v, dpp<0x118>(v));
-    v = __builtin_elementwise_max(v, dpp<0x142, 0xA, false>(v));
-    v = __builtin_elementwise_max(v, dpp<0x143, 0xC, false>(v));
-    return rl32(v, 63);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -157,21 +164,33 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {   // (every lane gets
 // Row b of Smem::C2 (64 dwords):
 //   [0, 32):  dword 8 t + r = table t (t = 0: one byte, t = k: a byte then k zero bytes) for byte
 //             b, replica r < 8 -- the slice-by-4 set of the unit loop
-//   [32, 48): table 0, replica lane & 15 (single-byte steps)
+//   [32, 48): table 0, replica lane & 15;  [48, 64): table 1, replica lane & 15 (slice-by-2 set)
 // A slice-by-4 step x = c ^ w needs T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3].  Lane group
 // g = (lane >> 3) & 3 takes table (g + i) & 3 in its i-th lookup and replica lane & 7, so the 32
 // lanes of a half-wave hit 32 distinct banks in every lookup; the group's byte order is absorbed
 // by rotating x left by 8 g first (one v_alignbit), which keeps the four selectors uniform.
+#ifndef KVR_S4
+#define KVR_S4 1
+#endif
 struct Crc {
     const uint8_t *t;   // Smem::C2
-    uint32_t L;         // byte 0: T0 copy (128 + 4 (lane & 15))
+    uint32_t L;         // byte 0: T0 copy (128 + 4 (lane & 15)), byte 1: T1 copy (192 + 4 (lane & 15))
     uint32_t L4;        // byte i: 4 (8 ((g + i) & 3) + (lane & 7)), this lane's i-th slice-by-4 lookup
     uint32_t rot;       // (32 - 8 g) & 31: x rotated right by this = x rotated left by 8 g
 };
 // v_perm_b32 builds the LDS address: byte 1 = a byte of x, byte 0 = this lane's table copy
-constexpr uint32_t SEL_T0_B0 = 0x0C0C0400u;
+constexpr uint32_t SEL_T1_B0 = 0x0C0C0401u, SEL_T0_B1 = 0x0C0C0500u, SEL_T0_B0 = 0x0C0C0400u;
 __device__ __forceinline__ uint32_t tget(const Crc &k, uint32_t x, uint32_t sel) {
     return *reinterpret_cast<const uint32_t *>(k.t + __builtin_amdgcn_perm(x, k.L, sel));
+}
+// the register after the two bytes sitting in x's low half (x = register ^ data)
+// (both lookups are issued before either is used: the empty asm keeps the scheduler from
+// serialising them, which would cost a third LDS round trip per word; it is not volatile, so
+// independent chains still interleave around it)
+__device__ __forceinline__ uint32_t crc2(const Crc &k, uint32_t x) {
+    uint32_t t0 = tget(k, x, SEL_T1_B0), t1 = tget(k, x, SEL_T0_B1);
+    asm("" : "+v"(t0), "+v"(t1));
+    return (x >> 16) ^ t0 ^ t1;
 }
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {   // one VALU op
     uint32_t r;
@@ -184,22 +203,56 @@ __device__ __forceinline__ uint32_t s4get(const Crc &k, uint32_t xr, uint32_t i)
     return *reinterpret_cast<const uint32_t *>(
         k.t + __builtin_amdgcn_perm(xr, k.L4, 0x0C0C0000u | ((7u - i) << 8) | i));
 }
-// (the four lookups are issued before any is used: the empty asm keeps the scheduler from
-// serialising them; it is not volatile, so independent chains still interleave around it)
 __device__ __forceinline__ uint32_t crc4(uint32_t c, uint32_t w, const Crc &k) {
+#if KVR_S4
     const uint32_t x = c ^ w, xr = __builtin_amdgcn_alignbit(x, x, k.rot);
     uint32_t a0 = s4get(k, xr, 0), a1 = s4get(k, xr, 1), a2 = s4get(k, xr, 2), a3 = s4get(k, xr, 3);
     asm("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
     return xor3(a0, a1, a2) ^ a3;
+#else
+    return crc2(k, crc2(k, c ^ w));
+#endif
 }
-// two independent chains stepped together from their inputs x = register ^ data
-__device__ __forceinline__ void crc4x2(uint32_t &ca, uint32_t xa, uint32_t &cb, uint32_t xb, const Crc &k) {
+// two independent chains stepped together: their lookups share one LDS round trip
+__device__ __forceinline__ void crc2x2(const Crc &k, uint32_t &xa, uint32_t &xb) {
+    uint32_t a0 = tget(k, xa, SEL_T1_B0), a1 = tget(k, xa, SEL_T0_B1);
+    uint32_t b0 = tget(k, xb, SEL_T1_B0), b1 = tget(k, xb, SEL_T0_B1);
+    asm("" : "+v"(a0), "+v"(a1), "+v"(b0), "+v"(b1));
+    xa = (xa >> 16) ^ a0 ^ a1;
+    xb = (xb >> 16) ^ b0 ^ b1;
+}
+// (pre = true: wa, wb are already the steps' inputs x = register ^ data)
+__device__ __forceinline__ void crc4x2(uint32_t &ca, uint32_t wa, uint32_t &cb, uint32_t wb, const Crc &k,
+                                       bool pre = false) {
+#if KVR_S4
+    const uint32_t xa = pre ? wa : ca ^ wa, xb = pre ? wb : cb ^ wb;
     const uint32_t ra = __builtin_amdgcn_alignbit(xa, xa, k.rot), rb = __builtin_amdgcn_alignbit(xb, xb, k.rot);
     uint32_t a0 = s4get(k, ra, 0), a1 = s4get(k, ra, 1), a2 = s4get(k, ra, 2), a3 = s4get(k, ra, 3);
     uint32_t b0 = s4get(k, rb, 0), b1 = s4get(k, rb, 1), b2 = s4get(k, rb, 2), b3 = s4get(k, rb, 3);
     asm("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
     ca = xor3(a0, a1, a2) ^ a3;
     cb = xor3(b0, b1, b2) ^ b3;
+#else
+    uint32_t xa = pre ? wa : ca ^ wa, xb = pre ? wb : cb ^ wb;
+    crc2x2(k, xa, xb);
+    crc2x2(k, xa, xb);
+    ca = xa;
+    cb = xb;
+#endif
+}
+// KVR_XFUSE: two chains' slice-by-4 step from their inputs x = register ^ data, each new register
+// kept as two terms t ^ u (three lookups XORed, the fourth alone), so the next step's input
+// t ^ u ^ data is one v_bitop3 instead of two XORs
+__device__ __forceinline__ void step4x2(uint32_t xa, uint32_t xb, const Crc &k, uint32_t &ta, uint32_t &ua,
+                                        uint32_t &tb, uint32_t &ub) {
+    const uint32_t ra = __builtin_amdgcn_alignbit(xa, xa, k.rot), rb = __builtin_amdgcn_alignbit(xb, xb, k.rot);
+    uint32_t a0 = s4get(k, ra, 0), a1 = s4get(k, ra, 1), a2 = s4get(k, ra, 2), a3 = s4get(k, ra, 3);
+    uint32_t b0 = s4get(k, rb, 0), b1 = s4get(k, rb, 1), b2 = s4get(k, rb, 2), b3 = s4get(k, rb, 3);
+    asm("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
+    ta = xor3(a0, a1, a2);
+    ua = a3;
+    tb = xor3(b0, b1, b2);
+    ub = b3;
 }
 __device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
     const uint32_t x = c ^ b;
@@ -235,9 +288,9 @@ __device__ __forceinline__ uint32_t kmulr(uint32_t v, const uint32_t *KR, uint32
 // ---------------------------------------------------------------------------------------
 // Segment reads relative to a tile's first byte (offset o = segment position lo + o), through a
 // buffer resource that ends at the segment's last 16-B word (words past it read as 0).  Used
-// for what is not in the registers: the candidates' decode windows, key and value bytes of the
-// records, headers past the tile end, the stripe's entry search.  Offsets the resource cannot
-// reach (before the tile, or past 2^31) go through plain loads; callers stay inside the segment.
+// for what is not in the registers: key and value bytes of the records, headers past the tile
+// end, the stripe's entry search.  Offsets the resource cannot reach (before the tile, or past
+// 2^31) go through plain loads; callers stay inside the segment.
 // ---------------------------------------------------------------------------------------
 struct TileSeg {
     __amdgpu_buffer_rsrc_t rs;
@@ -262,9 +315,21 @@ struct TileSeg {
     }
 };
 
-// raw CRC register (from ~0) over the n <= 4 NW bytes of a span whose aligned words are r[0..NW]
-// (sh = the span's start mod 4), and in *bad the 0x80 bits of those bytes; nw (wave-uniform) >=
-// the words any lane needs
+// raw CRC register (from ~0) over the n <= 4 NW bytes at offset o >= 0 (o + 4 NW + 4 <= lim),
+// and in *bad the 0x80 bits of those bytes; nw (wave-uniform) >= the words any lane needs
+template <int NW>
+__device__ __forceinline__ uint32_t crc_words(const uint32_t (&r)[NW + 1], const Crc &K, uint32_t sh, uint32_t n,
+                                              uint32_t nw, uint32_t *bad);
+template <int NW>
+__device__ __forceinline__ uint32_t crc_span(const TileSeg &ts, const Crc &K, int o, uint32_t n, uint32_t nw,
+                                             uint32_t *bad) {
+    const int a = o & ~3;
+    uint32_t r[NW + 1];
+#pragma unroll
+    for (int i = 0; i <= NW; ++i) r[i] = (uint32_t)i <= nw ? ts.w32a(a + 4 * i) : 0u;
+    return crc_words<NW>(r, K, (uint32_t)o & 3u, n, nw, bad);
+}
+// the same over words already loaded: r[i] = the aligned word i of the span (sh = its start mod 4)
 template <int NW>
 __device__ __forceinline__ uint32_t crc_words(const uint32_t (&r)[NW + 1], const Crc &K, uint32_t sh, uint32_t n,
                                               uint32_t nw, uint32_t *bad) {
@@ -284,16 +349,6 @@ __device__ __forceinline__ uint32_t crc_words(const uint32_t (&r)[NW + 1], const
     for (uint32_t b = 0; b < (n & 3u); ++b) c = crc1(c, (tail >> (8 * b)) & 255u, K);
     *bad = bd;
     return c;
-}
-// the same over segment bytes [o, o + n) loaded here (o >= 0, o + 4 NW + 4 <= lim)
-template <int NW>
-__device__ __forceinline__ uint32_t crc_span(const TileSeg &ts, const Crc &K, int o, uint32_t n, uint32_t nw,
-                                             uint32_t *bad) {
-    const int a = o & ~3;
-    uint32_t r[NW + 1];
-#pragma unroll
-    for (int i = 0; i <= NW; ++i) r[i] = (uint32_t)i <= nw ? ts.w32a(a + 4 * i) : 0u;
-    return crc_words<NW>(r, K, (uint32_t)o & 3u, n, nw, bad);
 }
 
 // CRC register update over segment bytes [o, o + n) (any length; the general path)
@@ -470,7 +525,7 @@ struct RecRes {          // one record's outcome on the general path
 };
 
 // parse + emit the record at tile offset o with every engine.rs check, in engine.rs order
-// (its value, if longer than SMALL, was folded by the framing)
+// (its value, if longer than SMALL, was folded by the hop loop)
 __device__ inline RecRes do_record(const TileSeg &ts, const Crc &K, int64_t o, uint32_t j, uint64_t slot, uint32_t seg,
                                    kvr_tuple *pool, uint64_t pool_cap) {
     RecRes ro;
@@ -509,21 +564,6 @@ __device__ inline RecRes do_record(const TileSeg &ts, const Crc &K, int64_t o, u
     return ro;
 }
 
-// the value CRC a record's own lane computes: a value of at most SMALL bytes, or one inside a
-// single unit (longer values crossing a unit boundary are folded into the unit CRC phase)
-__device__ __forceinline__ uint32_t short_value_crc(const TileSeg &ts, const Crc &K, int vb, uint32_t vlen) {
-    uint32_t vbad;
-    if (vlen <= (uint32_t)SMALL) {
-        if (vb + 4 * VALW + 8 <= ts.lim) return ~crc_span<VALW>(ts, K, vb, vlen, (uint32_t)VALW, &vbad);
-        return ~crc_long(ts, ~0u, vb, vlen, K);
-    }
-    if ((vb >> SC_LOG) == ((vb + (int)vlen - 1) >> SC_LOG)) {   // inside one unit
-        if (vb + 4 * UW + 8 <= ts.lim) return ~crc_span<UW>(ts, K, vb, vlen, (uint32_t)UW, &vbad);
-        return ~crc_long(ts, ~0u, vb, vlen, K);
-    }
-    return 0u;
-}
-
 // this lane's 128-B unit of tile k: eight 16-B raw buffer loads through a per-tile resource whose
 // range is the 16-B words touching the segment, so words outside it read as 0 in hardware
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -547,6 +587,24 @@ __device__ __forceinline__ void load_unit(const uint8_t *abase, int64_t d0, uint
     }
 }
 
+// KVR_PF: one 4-B load per lane at its unit of tile k brings the tile's 128-B lines towards L2
+// while the CRC phase runs, so the unit load issued after it finds them on chip (the result is
+// only kept alive, never used)
+#ifndef KVR_PF
+#define KVR_PF 0
+#endif
+__device__ __forceinline__ uint32_t touch_unit(const uint8_t *abase, int64_t d0, uint64_t len, uint32_t k, int lane) {
+    const int64_t t0 = (int64_t)k * TILE;
+    const int64_t endw = (d0 + (int64_t)len + 15) & ~(int64_t)15;
+    int64_t nrec = endw - t0;
+    nrec = nrec < 0 ? 0 : (nrec > TILE ? TILE : nrec);
+    const uint64_t b = (uint64_t)(abase + t0);
+    const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)b), bhi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(((uint64_t)bhi << 32) | blo), (short)0, __builtin_amdgcn_readfirstlane((int)nrec), 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, lane * SC, 0, 0);
+}
+
 // the reads of tile k relative to its first byte (see TileSeg)
 __device__ __forceinline__ TileSeg tile_seg(const uint8_t *abase, const uint8_t *seg, int64_t d0, uint64_t len,
                                             uint32_t k) {
@@ -567,73 +625,6 @@ __device__ __forceinline__ TileSeg tile_seg(const uint8_t *abase, const uint8_t 
 }
 
 // ---------------------------------------------------------------------------------------
-// the prefetch wave: the worker waves of a workgroup each hold one tile in registers and load the
-// next only when the current one's CRC is done, so at 15-16 waves per CU too few bytes are in
-// flight to keep HBM busy (the workers' loads alone reach about 4.4 TB/s).  This wave walks a
-// tile ahead of every worker of its workgroup and touches the tile's 64-B sectors (one dword
-// load per sector, all of a round in flight together), so a worker's own load finds its lines in
-// L2 or the Infinity Cache.  It only reads; results never depend on it.
-// ---------------------------------------------------------------------------------------
-__device__ inline void prefetch_wave(Smem &S, const SegDesc *__restrict__ segs, const StripeDesc *__restrict__ stripes,
-                                     uint32_t n_stripes, const RedoEnt *__restrict__ redo,
-                                     const LinkResult *__restrict__ link, int redo_mode, int lane) {
-    // lane w < WPB follows worker w: the stripe it walks, as the worker computes it
-    uint32_t t_next = 0, t_end = 0, t_begin = 0;
-    uint64_t abase = 0, span = 0;
-    if (lane < WPB) {
-        const uint32_t gw = blockIdx.x * WPB + (uint32_t)lane;
-        bool have;
-        uint32_t si = gw;
-        if (redo_mode) {
-            have = gw < link->n_redo && link->status == 3;
-            if (have) si = redo[gw].stripe;
-        } else {
-            have = gw < n_stripes;
-        }
-        if (have) {
-            const StripeDesc sd = stripes[si];
-            const SegDesc sg = segs[sd.seg];
-            t_begin = sd.t_begin;
-            t_next = sd.t_begin + 1u;
-            t_end = sd.t_end < sg.n_tiles ? sd.t_end : sg.n_tiles;
-            abase = (uint64_t)(sg.base - sg.d0);
-            span = ((uint64_t)sg.d0 + sg.len + 15u) & ~15ull;   // bytes from abase the segment covers
-        }
-    }
-    uint32_t sink = 0;
-#pragma unroll 1
-    for (uint32_t guard = 0; guard < (1u << 24); ++guard) {
-        const uint32_t pr = lane < WPB ? __hip_atomic_load(&S.PROG[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                                       : PDONE;
-        if (__ballot(pr != PDONE) == 0ull) break;
-        const uint32_t at = pr > t_begin ? pr : t_begin;
-        const bool want = pr != PDONE && t_next < t_end && t_next <= at + (uint32_t)KVR_PF_DIST;
-        const uint64_t m = __ballot(want);
-        if (m == 0ull) { __builtin_amdgcn_s_sleep(2); continue; }
-        // one round: every wanted worker's next tile touched (two dwords per 128-B unit, one per
-        // 64-B sector), all loads in flight together, one wait at the end of the round
-        uint32_t t[WPB][2];
-#pragma unroll
-        for (int w = 0; w < WPB; ++w) {
-            t[w][0] = t[w][1] = 0u;
-            if ((m >> w) & 1ull) {
-                const uint64_t t0 = (uint64_t)rl32(t_next, w) * TILE;
-                const uint64_t b = rl64(abase, w) + t0, sp = rl64(span, w);
-                const int64_t nr = sp > t0 ? ((sp - t0) > (uint64_t)TILE ? TILE : (int64_t)(sp - t0)) : 0;
-                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                    (void *)b, (short)0, __builtin_amdgcn_readfirstlane((int)nr), 0x00020000);
-                t[w][0] = __builtin_amdgcn_raw_buffer_load_b32(rs, lane * SC, 0, 0);
-                t[w][1] = __builtin_amdgcn_raw_buffer_load_b32(rs, lane * SC + 64, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int w = 0; w < WPB; ++w) sink ^= t[w][0] ^ t[w][1];
-        t_next += want ? 1u : 0u;
-    }
-    S.PSINK[lane] = sink;   // (the touches' values are never used; this keeps them)
-}
-
-// ---------------------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
@@ -646,7 +637,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     __shared__ Smem S;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (int i = tid; i < 256 * 64; i += RT) {
-        const int d = i & 63, t = d < 32 ? d >> 3 : 0;
+        const int d = i & 63, t = d < 32 ? d >> 3 : (d >> 4) - 2;
         S.C2[i] = tb.crc8[t * 256 + (i >> 6)];
     }
     for (int i = tid; i < 8 * 16 * 64; i += RT)
@@ -654,21 +645,13 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     for (int i = tid; i < 4 * 8 * 16; i += RT) S.KT[i] = tb.kmul[i];
     for (int i = tid; i < NQ * 8 * 16; i += RT) S.KQ[i] = tb.kmul[KSET_Q * 8 * 16 + i];
     if (tid < NIX) S.IX[tid] = tb.initx[tid];
-    if (tid < NWAVE) S.PROG[tid] = 0u;
     __syncthreads();   // the only workgroup barrier: from here on every wave is on its own
-    // (the wave index made wave-uniform first: a divergent return would leave this wave running
-    // the worker code below with EXEC = 0, and its scalar loads are not masked)
-    if (KVR_PREFETCH && __builtin_amdgcn_readfirstlane(wv) == WPB) {
-        prefetch_wave(S, segs, stripes, n_stripes, redo, link, redo_mode, lane);
-        return;
-    }
-    uint32_t *const MK = S.MK[wv];   // this wave's long-value marks
 
     Crc K;
     {
         const uint32_t g = (uint32_t)(lane >> 3) & 3u, r = (uint32_t)lane & 7u, r16 = (uint32_t)lane & 15u;
         K.t = reinterpret_cast<const uint8_t *>(S.C2);
-        K.L = 128u + 4u * r16;
+        K.L = (128u + 4u * r16) | ((192u + 4u * r16) << 8);
         K.L4 = 0;
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i) K.L4 |= (4u * (8u * ((g + i) & 3u) + r)) << (8 * i);
@@ -678,13 +661,12 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     const uint32_t gw = blockIdx.x * WPB + (uint32_t)__builtin_amdgcn_readfirstlane(wv);
     uint32_t si;
     uint64_t forced = NONE;
-    uint32_t *const prog = &S.PROG[wv];   // this worker's progress (read by the prefetch wave)
     if (redo_mode) {
-        if (gw >= link->n_redo || link->status != 3) { if (lane == 0) __hip_atomic_store(prog, PDONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); return; }
+        if (gw >= link->n_redo || link->status != 3) return;
         si = redo[gw].stripe;
         forced = redo[gw].entry;
     } else {
-        if (gw >= n_stripes) { if (lane == 0) __hip_atomic_store(prog, PDONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); return; }
+        if (gw >= n_stripes) return;
         si = gw;
     }
     const StripeDesc sd = stripes[si];
@@ -708,7 +690,6 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     uint64_t err_pos = NONE, err_aux = 0;
     uint32_t err_kind = 0, total = 0;
     uint64_t chunk_base = 0, chunk_left = 0;
-    uint32_t stride = 0, fast_skip = 0;           // lane-parallel framing: the last record length, tiles left to skip
     uint32_t carry = 0, c_state = 0;              // 1: a long value crosses the tile start (c_state: its register);
     uint64_t c_vb = 0, c_ve = 0, c_slot = 0;      // 2: pending (its value starts in a later tile)
 
@@ -719,12 +700,21 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     unsigned long long t_last = __builtin_amdgcn_s_memtime();
     unsigned long long prof_acc[16] = {};
 #endif
+    if (KVR_BULK_LOWPRIO) __builtin_amdgcn_s_setprio(2);
+    uint32_t pf_sink = 0;   // KVR_PF: the touch load's result, kept alive until this wait
+    // KVR_LATEREC: the tile's last record batch, emitted after the unit loop (its key words are
+    // loaded before it, so their latency runs under the loop)
+    bool pend = false;
+    int32_t pm_rec = -1;
+    uint32_t pm_op = 0, pm_klen = 0, pm_vlen = 0, pm_nw = 0, pm_nrec0 = 0;
+    uint64_t pm_slot = 0;
+    uint32_t kr[KEYW + 1];
     for (;; ++k) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (KVR_PF) asm volatile("" ::"v"(pf_sink));
         KVR_STAMP(5);
         const bool in_stripe = k < sd.t_end;
         if (stop || (!in_stripe && !carry) || k >= sg.n_tiles) break;
-        if (KVR_PREFETCH && lane == 0) __hip_atomic_store(prog, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (!loaded) {
             load_unit(abase, d0, len, k, lane, w);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -735,6 +725,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
 #pragma unroll
             for (int i = 0; i < UW; ++i) x ^= w[i];
             if (x == 0x9E3779B9u && lane == 0) atomicOr(&ctr->overflow, 8u);   // keeps the loads alive
+            if (in_stripe) total += 0;
             carry = 0;
             continue;
         }
@@ -776,6 +767,10 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                 }
                 cm[i >> 3] |= z >> (7 - (i & 7));
             }
+            KVR_STAMP(11);
+#ifdef KVR_PROF
+            prof_acc[14] += 1000;   // search tiles, x1000
+#endif
             // each round every lane tests one survivor, so the lanes' plausible() calls (dependent
             // loads) run side by side; a lane keeps its lowest plausible start, and lanes above the
             // lowest lane holding one stop (unit positions grow with the lane)
@@ -796,14 +791,17 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     if (o >= o0 && o < o1 && (cand < 0 || o < cand) && plausible(ts, o)) cand = o;
                 }
             }
+            KVR_STAMP(12);
             const uint64_t fnd = __ballot(cand >= 0);
             const uint64_t mn = fnd == 0ull ? NONE : (uint64_t)(lo + (int64_t)rl32((uint32_t)cand, (int)__builtin_ctzll(fnd)));
             if (mn != NONE) { entry = mn; search = false; stripe_entry = mn; }
+            KVR_STAMP(13);
         }
         const bool walk = in_stripe && !search && entry < vhi;
         uint64_t tile_exit = entry;
         // the long values touching this tile, folded into every unit's view as they are found
-        // (per-lane flags as 32-bit values: a per-lane bool lives in an SGPR lane mask)
+        // (per-lane flags as 32-bit values: a per-lane bool lives in an SGPR lane mask, and every
+        // update of it is scalar work in the SALU-bound hop loop)
         int32_t vx = 0;                      // a long value crosses the end of this unit: its end
                                              // (tile-relative, clamped to FAR; 0: none)
         int32_t a_off = -1;                  // ... starting inside the unit at a_off
@@ -823,6 +821,19 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             if (ver > TILE) { out = true; out_ve = ve_abs; out_ref = ref; out_abs = is_abs; }
             any_long = true;
         };
+        // the same for a value of this tile's records, tile-relative [vb, ver) (ver <= 2^31), in
+        // 32-bit arithmetic (the hop loop's common case)
+        auto consider_rel = [&](int32_t vb, int32_t ver, uint32_t ref) {
+            const bool cx = vb < ue && ver > ue, cm = vb < us && ver > us && ver <= ue;
+            vx = cx ? ver : vx;
+            a_off = cx ? (vb >= us ? vb - us : -1) : a_off;
+            vx_carry = cx ? 0u : vx_carry;
+            m = cm ? ver - us : m;
+            m_ref = cm ? (uint64_t)ref : m_ref;
+            m_abs = cm ? 0u : m_abs;
+            if (ver > TILE) { out = true; out_ve = (uint64_t)(lo + ver); out_ref = ref; out_abs = false; }
+            any_long = true;
+        };
         uint32_t n_carry = 0;
         uint64_t n_vb = 0, n_ve = 0, n_ref = 0;   // the next tile's carry (n_ref: a slot, or a record index)
         bool n_abs = true;
@@ -835,236 +846,21 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         uint64_t b1 = 0, b2 = 0;
         uint32_t c1 = N32;
         uint32_t nrec = 0, err_rec = N32;    // records emitted; index of the tile's first error
-        // claim pool slots for nb more records of the tile (one run: a fresh chunk holds any
-        // tile's rest); returns the first slot
-        auto claim = [&](uint32_t nb) -> uint64_t {
-            if (nb > chunk_left) {
-                const uint64_t cm = pool_chunk > TILE_RECS ? pool_chunk : TILE_RECS;
-                unsigned long long bb = 0;
-                if (lane == 0) {
-                    bb = atomicAdd(&ctr->pool_cursor, (unsigned long long)cm);
-                    if (bb + cm > pool_cap) atomicOr(&ctr->overflow, 1u);
-                }
-                chunk_base = uni64(bb);
-                chunk_left = cm;
-                if (nrec) { b2 = chunk_base; c1 = nrec; }   // the tile's second run
-            }
-            if (nrec == 0) b1 = chunk_base;
-            const uint64_t s0 = chunk_base;
-            chunk_base += nb;
-            chunk_left -= nb;
-            return s0;
-        };
-        // a batch's long values crossing a unit boundary: each marks its first unit with its lane
-        // + 1 (lmark); one DPP prefix max over the units finds, for every unit, the last one
-        // starting at or before it (and, shifted by one lane, before it); two ds_bpermute fetch
-        // that record's value span from its lane.  Long values are disjoint and in order (lane
-        // order = position order), so these are the only candidates.  rank: the record's index
-        // within the tile's records so far, per lane.
-        auto fold_views = [&](uint32_t lmark, int32_t rvb, int32_t re2, uint32_t rank) {
-            uint32_t pm = lmark;
-            pm = __builtin_elementwise_max(pm, dpp<0x111>(pm));
-            pm = __builtin_elementwise_max(pm, dpp<0x112>(pm));
-            pm = __builtin_elementwise_max(pm, dpp<0x114>(pm));
-            pm = __builtin_elementwise_max(pm, dpp<0x118>(pm));
-            pm = __builtin_elementwise_max(pm, dpp<0x142, 0xA, false>(pm));
-            pm = __builtin_elementwise_max(pm, dpp<0x143, 0xC, false>(pm));
-            const uint32_t pp = dpp<0x138>(pm);   // wave_shr:1: the marks before this unit
-            const int ic = 4 * (int)(pm ? pm - 1u : 0u), ip = 4 * (int)(pp ? pp - 1u : 0u);
-            const int32_t vbc = __builtin_amdgcn_ds_bpermute(ic, rvb), e2c = __builtin_amdgcn_ds_bpermute(ic, re2);
-            const int32_t e2p = __builtin_amdgcn_ds_bpermute(ip, re2);
-            const uint32_t rkp = (uint32_t)__builtin_amdgcn_ds_bpermute(ip, (int)rank);
-            const bool cx = pm != 0u && e2c > ue;
-            vx = cx ? e2c : vx;
-            a_off = cx ? (vbc >= us ? vbc - us : -1) : a_off;
-            vx_carry = cx ? 0u : vx_carry;
-            const bool cmn = pp != 0u && e2p > us && e2p <= ue;
-            m = cmn ? e2p - us : m;
-            m_ref = cmn ? (uint64_t)rkp : m_ref;
-            m_abs = cmn ? 0u : m_abs;
-            // a value crossing the last unit's end runs past the tile (ue = TILE there)
-            const uint32_t e63 = rl32(cx ? (uint32_t)e2c : 0u, 63);
-            if (e63 != 0u) {
-                out = true; out_ve = (uint64_t)(lo + (int32_t)e63);
-                out_ref = rl32((uint32_t)__builtin_amdgcn_ds_bpermute(ic, (int)rank), 63); out_abs = false;
-            }
-            any_long = true;
-        };
         if (walk) {
             // positions are tile-relative, in 32 bits unless the segment runs more than 2 GiB past
-            // the tile (then the 64-bit copy of the exact hop loop takes the whole tile)
+            // the tile (then a 64-bit copy of the hop loop runs): the bounds checks stay scalar
             const bool huge = rem > 0x7FFFFFFFll;
             int64_t p = (int64_t)entry - lo;
             bool broke = false;              // the chain broke at the last record walked
             if (KVR_ABLATE & 4) p = vhi_r;
-            if (KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
-#if KVR_LANEFRAME
-            if (!huge && p < vhi_r && fast_skip == 0u) {
-                // ---- lane-parallel framing: stride prediction, verified -----------------------
-                // Lane j decodes the record that would start at cur + j L, L = the length of the
-                // last record walked (in a store of equal-sized records, every record of the tile
-                // in one round).  Each lane reads its record's header from a window of the segment
-                // bytes (opcode, key length, value length, every engine.rs framing check) and
-                // computes where its successor starts.  Lane 0's position is exact; lane j's is
-                // exact if every lane below it had a valid record whose successor was the predicted
-                // position, so the first mismatch f ends the round: records 0 .. f are the chain
-                // (f's own successor is exact, so the next round predicts from there).  A broken
-                // record, or rounds that stop finding runs of equal lengths, leave the rest of the
-                // tile to the exact scalar hop loop below.
-                const int32_t vhiT = (int32_t)vhi_r, remT = (int32_t)rem;
-                int32_t cur = (int32_t)p;
-                uint32_t L = stride;
-#pragma unroll 1
-                while (cur < vhiT) {
-                    const bool one = L == 0u || L >= (uint32_t)TILE;   // no usable stride: lane 0 only
-                    const int32_t c = cur + (one ? 0 : lane * (int32_t)L);
-                    const bool act = lane == 0 || (!one && c < vhiT);
-                    const int32_t a = c & ~3;
-                    const uint32_t s = (uint32_t)c & 3u;
-                    uint32_t win[WINW];
-#pragma unroll
-                    for (int i = 0; i < WINW; ++i) win[i] = act ? ts.w32a(a + 4 * i) : 0u;
-                    const uint32_t x0 = __builtin_amdgcn_alignbyte(win[1], win[0], s);
-                    const uint32_t x1 = __builtin_amdgcn_alignbyte(win[2], win[1], s);
-                    const uint32_t op = x0 & 255u, klen = (x0 >> 8) | (x1 << 24);
-                    // engine.rs framing checks, tile-relative in 32 bits (rem < 2^31)
-                    const uint32_t room = (uint32_t)(remT - c);
-                    bool ok = act && op <= 1u && c < vhiT && room >= 5u && klen <= room - 5u;
-                    const uint32_t e = (uint32_t)c + 5u + (ok ? klen : 0u);   // < 2^31
-                    const bool need_v = ok && op == 0u;
-                    ok = ok && (!need_v || (uint32_t)remT - e >= 4u);
-                    // the value length: from the window when the key length is lane 0's (one length
-                    // for every key is the usual case) and the field lies in it, else from memory
-                    const uint32_t ku = rl32(klen, 0);
-                    uint32_t vlen = 0;
-                    bool vdone = false;
-                    {
-                        const uint32_t dd = 5u + ku, B0 = dd >> 2;
-                        if (B0 >= 1u && B0 <= (uint32_t)(WINW - 3)) {
-                            uint32_t wa = 0, wb = 0, wc = 0;
-#pragma unroll
-                            for (int bb = 1; bb <= WINW - 3; ++bb)
-                                if (B0 == (uint32_t)bb) { wa = win[bb]; wb = win[bb + 1]; wc = win[bb + 2]; }
-                            const uint32_t oo = s + (dd & 3u);
-                            const bool cy = oo >= 4u;
-                            vlen = __builtin_amdgcn_alignbyte(cy ? wc : wb, cy ? wb : wa, oo & 3u);
-                            vdone = klen == ku;
-                        }
-                    }
-                    if (need_v && ok && !vdone) vlen = ts.u32((int64_t)e);
-                    const uint32_t vb = e + 4u;
-                    ok = ok && (!need_v || vlen <= (uint32_t)remT - vb);
-                    const uint32_t nx = op == 1u ? e : vb + vlen;
-                    // the first lane whose record is broken or whose successor is not the next
-                    // prediction (the last active lane's successor is unconstrained)
-                    const uint64_t actm = __ballot(act);
-                    const int n = (int)__builtin_popcountll(actm);
-                    const bool mis = act && (!ok || (lane < n - 1 && nx != (uint32_t)(c + (int32_t)L)));
-                    const uint64_t mm = __ballot(mis);
-                    const int f = mm ? (int)__builtin_ctzll(mm) : n - 1;
-                    const bool okf = rl32(ok ? 1u : 0u, f) != 0u;
-                    const uint32_t cf = rl32((uint32_t)c, f);
-                    const uint32_t n_on = okf ? (uint32_t)f + 1u : (uint32_t)f;
-                    if (n_on) {
-                        // the walked records, lane j = record nrec + j
-                        if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
-                        const bool on = (uint32_t)lane < n_on;
-                        const uint64_t slot0 = claim(n_on);
-                        const uint32_t kmx = wave_max(on ? klen : 0u);
-                        uint32_t rerr = N32, rkind = 0;
-                        uint64_t raux = 0;
-                        if (on && !(KVR_ABLATE & 1)) {
-                            const uint32_t kc = kmx > 4u * KEYW ? 4u * KEYW : kmx;
-                            const uint32_t nw = (kc + 3u) >> 2;   // key words of the longest key
-                            uint32_t kr[KEYW + 1];
-#pragma unroll
-                            for (int i = 0; i <= KEYW; ++i) kr[i] = s == 3u ? win[i + 2] : win[i + 1];
-                            const int kb = c + 5;
-                            uint32_t cc = ~0u, bad = 0x80u;
-                            if (klen <= 4u * KEYW) cc = crc_words<KEYW>(kr, K, (s + 1u) & 3u, klen, nw, &bad);
-                            if (bad != 0u) {              // non-ASCII or long key: the full UTF-8 check
-                                uint64_t vu = 0;
-                                uint32_t el = 0;
-                                if (!utf8_check(ts, kb, klen, &vu, &el)) {   // engine.rs:114
-                                    rerr = nrec + (uint32_t)lane; rkind = KVR_E_UTF8; raux = vu | ((uint64_t)el << 32);
-                                } else {
-                                    cc = crc_long(ts, ~0u, kb, klen, K);
-                                }
-                            }
-                            if (rerr == N32) {
-                                kvr_tuple t;
-                                t.rec_off = (uint64_t)(lo + c);
-                                t.seg_idx = sd.seg;
-                                t.key_len = klen;
-                                t.val_len = op == 0u ? vlen : 0u;
-                                t.crc32 = op == 0u ? short_value_crc(ts, K, (int)vb, vlen) : 0u;
-                                t.key_tag = ~cc;
-                                t.op = (uint8_t)op;
-                                t.flags = 0;
-                                t.reserved = 0;
-                                const uint64_t slot = slot0 + (uint64_t)lane;
-                                if (slot < pool_cap) pool[slot] = t;
-                            }
-                        }
-                        // long values crossing a unit boundary: marked at their first unit (a scatter
-                        // through this wave's LDS row), then folded into every unit's view
-                        const bool lv = on && op == 0u && vlen > (uint32_t)SMALL &&
-                                        ((vb ^ (vb + vlen - 1u)) >> SC_LOG) != 0u;
-                        const uint64_t lvm = __ballot(lv);
-                        if (lvm && !(KVR_ABLATE & 32)) {
-                            MK[lane] = 0u;
-                            __builtin_amdgcn_wave_barrier();
-                            if (lv && vb < (uint32_t)TILE) MK[vb >> SC_LOG] = (uint32_t)lane + 1u;
-                            __builtin_amdgcn_wave_barrier();
-                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                            const uint32_t lmark = MK[lane];
-                            // a long value starting past the tile end (only the last record): carried
-                            const int jl = 63 - (int)__builtin_clzll(lvm);
-                            const uint32_t vbl = rl32(vb, jl);
-                            if (vbl >= (uint32_t)TILE) {
-                                n_carry = 2; n_vb = (uint64_t)(lo + (int64_t)vbl);
-                                n_ve = (uint64_t)(lo + (int64_t)vbl + rl32(vlen, jl));
-                                n_ref = nrec + (uint32_t)jl; n_abs = false;
-                            }
-                            fold_views(lmark, (int32_t)vb, (int32_t)(vb + vlen), nrec + (uint32_t)lane);
-                        } else if (lvm) {
-                            any_long = true;
-                        }
-                        // the first error of the batch (lowest record index)
-                        if (__ballot(rerr != N32)) {
-                            const int el = (int)__builtin_ctzll(__ballot(rerr != N32));
-                            err_rec = rl32(rerr, el);
-                            err_kind = rl32(rkind, el);
-                            err_aux = rl64(raux, el);
-                            err_pos = (uint64_t)(lo + (int64_t)(int32_t)rl32((uint32_t)c, el));
-                        }
-                        nrec = err_rec != N32 ? err_rec : nrec + n_on;
-                        if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
-                    }
-                    if (!okf) { cur = (int32_t)cf; break; }    // a broken record at cf: the exact loop reports it
-                    const uint32_t nf = rl32(nx, f);
-                    L = nf - cf;                                // record f's length predicts the next round
-                    cur = (int32_t)nf;
-                    if (err_rec != N32) break;
-                    if (!one && n_on < 3u && cur < vhiT) {      // lengths vary: the scalar loop is cheaper
-                        fast_skip = KVR_FAST_BACKOFF;
-                        break;
-                    }
-                }
-                stride = L;
-                p = cur;
-            } else if (fast_skip) {
-                --fast_skip;
-            }
-#endif
-            // ---- the exact scalar hop loop: anything the lane-parallel framing left -----------
-            int64_t lastq = -1;              // the last record start it walked (its length is the next stride)
 #pragma unroll 1
             while (p < vhi_r && !broke && err_rec == N32) {
                 // exact hops; lane j keeps record nrec + j (per-lane selects)
                 uint32_t nb = 0, kmx = 0;
                 int32_t myrec = -1;
                 uint32_t my_op = 0, my_klen = 0, my_vlen = 0;
+                // KVR_DEFER: a long value found by the hop chain only marks its first unit
+                // (lmark[unit] = its batch index + 1); the unit views are updated once per batch
                 uint32_t lmark = 0, bl = 0;
                 auto hops = [&](auto q) -> decltype(q) {
                     using T = decltype(q);
@@ -1082,7 +878,6 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                             klen = remT - q >= 5 ? uni32(ts.u32(q + 1)) : 0u;
                         }
                         const bool me = lane == (int)nb;
-                        lastq = (int64_t)q;
                         myrec = me ? (int32_t)q : myrec;
                         my_op = me ? op : my_op;
                         my_klen = me ? klen : my_klen;
@@ -1102,31 +897,227 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                         if (vlen > (uint32_t)SMALL && (vb >> SC_LOG) != ((e2 - 1) >> SC_LOG)) {
                             const uint64_t idx = nrec + nb - 1;
                             if (KVR_ABLATE & 32) any_long = true;
-                            else if (vb < TILE) {
-                                // (a 64-bit walk: the value may end more than 2^31 bytes on, so it
-                                // is folded on the spot with its 64-bit end, not batched in 32 bits)
-                                if constexpr (sizeof(T) == 8) consider((int32_t)vb, (uint64_t)(lo + e2), idx, false, false);
-                                else { lmark = wl32(lmark, nb, (uint32_t)vb >> SC_LOG); bl = 1; }
-                            }
+                            else if (vb < TILE) consider((int32_t)vb, (uint64_t)(lo + e2), idx, false, false);
                             else { n_carry = 2; n_vb = (uint64_t)(lo + vb); n_ve = (uint64_t)(lo + e2); n_ref = idx; n_abs = false; }
                         }
                         q = e2;
                     }
                     return q;
                 };
+                // the common case: 32-bit, flags as integers, the batch's per-lane record fields
+                // written with v_writelane (one instruction each, no lane compare and select)
+                auto hops32 = [&](int32_t q) -> int32_t {
+                    const int32_t remT = (int32_t)rem, vhiT = (int32_t)vhi_r;
+                    uint32_t brk = 0;
+#pragma unroll 1
+                    for (;;) {
+                        // (conditions combined as integers: one branch, no lane-mask arithmetic)
+#if KVR_HOPFAST
+                        if (((vhiT - 1 - q) | (63 - (int32_t)nb)) < 0) break;   // q >= vhi or 64 records
+#else
+                        if (((uint32_t)(q >= vhiT) | (uint32_t)(nb >= 64u)) != 0u) break;
+#endif
+                        uint32_t op, klen;
+                        if (q + 8 <= TILE) {
+                            const uint64_t x = tu64((int)q);
+                            op = (uint32_t)x & 255u;
+                            klen = (uint32_t)(x >> 8);
+                        } else {                     // the header crosses the tile end
+                            op = uni32(ts.b8(q));
+                            klen = remT - q >= 5 ? uni32(ts.u32(q + 1)) : 0u;
+                        }
+                        myrec = (int32_t)wl32((uint32_t)myrec, (uint32_t)q, nb);
+                        my_op = wl32(my_op, op, nb);
+                        my_klen = wl32(my_klen, klen, nb);
+                        ++nb;
+#if KVR_HOPFAST
+                        // (remT < 2^31 and q <= remT: the sums below stay below 2^32; a bad op
+                        // saturates the key length, so one compare covers op, room and klen)
+                        {
+                            const uint32_t kk = __builtin_elementwise_min(klen | (0u - (op >> 1)), 0x80000000u);
+                            if ((uint32_t)q + 5u + kk > (uint32_t)remT) { brk = 1; break; }
+                        }
+                        kmx = klen > kmx ? klen : kmx;
+                        const int32_t e = q + 5 + (int32_t)klen;
+                        if (op == 1u) { q = e; continue; }
+                        // (past the segment end the buffer reads 0; the compare below fails then)
+                        const uint32_t vlen = e + 8 <= TILE ? (uint32_t)tu64((int)e) : uni32(ts.u32(e));
+                        my_vlen = wl32(my_vlen, vlen, nb - 1u);
+                        const int32_t vb = e + 4;
+                        if ((uint32_t)vb + __builtin_elementwise_min(vlen, 0x80000000u) > (uint32_t)remT) { brk = 1; break; }
+#else
+                        const uint32_t room = (uint32_t)(remT - q);   // >= 0: q < vhi <= rem
+                        if (((uint32_t)(op > 1u) | (uint32_t)(room < 5u) | (uint32_t)(klen > room - 5u)) != 0u) { brk = 1; break; }
+                        kmx = klen > kmx ? klen : kmx;
+                        const int32_t e = q + 5 + (int32_t)klen;
+                        if (op == 1u) { q = e; continue; }
+                        const uint32_t vroom = (uint32_t)(remT - e);
+                        if (vroom < 4u) { brk = 1; break; }
+                        const uint32_t vlen = e + 8 <= TILE ? (uint32_t)tu64((int)e) : uni32(ts.u32(e));
+                        my_vlen = wl32(my_vlen, vlen, nb - 1u);
+                        const int32_t vb = e + 4;
+                        if (vlen > vroom - 4u) { brk = 1; break; }
+#endif
+                        const int32_t e2 = vb + (int32_t)vlen;
+                        if (vlen > (uint32_t)SMALL && (vb >> SC_LOG) != ((e2 - 1) >> SC_LOG)) {
+                            const uint32_t idx = nrec + nb - 1;
+                            if (KVR_ABLATE & 32) any_long = true;
+                            else if (vb < TILE) {
+                                if (KVR_DEFER) { lmark = wl32(lmark, nb, (uint32_t)vb >> SC_LOG); bl = 1; }
+                                else consider_rel(vb, e2, idx);
+                            }
+                            else { n_carry = 2; n_vb = (uint64_t)(lo + vb); n_ve = (uint64_t)(lo + e2); n_ref = idx; n_abs = false; }
+                        }
+                        q = e2;
+                    }
+                    broke = brk != 0;
+                    return q;
+                };
+#if KVR_HOP2
+                // KVR_HOP2: the fast loop takes only records whose header and value-length field sit
+                // in the registers and that pass every framing check; it stops before anything else
+                // (a field past the tile, a broken record), which the exact loop above then takes
+                // from the same position.  Nothing is written for a record before it is accepted, so
+                // each hop is two register reads, three range tests and the lane writes.
+                // the two words holding tile bytes [o, o + 8) (uniform o, o + 8 <= TILE): w[r] and
+                // w[r + 1] of lane o >> 7 moved under one register index, aligned in the vector unit
+                // (v_alignbyte takes the byte shift from o's low bits), then one readlane each; only
+                // a pair that wraps into the next lane (r = 31) goes through two separate reads
+                auto tpair = [&](int o, uint32_t &lo, uint32_t &hi) {
+                    const int r = (o >> 2) & 31, l = o >> 7;
+                    if (r != 31) {
+                        const uint32_t a = w[r], b = w[r + 1];
+                        lo = rl32(__builtin_amdgcn_alignbyte(b, a, (uint32_t)o), l);
+                        hi = rl32(b >> (8u * ((uint32_t)o & 3u)), l);
+                    } else {
+                        const uint64_t v = tu64(o);
+                        lo = (uint32_t)v;
+                        hi = (uint32_t)(v >> 32);
+                    }
+                };
+                auto hops_fast = [&](int32_t q) -> int32_t {
+                    const int32_t vhiT = (int32_t)vhi_r, remT = (int32_t)rem;
+                    const int32_t lim = remT < TILE - 4 ? remT : TILE - 4;   // e + 4 <= lim: vlen readable and inside the segment
+#pragma unroll 1
+                    for (;;) {
+                        if (((vhiT - 1 - q) | (63 - (int32_t)nb) | (TILE - 8 - q)) < 0) break;
+                        uint32_t x0, x1;
+                        tpair((int)q, x0, x1);
+                        const uint32_t op = x0 & 255u, klen = (uint32_t)((((uint64_t)x1 << 32) | x0) >> 8);
+                        // the value length is read for every record (a DEL ignores it), at a position
+                        // clamped into the registers: one exit test, no branch per record kind
+                        const uint32_t kk = __builtin_elementwise_min(klen, 0x40000000u);
+                        const uint32_t e = (uint32_t)q + 5u + kk, vb = e + 4u;
+                        uint32_t vraw, vhi_unused;
+                        tpair((int)__builtin_elementwise_min(e, (uint32_t)(TILE - 8)), vraw, vhi_unused);
+                        const uint32_t vlen = vraw & (op - 1u);   // (op 0: vraw, op 1: 0)
+                        // the tests as one sign: lim <= TILE - 4 and the key length clamped to 2^30
+                        // keep lim - vb inside int32; the value end is compared unsigned (vb < 2^31,
+                        // the value length clamped to 2^31 > remT, so a clamped length always fails)
+                        const uint32_t vv = __builtin_elementwise_min(vlen, 0x80000000u);
+                        const uint32_t vbad = vb + vv > (uint32_t)remT ? 0x80000000u : 0u;
+                        if ((int32_t)(((uint32_t)lim - vb) | vbad | (0u - (op >> 1))) < 0) break;
+                        const int32_t qn = (int32_t)(e + ((vlen + 4u) & (op - 1u)));
+                        if (vlen > (uint32_t)SMALL && ((vb ^ ((uint32_t)qn - 1u)) >> SC_LOG) != 0u) {   // vb < TILE here
+                            if (KVR_ABLATE & 32) any_long = true;
+                            else { lmark = wl32(lmark, nb + 1u, vb >> SC_LOG); bl = 1; }
+                        }
+                        myrec = (int32_t)wl32((uint32_t)myrec, (uint32_t)q, nb);
+                        my_op = wl32(my_op, op, nb);
+                        my_klen = wl32(my_klen, klen, nb);
+                        my_vlen = wl32(my_vlen, vlen, nb);
+                        ++nb;
+                        kmx = klen > kmx ? klen : kmx;
+                        q = qn;
+                    }
+                    return q;
+                };
+#endif
+                // the hop chain is the tile's serial critical path and shares the CU's scalar unit
+                // with 15 other waves: it issues at raised priority (KVR_HOP_PRIO)
+                if (KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
                 if (huge) p = hops((int64_t)p);
-                else p = hops((int32_t)p);
-                if (bl) {
+#if KVR_HOP2
+                else p = hops((int32_t)hops_fast((int32_t)p));
+#else
+                else p = hops32((int32_t)p);
+#endif
+                if (KVR_DEFER && bl) {
+                    // unit u's candidates: the batch's last long value starting in a unit <= u (it
+                    // crosses u's end if it ends past ue) and the last one starting before u (it
+                    // ends inside u if us < end <= ue).  Long values are disjoint and in order, so
+                    // these are the only ones that can; a prefix max over the marks finds them.
+                    uint32_t pm = lmark;
+                    pm = __builtin_elementwise_max(pm, dpp<0x111>(pm));
+                    pm = __builtin_elementwise_max(pm, dpp<0x112>(pm));
+                    pm = __builtin_elementwise_max(pm, dpp<0x114>(pm));
+                    pm = __builtin_elementwise_max(pm, dpp<0x118>(pm));
+                    pm = __builtin_elementwise_max(pm, dpp<0x142, 0xA, false>(pm));
+                    pm = __builtin_elementwise_max(pm, dpp<0x143, 0xC, false>(pm));
+                    const uint32_t pp = dpp<0x138>(pm);   // wave_shr:1: the marks before this unit
                     // lane j holds batch record j: its value [rvb, re2) (tile-relative)
                     const int32_t rvb = myrec + 9 + (int32_t)my_klen, re2 = rvb + (int32_t)my_vlen;
-                    fold_views(lmark, rvb, re2, nrec + (uint32_t)lane);
+                    const int ic = 4 * (int)(pm ? pm - 1u : 0u), ip = 4 * (int)(pp ? pp - 1u : 0u);
+                    const int32_t vbc = __builtin_amdgcn_ds_bpermute(ic, rvb), e2c = __builtin_amdgcn_ds_bpermute(ic, re2);
+                    const int32_t e2p = __builtin_amdgcn_ds_bpermute(ip, re2);
+                    const bool cx = pm != 0u && e2c > ue;
+                    vx = cx ? e2c : vx;
+                    a_off = cx ? (vbc >= us ? vbc - us : -1) : a_off;
+                    vx_carry = cx ? 0u : vx_carry;
+                    const bool cm = pp != 0u && e2p > us && e2p <= ue;
+                    m = cm ? e2p - us : m;
+                    m_ref = cm ? (uint64_t)(nrec + pp - 1u) : m_ref;
+                    m_abs = cm ? 0u : m_abs;
+                    // a value crossing the last unit's end runs past the tile (ue = TILE there)
+                    const uint32_t e63 = rl32(cx ? (uint32_t)e2c : 0u, 63);
+                    if (e63 != 0u) { out = true; out_ve = (uint64_t)(lo + (int32_t)e63); out_ref = nrec + rl32(pm, 63) - 1u; out_abs = false; }
+                    any_long = true;
                 }
-                const uint64_t slot = claim(nb) + (uint64_t)lane;
+                if (KVR_HOP_PRIO && !KVR_REC_PRIO) __builtin_amdgcn_s_setprio(KVR_BULK_LOWPRIO ? 2 : 0);
+                KVR_STAMP(1);
+                // pool slots of the batch (one run: a fresh chunk holds any tile's rest)
+                if (nb > chunk_left) {
+                    const uint64_t cm = pool_chunk > TILE_RECS ? pool_chunk : TILE_RECS;
+                    unsigned long long bb = 0;
+                    if (lane == 0) {
+                        bb = atomicAdd(&ctr->pool_cursor, (unsigned long long)cm);
+                        if (bb + cm > pool_cap) atomicOr(&ctr->overflow, 1u);
+                    }
+                    chunk_base = uni64(bb);
+                    chunk_left = cm;
+                    if (nrec) { b2 = chunk_base; c1 = nrec; }   // the tile's second run
+                }
+                if (nrec == 0) b1 = chunk_base;
+                const uint64_t slot = chunk_base + (uint64_t)lane;
+                chunk_base += nb;
+                chunk_left -= nb;
                 // the batch's records: lane j emits record nrec + j
                 uint32_t rerr = N32, rkind = 0;
                 uint64_t raux = 0;
                 const uint32_t j = nrec + (uint32_t)lane;
-                if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
+#if KVR_LATEREC
+                // the tile's last batch, no broken record and no value the records phase must read
+                // (values in one unit or of at most SMALL bytes): its key words are loaded now and
+                // the records are emitted after the unit loop
+                const int32_t vb_ = myrec + 9 + (int32_t)my_klen;
+                const bool vmem = myrec >= 0 && my_op == 0u &&
+                                  (my_vlen <= (uint32_t)SMALL || (vb_ >> SC_LOG) == ((vb_ + (int32_t)my_vlen - 1) >> SC_LOG));
+                if (!(KVR_ABLATE & 1) && !huge && !broke && p >= vhi_r && !__ballot(vmem)) {
+                    pend = true;
+                    pm_rec = myrec; pm_op = my_op; pm_klen = my_klen; pm_vlen = my_vlen;
+                    pm_slot = slot; pm_nrec0 = nrec;
+                    const uint32_t kc = kmx > 4u * KEYW ? 4u * KEYW : kmx;
+                    pm_nw = (kc + 3u) >> 2;
+                    const int kb = myrec + 5;
+                    const bool kf = myrec >= 0 && my_klen <= 4u * KEYW && kb + 4 * KEYW + 8 <= ts.lim;
+                    const int ka = kf ? (kb & ~3) : 0;
+#pragma unroll
+                    for (int i = 0; i <= KEYW; ++i) kr[i] = (uint32_t)i <= pm_nw ? ts.w32a(ka + 4 * i) : 0u;
+                    nrec += nb;   // (an error found after the loop lowers it)
+                    if (KVR_REC_PRIO) __builtin_amdgcn_s_setprio(KVR_BULK_LOWPRIO ? 2 : 0);
+                    continue;
+                }
+#endif
                 if (!(KVR_ABLATE & 1) && myrec >= 0) {
                     if (broke && lane == (int)nb - 1) {   // the record that broke the chain: every check
                         const RecRes r = do_record(ts, K, myrec, j, slot, sd.seg, pool, pool_cap);
@@ -1138,6 +1129,13 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                         const int kb = myrec + 5;
                         const uint32_t klen = my_klen;
                         uint32_t c = ~0u, bad = 0x80u;
+                        if (KVR_ABLATE & 128) {   // timing only: the key CRC over register words, no key loads
+                            uint32_t r_[KEYW + 1];
+#pragma unroll
+                            for (int i = 0; i <= KEYW; ++i) r_[i] = (uint32_t)kb * 0x9E3779B9u + (uint32_t)i;
+                            c = crc_words<KEYW>(r_, K, (uint32_t)kb & 3u, klen, nw, &bad);
+                            bad = 0u;
+                        } else
                         if (klen <= 4u * KEYW && kb + 4 * KEYW + 8 <= ts.lim) c = crc_span<KEYW>(ts, K, kb, klen, nw, &bad);
                         if (bad != 0u) {              // non-ASCII or long key: the full UTF-8 check
                             uint64_t vu = 0;
@@ -1153,53 +1151,128 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                             t.rec_off = (uint64_t)(lo + myrec);
                             t.seg_idx = sd.seg;
                             t.key_len = klen;
-                            t.val_len = my_op == 0u ? my_vlen : 0u;
-                            t.crc32 = my_op == 0u ? short_value_crc(ts, K, kb + (int)klen + 4, my_vlen) : 0u;
+                            t.val_len = 0;
+                            t.crc32 = 0;
                             t.key_tag = ~c;
                             t.op = (uint8_t)my_op;
                             t.flags = 0;
                             t.reserved = 0;
+                            if (my_op == 0u) {
+                                t.val_len = my_vlen;
+                                const int vb = kb + (int)klen + 4;
+                                uint32_t vbad;
+                                if (my_vlen <= (uint32_t)SMALL) {
+                                    if (vb + 4 * VALW + 8 <= ts.lim) t.crc32 = ~crc_span<VALW>(ts, K, vb, my_vlen, (uint32_t)VALW, &vbad);
+                                    else t.crc32 = ~crc_long(ts, ~0u, vb, my_vlen, K);
+                                } else if ((vb >> SC_LOG) == ((vb + (int)my_vlen - 1) >> SC_LOG)) {   // inside one unit
+                                    if (vb + 4 * UW + 8 <= ts.lim) t.crc32 = ~crc_span<UW>(ts, K, vb, my_vlen, (uint32_t)UW, &vbad);
+                                    else t.crc32 = ~crc_long(ts, ~0u, vb, my_vlen, K);
+                                }
+                            }
                             if (slot < pool_cap) pool[slot] = t;
                         }
                     }
                 }
+                KVR_STAMP(6);
                 // first error of the batch (lowest record index)
                 if (__ballot(rerr != N32)) {
-                    const int el = (int)__builtin_ctzll(__ballot(rerr != N32));
-                    err_rec = rl32(rerr, el);
+                    uint32_t er = rerr;
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) {
+                        const uint32_t o = __shfl_xor(er, d, 64);
+                        er = o < er ? o : er;
+                    }
+                    err_rec = uni32(er);
+                    const int el = (int)(err_rec - nrec);
                     err_kind = rl32(rkind, el);
                     err_aux = rl64(raux, el);
                     err_pos = (uint64_t)(lo + (int64_t)(int32_t)rl32((uint32_t)myrec, el));
                 }
                 nrec = err_rec != N32 ? err_rec : nrec + nb;
-                if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
+                if (KVR_REC_PRIO) __builtin_amdgcn_s_setprio(KVR_BULK_LOWPRIO ? 2 : 0);   // (records raised too)
+                KVR_STAMP(7);
             }
-            if (lastq >= 0 && !broke && !huge) stride = (uint32_t)(p - lastq);
-            if (KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(0);
             tile_exit = broke ? ERRP : (uint64_t)(lo + p);
         }
         if (c1 == N32) c1 = nrec;
-        // the tile's result record, stored ahead of the next tile's load, so that the wait for that
-        // load at the loop top does not also wait for this store's ack
-        if (in_stripe && lane == 0) {
+        // the tile's result record; KVR_TRES_EARLY: stored here, ahead of the next tile's load, so
+        // that the wait for that load at the loop top does not also wait for this store's ack
+        auto store_tres = [&]() {
             TileRes tr;
             tr.pool_off = nrec ? b1 : 0ull;
             tr.pool_off2 = b2;
             tr.count = nrec;
             tr.count1 = c1 < nrec ? c1 : nrec;
             tres[sg.tile0 + k] = tr;
-        }
+        };
+        if (KVR_TRES_EARLY && !KVR_LATEREC && in_stripe && lane == 0) store_tres();
         // a record index of this tile -> its pool slot
         auto slot_of = [&](uint64_t ref, bool is_abs) -> uint64_t {
             return is_abs ? ref : (ref < c1 ? b1 + ref : b2 + (ref - c1));
         };
         if (n_carry == 2u && !n_abs) n_ref = slot_of(n_ref, false);
+        if (KVR_PF && err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry))
+            pf_sink = touch_unit(abase, d0, len, k + 1, lane);
+
+        // KVR_LATEREC: the pending batch's records (key CRC from the preloaded words, tuples,
+        // the batch's first error), emitted before the finalize patches any of their crc32
+        auto rec2 = [&]() {
+            pend = false;
+            if (KVR_REC_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
+            uint32_t rerr = N32, rkind = 0;
+            uint64_t raux = 0;
+            const uint32_t j = pm_nrec0 + (uint32_t)lane;
+            if (pm_rec >= 0) {
+                const int kb = pm_rec + 5;
+                const uint32_t klen = pm_klen;
+                uint32_t c = ~0u, bad = 0x80u;
+                if (klen <= 4u * KEYW && kb + 4 * KEYW + 8 <= ts.lim) c = crc_words<KEYW>(kr, K, (uint32_t)kb & 3u, klen, pm_nw, &bad);
+                if (bad != 0u) {              // non-ASCII or long key: the full UTF-8 check
+                    uint64_t vu = 0;
+                    uint32_t el = 0;
+                    if (!utf8_check(ts, kb, klen, &vu, &el)) {   // engine.rs:114
+                        rerr = j; rkind = KVR_E_UTF8; raux = vu | ((uint64_t)el << 32);
+                    } else {
+                        c = crc_long(ts, ~0u, kb, klen, K);
+                    }
+                }
+                if (rerr == N32) {   // (a SET's value is long: its crc32 comes from the CRC phase)
+                    kvr_tuple t;
+                    t.rec_off = (uint64_t)(lo + pm_rec);
+                    t.seg_idx = sd.seg;
+                    t.key_len = klen;
+                    t.val_len = pm_op == 0u ? pm_vlen : 0u;
+                    t.crc32 = 0;
+                    t.key_tag = ~c;
+                    t.op = (uint8_t)pm_op;
+                    t.flags = 0;
+                    t.reserved = 0;
+                    if (pm_slot < pool_cap) pool[pm_slot] = t;
+                }
+            }
+            if (__ballot(rerr != N32)) {
+                uint32_t er = rerr;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) {
+                    const uint32_t o = __shfl_xor(er, d, 64);
+                    er = o < er ? o : er;
+                }
+                err_rec = uni32(er);
+                const int el = (int)(err_rec - pm_nrec0);
+                err_kind = rl32(rkind, el);
+                err_aux = rl64(raux, el);
+                err_pos = (uint64_t)(lo + (int64_t)(int32_t)rl32((uint32_t)pm_rec, el));
+                nrec = err_rec;
+            }
+            if (KVR_REC_PRIO) __builtin_amdgcn_s_setprio(0);
+        };
         // the stripe goes on past this tile (a value running past its end is carried on)
         const bool need_next = err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry || out);
         KVR_STAMP(2);
         // ---- C. CRC of long values --------------------------------------------------------
         if (!(KVR_ABLATE & 2) && any_long) {
             KVR_STAMP(8);
+            if (KVR_BULK_LOWPRIO) __builtin_amdgcn_s_setprio(0);
             // the unit's two halves, words 0..15 (A) and 16..31 (B), CRC'd as independent chains
             // from a zero register, with the snapshot of the raw CRC of the unit's first 4 qm
             // bytes (the value ending here) and the restart at the value starting here (a)
@@ -1214,9 +1287,35 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             if (KVR_ABLATE & 8) {
                 ca = w[0]; cb = w[1];
             } else if (!__ballot(m != 0 || qa >= 0)) {
+#if KVR_XFUSE && KVR_S4
+                uint32_t ta = 0, ua = 0, tb = 0, ub = 0;
 #pragma unroll
-                for (int kk = 0; kk < H; ++kk) crc4x2(ca, ca ^ w[kk], cb, cb ^ w[kk + H], K);
+                for (int kk = 0; kk < H; ++kk) step4x2(xor3(ta, ua, w[kk]), xor3(tb, ub, w[kk + H]), K, ta, ua, tb, ub);
+                ca = ta ^ ua;
+                cb = tb ^ ub;
+#else
+#pragma unroll
+                for (int kk = 0; kk < H; ++kk) crc4x2(ca, w[kk], cb, w[kk + H], K);
+#endif
             } else {
+#if KVR_XFUSE && KVR_S4 && KVR_UNITLITE
+                // the snapshot is taken of the step's input x = c ^ w[qm] (no restart can fall on
+                // that step: a value starts at least 9 bytes after the one ending here) and the
+                // register recovered after the loop with the word at qm, which is loaded anyway
+                if (m != 0 && qm < UW) wm = ts.w32a(us + 4 * qm);
+                uint32_t ta = 0, ua = 0, tb = 0, ub = 0, snx = 0;
+#pragma unroll
+                for (int kk = 0; kk < H; ++kk) {
+                    const bool r = kk == qah, ra = r && !ab, rb = r && ab;
+                    const uint32_t xa = ra ? (w[kk] & amask) : xor3(ta, ua, w[kk]);
+                    const uint32_t xb = rb ? (w[kk + H] & amask) : xor3(tb, ub, w[kk + H]);
+                    snx = kk == qh ? (mb ? xb : xa) : snx;
+                    step4x2(xa, xb, K, ta, ua, tb, ub);
+                }
+                ca = ta ^ ua;
+                cb = tb ^ ub;
+                sn = snx ^ wm;
+#elif KVR_UNITLITE
                 // the word at qm comes from memory (issued here, used after the scan), and a restart
                 // is one select of the step's input: x = restart ? (w & amask) : (c ^ w)
                 if (m & 3) wm = ts.w32a(us + 4 * qm);
@@ -1227,19 +1326,33 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     const bool r = kk == qah, ra = r && !ab, rb = r && ab;
                     const uint32_t xa = ra ? (w[kk] & amask) : (ca ^ w[kk]);
                     const uint32_t xb = rb ? (w[kk + H] & amask) : (cb ^ w[kk + H]);
-                    crc4x2(ca, xa, cb, xb, K);
+                    crc4x2(ca, xa, cb, xb, K, true);
                 }
+#else
+#pragma unroll
+                for (int kk = 0; kk < H; ++kk) {
+                    const bool s_ = kk == qh;
+                    sn = s_ ? (mb ? cb : ca) : sn;
+                    wm = s_ ? (mb ? w[kk + H] : w[kk]) : wm;   // (not re-read from memory: its line has left L2)
+                    const bool r = kk == qah, ra = r && !ab, rb = r && ab;
+                    ca = ra ? 0u : ca;
+                    cb = rb ? 0u : cb;
+                    crc4x2(ca, ra ? (w[kk] & amask) : w[kk], cb, rb ? (w[kk + H] & amask) : w[kk + H], K);
+                }
+#endif
                 sn = qm == UW ? cb : sn;
             }
-            // the unit loop was the tile registers' last reader: the next tile's load is issued
-            // here and its latency runs under the scan and the finalize
-            if (need_next) {
+            // KVR_EARLY: the unit loop was the tile registers' last reader, so the next tile's load
+            // is issued here and its latency runs under the scan and the finalize
+            if (KVR_EARLY && need_next) {
                 load_unit(abase, d0, len, k + 1, lane, w);
                 loaded = true;
             }
+            if (KVR_LATEREC && pend) rec2();
             // the piece of the value crossing the unit end: A pushed through B's bytes, then B
             // (A does not count when that value starts in B's half); the raw CRC of the first
             // 4 qm bytes: A's snapshot, or all of A pushed through 4 (qm - H) bytes, then B's
+            if (KVR_BULK_LOWPRIO) __builtin_amdgcn_s_setprio(2);
             if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(KVR_FIN_PRIO);
             const uint32_t pa = kmul(ca, S.KQ + 128 * H);
             const uint32_t ps = kmul(ca, S.KQ + 128 * (qm > H ? qm - H : 0));
@@ -1252,10 +1365,19 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                 else if (lane == 0 && vx_carry) v = c ^ kmul(c_state, S.KT);   // carried register across unit 0
                 else { v = c; f = 0; }
             }
+            // segmented scan: state at the end of unit l = f ? v : state(l-1) * x^(8*SC) ^ v
+#define KVR_SCAN_ROW(CTRL, D, KTAB)                                          \
+            {                                                                \
+                const uint32_t ov = dpp<CTRL>(v), of = dpp<CTRL>(f);         \
+                const uint32_t t_ = kmul(ov, KTAB);                          \
+                const bool ok = (lane & 15) >= (D) && !f;                    \
+                v = ok ? (v ^ t_) : v;                                       \
+                f = ok ? of : f;                                             \
+            }
+#if KVR_XSCAN
             // every piece pushed straight to where it is consumed (the unit before the one the
             // value ends in, or lane 63 for a value running past the tile): one multiply by
             // x^(8 SC d), then a segmented XOR scan (DPP only) sums each value's pieces there
-            // (state at the end of unit l = f ? v : state(l-1) * x^(8*SC) ^ v)
             if (!(KVR_ABLATE & 16)) {
                 const int32_t ce = vx > TILE ? 63 : ((vx - 1) >> SC_LOG) - 1;   // (vx = 0: v = 0)
                 const int32_t dd = ce - lane;
@@ -1284,6 +1406,28 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                     v = (lane >= 32 && !f) ? (v ^ ov) : v;
                 }
             }
+#else
+            if (!(KVR_ABLATE & 16)) {
+            KVR_SCAN_ROW(0x111, 1, S.KT)
+            KVR_SCAN_ROW(0x112, 2, S.KT + 128)
+            KVR_SCAN_ROW(0x114, 4, S.KT + 256)
+            KVR_SCAN_ROW(0x118, 8, S.KT + 384)
+#undef KVR_SCAN_ROW
+            {   // rows 1 and 3 take the end of rows 0 and 2 (lane 15, 47): distance (l & 15) + 1 units
+                const uint32_t ov = dpp<0x142, 0xA, false>(v), of = dpp<0x142, 0xA, false>(f);
+                const uint32_t t_ = kmulr(ov, S.KR, (uint32_t)(lane & 15));
+                const bool ok = (lane & 16) != 0 && !f;
+                v = ok ? (v ^ t_) : v;
+                f = ok ? of : f;
+            }
+            {   // rows 2 and 3 take the end of row 1 (lane 31): distance (l & 31) + 1 units
+                const uint32_t ov = dpp<0x143, 0xC, false>(v);
+                const uint32_t t_ = kmulr(ov, S.KR, (uint32_t)(lane & 31));
+                const bool ok = lane >= 32 && !f;
+                v = ok ? (v ^ t_) : v;
+            }
+            }
+#endif
             KVR_STAMP(10);
             uint32_t sin = dpp<0x138>(v);        // wave_shr:1: the state at this unit's start
             if (lane == 0) sin = c_state;
@@ -1292,10 +1436,31 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             if (!(KVR_ABLATE & 16) && m != 0) {
                 const int r = m & 3;
                 uint32_t rp = snap, cf = kmul(sin, S.KQ + 128 * qm);
+#if KVR_FINR
+                // the last r < 4 bytes in one round of independent lookups: byte i of x = c ^ data
+                // goes through table r - 1 - i ("a byte then r - 1 - i zero bytes"), the rest of x
+                // is shifted past them
+                auto part = [&](uint32_t c, uint32_t d) -> uint32_t {
+                    const uint32_t x = c ^ (d & ((1u << (8 * r)) - 1u));
+                    uint32_t res = r ? x >> (8 * r) : x, tv[3];
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) {
+                        const int t = r - 1 - i;
+                        tv[i] = *reinterpret_cast<const uint32_t *>(
+                            K.t + ((((x >> (8 * i)) & 255u) << 8) | (32u * (uint32_t)(t < 0 ? 0 : t) + 4u * ((uint32_t)lane & 7u))));
+                    }
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) res ^= (r - 1 - i >= 0) ? tv[i] : 0u;
+                    return res;
+                };
+                rp = part(rp, wm);
+                cf = part(cf, 0u);
+#else
                 for (int b = 0; b < r; ++b) {
                     rp = crc1(rp, (wm >> (8 * b)) & 255u, K);
                     cf = crc1(cf, 0u, K);
                 }
+#endif
                 const uint64_t ms = slot_of(m_ref, m_abs);
                 if (ms < pool_cap) pool[ms].crc32 = ~(cf ^ rp);
             }
@@ -1307,6 +1472,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             }
         }
 
+        if (KVR_LATEREC && pend) rec2();   // (no long value touched the tile)
         if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(0);
         // the tile's registers are dead from here on: the next tile's load overlaps the rest
         if (!loaded && err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry)) {
@@ -1316,6 +1482,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         KVR_STAMP(3);
         // ---- bookkeeping ------------------------------------------------------------------
         if (in_stripe) {
+            if (!(KVR_TRES_EARLY && !KVR_LATEREC) && lane == 0) store_tres();
             total += nrec;
             if (walk) entry = tile_exit;
         }
@@ -1350,7 +1517,6 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         r.forced = redo_mode ? 1u : 0u;
         r.pad = 0;
         sres[si] = r;
-        if (KVR_PREFETCH) __hip_atomic_store(prog, PDONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
