@@ -3,9 +3,10 @@
  * pipeline of one replay call, the device-side generator and host helpers.
  *
  * One kvr_replay call:
- *   [H2D of host segments]  k_replay(all stripes)  k_link  k_replay(re-walk list)  k_link
+ *   [H2D of host segments]  k_replay(all stripes)  k_link  k_rewalk(re-walk list)  k_link
  *   k_tsum  k_tscan  k_compact  [D2H of tuples]  — one stream, one host synchronisation in the
- *   common case; more k_replay/k_link rounds only when a speculated stripe entry was wrong.
+ *   common case; k_rewalk/k_link rounds only when a speculated stripe entry was wrong (a re-walk
+ *   walks on through the wrongly speculated stripes after its own, so one round is the usual case).
  */
 #include <hip/hip_runtime.h>
 
@@ -605,7 +606,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         c->lc_zero = false;
         HIPCHK(hipEventRecord(c->ev[0], st));
         hipLaunchKernelGGL(KR_KERNEL, dim3((n_stripes + KR_WPB - 1) / KR_WPB), dim3(KR_RT), 0, st, c->segs.p, c->stripes.p, n_stripes,
-                           c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, c->redo.p, c->link.p, 0, pool_chunk);
+                           c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, pool_chunk);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[1], st));
         hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
@@ -651,9 +652,9 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             continue;
         }
         while (c->h_link->status == 3 && guard++ < n_stripes + 4) {
-            hipLaunchKernelGGL(KR_KERNEL, dim3((std::max(1u, std::min(c->h_link->n_redo, (uint32_t)c->redo.n)) + KR_WPB - 1) / KR_WPB), dim3(KR_RT),
+            hipLaunchKernelGGL(k_rewalk, dim3((std::max(1u, std::min(c->h_link->n_redo, (uint32_t)c->redo.n)) + KR_WPB - 1) / KR_WPB), dim3(KR_RT),
                                0, st, c->segs.p, c->stripes.p, n_stripes, c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p,
-                               tb, c->redo.p, c->link.p, 1, pool_chunk);
+                               tb, c->redo.p, c->link.p, pool_chunk);
             hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes,
                                c->sres.p, c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p, (uint32_t)KR_TILE,
                                c->soff.p, c->ctr.p);
@@ -735,23 +736,6 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
 // ---------------------------------------------------------------------------------------
 // live-record rewrite (kvr_compact.hip): replay -> fold -> live list -> gather -> cuts
 // ---------------------------------------------------------------------------------------
-// HyperLogLog estimate from the merged registers (alpha_m m^2 / sum 2^-M, the linear-counting
-// correction for small counts, the 2^32 range correction for 32-bit hashes)
-static double hll_estimate(const uint8_t *reg) {
-    double sum = 0;
-    uint32_t zeros = 0;
-    for (int j = 0; j < HLL_M; ++j) {
-        sum += std::ldexp(1.0, -(int)reg[j]);
-        zeros += reg[j] == 0;
-    }
-    const double m = HLL_M, alpha = 0.7213 / (1.0 + 1.079 / m);
-    double e = alpha * m * m / sum;
-    if (e <= 2.5 * m && zeros) e = m * std::log(m / zeros);
-    const double two32 = 4294967296.0;
-    if (e > two32 / 30.0) e = e < two32 ? -two32 * std::log(1.0 - e / two32) : two32;
-    return e;
-}
-
 // replay + the local last-writer fold (k_fold_claim / k_fold_verify): the front half of every
 // compaction and of kvr_replay_live / kvr_replay_index.  It reuses the buffers of a staged
 // sharded compaction, so it ends one (kvr_compact_export / _finish then return KVR_EINVAL until

@@ -57,7 +57,8 @@ struct StripeRes {
     uint32_t err_kind;
     uint32_t count;
     uint32_t forced;      // entry was imposed by k_link (re-walk pass)
-    uint32_t pad;
+    uint32_t owned;       // k_link, before a re-walk pass: bit 0 listed for re-walk, bit 1 inconsistent
+                          // (k_replay's re-walk sets 1 on the stripes it walks)
 };
 
 struct TileRes {          // a tile's tuples in the pool: [pool_off, + count1) then [pool_off2, + count - count1)

@@ -31,27 +31,12 @@ __global__ void k_etag_map(const uint64_t *__restrict__ cpre, uint64_t n, uint32
         for (uint64_t c = cpre[v]; c < cpre[v + 1]; ++c) chunk_blob[c] = (uint32_t)v;
 }
 
-// Slice-by-4 tables laid out for one-instruction addresses: entry e of table t, replica r at byte
-// e * 256 + t * 64 + r * 4 (16 replicas, r = lane & 15: a fixed 2-way bank pattern instead of
-// random conflicts).  The address of byte k of c is one v_perm_b32: byte 1 = c.byte[k], byte 0 =
-// the lane's replica offset `lo`, bytes 2-3 = 0; the table offset t * 64 is the ds_read immediate.
-__device__ inline uint32_t taddr(uint32_t c, uint32_t lo, int k) {
-    return __builtin_amdgcn_perm(c, lo, 0x0c0c0000u | ((4u + (uint32_t)k) << 8));
-}
+// The byte tables are k_replay's (kvr_replay_kernel.hip, Crc): slice-by-4 replicated per LDS bank
+// group with the rotation trick, so no lookup of a wave conflicts, plus a 16-replica single-byte
+// table; crc4 / crc1 are k_replay's steps.
+__device__ inline uint32_t crc_word4(const Crc &K, uint32_t c, uint32_t w) { return crc4(c, w, K); }
 
-__device__ inline uint32_t tget(const uint8_t *L, uint32_t a, int t) {
-    return *reinterpret_cast<const uint32_t *>(L + a + t * 64);
-}
-
-__device__ inline uint32_t crc_word4(const uint8_t *L, uint32_t lo, uint32_t c, uint32_t w) {
-    c ^= w;
-    return tget(L, taddr(c, lo, 0), 3) ^ tget(L, taddr(c, lo, 1), 2) ^ tget(L, taddr(c, lo, 2), 1) ^
-           tget(L, taddr(c, lo, 3), 0);
-}
-
-__device__ inline uint32_t crc_byte(const uint8_t *L, uint32_t lo, uint32_t c, uint32_t b) {
-    return (c >> 8) ^ tget(L, taddr(c ^ b, lo, 0), 0);
-}
+__device__ inline uint32_t crc_byte(const Crc &K, uint32_t c, uint32_t b) { return crc1(c, b, K); }
 
 // a * K_lane by nibble tables: K[i * 16 + n] = (n << 4i) * K_lane  (8 lookups, no bit loop)
 __device__ inline uint32_t kmul_nib(const uint32_t *K, uint32_t a) {
@@ -62,7 +47,7 @@ __device__ inline uint32_t kmul_nib(const uint32_t *K, uint32_t a) {
 }
 
 // One chunk through the general path: any alignment, partial units, bounds-checked loads.
-__device__ inline uint32_t etag_unit_general(const uint8_t *T, uint32_t lo, const uint8_t *data, uint64_t data_len, uint64_t start,
+__device__ inline uint32_t etag_unit_general(const Crc &T, const uint8_t *data, uint64_t data_len, uint64_t start,
                                              uint32_t clen, uint32_t lane, uint32_t reg, const uint32_t *xt) {
     const uint32_t u0 = lane * 64u;
     if (u0 >= clen) return 0u;
@@ -73,18 +58,18 @@ __device__ inline uint32_t etag_unit_general(const uint8_t *T, uint32_t lo, cons
     const uint64_t rel = start + u0;
     uint32_t k = 0;
     if (mis == 0) {
-        for (; k + 4 <= ul; k += 4) reg = crc_word4(T, lo, reg, *reinterpret_cast<const uint32_t *>(p + k));
+        for (; k + 4 <= ul; k += 4) reg = crc_word4(T, reg, *reinterpret_cast<const uint32_t *>(p + k));
     } else if (rel >= mis && rel - mis + ((ul + mis + 3u) & ~3u) <= data_len) {
         // dwords from the aligned-down window while it stays inside the buffer
         const uint32_t *q = reinterpret_cast<const uint32_t *>(p - mis);
         uint32_t w0 = q[0];
         for (uint32_t i = 1; k + 4 <= ul; ++i, k += 4) {
             const uint32_t hi = q[i];
-            reg = crc_word4(T, lo, reg, __builtin_amdgcn_alignbyte(hi, w0, mis));
+            reg = crc_word4(T, reg, __builtin_amdgcn_alignbyte(hi, w0, mis));
             w0 = hi;
         }
     }
-    for (; k < ul; ++k) reg = crc_byte(T, lo, reg, p[k]);
+    for (; k < ul; ++k) reg = crc_byte(T, reg, p[k]);
     return after ? gf_mul(reg, xt[after]) : reg;
 }
 
@@ -98,16 +83,27 @@ __global__ __launch_bounds__(64 * ETAG_WPB) void k_etag_chunk(const uint8_t *__r
                                                              const uint32_t *__restrict__ crc_tab,
                                                              const uint32_t *__restrict__ xt,
                                                              uint32_t *__restrict__ creg) {
-    // slice-by-4 (table t: byte pushed through t zero bytes), taddr layout: 64 KiB
-    __shared__ __align__(16) uint32_t T4[256 * 64];
+    // byte tables in k_replay's Smem::C2 layout (64 KiB, see Crc)
+    __shared__ __align__(16) uint32_t C2[256 * 64];
     __shared__ uint32_t KL[64 * 128];     // per lane: nibble tables of x^(8 (4096 - 64 (lane + 1)))
-    for (uint32_t i = threadIdx.x; i < 256 * 64; i += blockDim.x) T4[i] = crc_tab[((i >> 4) & 3u) * 256 + (i >> 6)];
+    for (uint32_t i = threadIdx.x; i < 256 * 64; i += blockDim.x) {
+        const uint32_t d = i & 63u, t = d < 32u ? d >> 3 : 0u;
+        C2[i] = crc_tab[t * 256 + (i >> 6)];
+    }
     for (uint32_t i = threadIdx.x; i < 64 * 128; i += blockDim.x) KL[i] = xt[ETAG_NX + i];
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t *K = KL + lane * 128;
-    const uint8_t *T = reinterpret_cast<const uint8_t *>(T4);
-    const uint32_t lo = (lane & 15u) << 2;
+    Crc T;
+    {
+        const uint32_t g = (lane >> 3) & 3u, r = lane & 7u, r16 = lane & 15u;
+        T.t = reinterpret_cast<const uint8_t *>(C2);
+        T.L = 128u + 4u * r16;
+        T.L4 = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) T.L4 |= (4u * (8u * ((g + i) & 3u) + r)) << (8 * i);
+        T.rot = (32u - 8u * g) & 31u;
+    }
     const uint64_t waves = (uint64_t)gridDim.x * ETAG_WPB;
     for (uint64_t base = (blockIdx.x * (uint64_t)ETAG_WPB + (threadIdx.x >> 6)) * ETAG_NC; base < n_chunks;
          base += waves * ETAG_NC) {
@@ -142,13 +138,13 @@ __global__ __launch_bounds__(64 * ETAG_WPB) void k_etag_chunk(const uint8_t *__r
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
 #pragma unroll
-                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, lo, reg[k], w[k][i].x);
+                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].x);
 #pragma unroll
-                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, lo, reg[k], w[k][i].y);
+                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].y);
 #pragma unroll
-                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, lo, reg[k], w[k][i].z);
+                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].z);
 #pragma unroll
-                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, lo, reg[k], w[k][i].w);
+                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].w);
             }
             if (lane != 63) {
 #pragma unroll
@@ -157,7 +153,7 @@ __global__ __launch_bounds__(64 * ETAG_WPB) void k_etag_chunk(const uint8_t *__r
         } else {
 #pragma unroll 1
             for (int k = 0; k < ETAG_NC; ++k)
-                if (clen[k]) reg[k] = etag_unit_general(T, lo, data, data_len, start[k], clen[k], lane, reg[k], xt);
+                if (clen[k]) reg[k] = etag_unit_general(T, data, data_len, start[k], clen[k], lane, reg[k], xt);
         }
 #pragma unroll
         for (int k = 0; k < ETAG_NC; ++k) {

@@ -32,7 +32,7 @@ __device__ __forceinline__ uint64_t stripe_lo(const StripeDesc &d, const SegDesc
 
 __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, uint32_t n_segs,
                                              const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
-                                             const StripeRes *__restrict__ sres, RedoEnt *__restrict__ redo,
+                                             StripeRes *__restrict__ sres, RedoEnt *__restrict__ redo,
                                              uint32_t redo_cap, LinkResult *res, uint32_t *seg_bad,
                                              uint32_t *seg_err, uint32_t tile, uint64_t *__restrict__ soff,
                                              Counters *ctr) {
@@ -172,30 +172,47 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
     __syncthreads();
     const uint32_t fu = first_problem;
     const bool unresolved = fu != ~0u;
-    // pass 2: re-walk list (stripes whose entry disagrees with the true chain so far), in every
-    // segment before the first resolved error
+    // pass 2: re-walk list, in every segment before the first resolved error.  A stripe whose
+    // entry disagrees with the chain so far is inconsistent (owned bit 1, every stripe's bits are
+    // rewritten here); it is listed (bit 0) only when its predecessor is consistent, so its entry
+    // is the predecessor's exit.  Its re-walk walks on into the inconsistent stripes after it
+    // (k_replay, redo pass), so a run of wrong speculations is one pass, not one per stripe.
     if (unresolved) {
-        run = run0;
-        for (uint32_t s = b; s < e; ++s) {
-            const StripeRes r = sres[s];
-            const StripeDesc d = stripes[s];
-            const SegDesc g = segs[d.seg];
-            if (d.seg < fe && s != g.stripe0) {
-                const uint64_t xp = run >= 0 ? sres[run].exit : NONE;
-                bool bad = false;
-                if (xp != ERRP) {
-                    if (r.entry == NONE) bad = xp < stripe_hi(d, g, tile);
-                    else bad = (r.entry != xp);
+        // (two sweeps: the first flags the inconsistent stripes, the second lists the first of each
+        // run; the flags of a neighbouring chunk are read only after the barrier)
+        for (int sweep = 0; sweep < 2; ++sweep) {
+            run = run0;
+            for (uint32_t s = b; s < e; ++s) {
+                const StripeRes r = sres[s];
+                const StripeDesc d = stripes[s];
+                const SegDesc g = segs[d.seg];
+                uint32_t own = 0;
+                if (d.seg < fe && s != g.stripe0) {
+                    const uint64_t xp = run >= 0 ? sres[run].exit : NONE;
+                    bool bad = false;
+                    if (xp != ERRP) {
+                        if (r.entry == NONE) bad = xp < stripe_hi(d, g, tile);
+                        else bad = (r.entry != xp);
+                    }
+                    own = bad ? 2u : 0u;
+                    if (sweep == 1 && bad) {
+                        const uint32_t se = __hip_atomic_load(&seg_err[d.seg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const bool prev_bad =
+                            (__hip_atomic_load(&sres[s - 1].owned, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2u) != 0u;
+                        // a predecessor exit short of this stripe lands in a pass-through stripe in
+                        // between, which is inconsistent too and listed or walked first
+                        if (!prev_bad && s < se && xp >= stripe_lo(d, g, tile)) {
+                            own = 3u;
+                            const uint32_t i = atomicAdd(&nredo, 1u);
+                            if (i < redo_cap) { redo[i].stripe = s; redo[i].pad = 0; redo[i].entry = xp; }
+                        }
+                    }
                 }
-                const uint32_t se = __hip_atomic_load(&seg_err[d.seg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                // a predecessor exit short of this stripe lands in a pass-through stripe in
-                // between, which is re-walked first; this one waits for the next round
-                if (bad && s < se && xp >= stripe_lo(d, g, tile)) {
-                    const uint32_t i = atomicAdd(&nredo, 1u);
-                    if (i < redo_cap) { redo[i].stripe = s; redo[i].pad = 0; redo[i].entry = xp; }
-                }
+                // (sweep 1 changes bit 0 only: a neighbour reading bit 1 sees the same either way)
+                __hip_atomic_store(&sres[s].owned, own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (r.entry != NONE) run = (int32_t)s;
             }
-            if (r.entry != NONE) run = (int32_t)s;
+            __syncthreads();
         }
     }
     __syncthreads();

@@ -46,15 +46,8 @@ namespace kvr {
 #define KVR_RT 1024
 #endif
 constexpr int RT = KVR_RT;
-#ifndef KVR_PREFETCH   // 1: one wave per workgroup prefetches the workers' next tiles into the caches
-#define KVR_PREFETCH 0
-#endif
-#ifndef KVR_PF_DIST    // tiles ahead of its worker the prefetch wave runs
-#define KVR_PF_DIST 1
-#endif
 constexpr int NWAVE = RT / 64;            // waves per workgroup
-constexpr int WPB = NWAVE - (KVR_PREFETCH ? 1 : 0);   // stripes (worker waves) per workgroup
-constexpr uint32_t PDONE = 0xFFFFFFFFu;   // a worker's progress word once its stripe is done
+constexpr int WPB = NWAVE;                // stripes per workgroup (one per wave)
 constexpr int UW = SC / 4;                // dwords of a lane's unit
 constexpr int SC_LOG = 7;
 static_assert(SC == 1 << SC_LOG, "unit size");
@@ -73,12 +66,10 @@ constexpr int WINW = KEYW + 3;            // decode window: dwords from the cand
 // below 64 KiB, which the ds_read instruction carries as its immediate offset.
 struct __align__(16) Smem {
     uint32_t KR[8 * 16 * 64];             // [i][n][k]: (n << 4i) * x^(8*SC*(k+1)), k < 64
-    uint32_t KT[4 * 8 * 16];              // [j][i][n]: (n << 4i) * x^(8*SC*2^j), j < 4
-    uint32_t KQ[NQ * 8 * 16];             // [q][i][n]: (n << 4i) * x^(8*4q), q <= SC/4
+    uint32_t KQL[8 * 16 * 64];            // [i][n][q]: (n << 4i) * x^(8*4q), q <= SC/4 (columns > SC/4: 0)
+    uint32_t KQ[NQ * 8 * 16];             // [q][i][n]: the same, rows by constant (a lane-uniform q)
     uint32_t IX[NIX + 3];                 // 0xFFFFFFFF * x^(8j): initial register pushed through j bytes
     uint32_t MK[NWAVE][64];               // per wave: long-value marks by unit (framing)
-    uint32_t PROG[NWAVE];                 // per worker: the tile it is on (PDONE: finished)
-    uint32_t PSINK[64];                   // the prefetch wave's loads land here (never read)
     uint32_t C2[256 * 64];                // byte tables, row b = 256 B (64 KiB), see Crc
 };
 
@@ -192,6 +183,9 @@ __device__ __forceinline__ uint32_t crc4(uint32_t c, uint32_t w, const Crc &k) {
     asm("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
     return xor3(a0, a1, a2) ^ a3;
 }
+__device__ __forceinline__ uint32_t bitop3_xandn(uint32_t a, uint32_t b, uint32_t c) {   // one v_bitop3
+    return a ^ (b & ~c);
+}
 // two independent chains stepped together from their inputs x = register ^ data
 __device__ __forceinline__ void crc4x2(uint32_t &ca, uint32_t xa, uint32_t &cb, uint32_t xb, const Crc &k) {
     const uint32_t ra = __builtin_amdgcn_alignbit(xa, xa, k.rot), rb = __builtin_amdgcn_alignbit(xb, xb, k.rot);
@@ -207,7 +201,8 @@ __device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
 }
 
 // register state v times a constant K (nibble tables; every lane reads table i at once, so the
-// 16 entries sit in 16 banks and equal indices broadcast: conflict free).  The eight lookups
+// 16 entries sit in 16 banks and equal indices broadcast: conflict free).  For a per-lane constant,
+// kmul_col below.  The eight lookups
 // are independent: the empty asm makes the scheduler issue them all before the first use.
 __device__ __forceinline__ uint32_t xor8(uint32_t *t) {
     asm("" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]), "+v"(t[7]));
@@ -222,13 +217,18 @@ __device__ __forceinline__ uint32_t kmul(uint32_t v, const uint32_t *K) {
     for (int i = 0; i < 8; ++i) t[i] = K[i * 16 + ((pl[i & 1] >> (8 * (i >> 1))) & 255u)];
     return xor8(t);
 }
-// v times x^(8*SC*(k+1)), k per lane (column k of KR: bank k mod 32)
-__device__ __forceinline__ uint32_t kmulr(uint32_t v, const uint32_t *KR, uint32_t k) {
+// v times the constant in column k (per lane) of a [i][n][k] table of 64 columns (KR, KQL): entry
+// (i, n, k) sits at byte i 4096 + n 256 + 4 k, so its address is one v_perm_b32 (byte 1 = the
+// nibble n from a plane, byte 0 = 4 k from L4k) and the ds_read immediate i 4096
+__device__ __forceinline__ uint32_t kmul_col(uint32_t v, const uint32_t *T, uint32_t L4k) {
     uint32_t pl[2] = {v & 0x0F0F0F0Fu, (v >> 4) & 0x0F0F0F0Fu};
     asm("" : "+v"(pl[0]), "+v"(pl[1]));   // keep the planes (no re-fusion into nibble shifts)
+    const uint8_t *tb = reinterpret_cast<const uint8_t *>(T);
     uint32_t t[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) t[i] = KR[(i * 16 + ((pl[i & 1] >> (8 * (i >> 1))) & 255u)) * 64 + k];
+    for (int i = 0; i < 8; ++i)
+        t[i] = *reinterpret_cast<const uint32_t *>(
+            tb + i * 4096 + __builtin_amdgcn_perm(pl[i & 1], L4k, 0x0C0C0000u | ((4u + (uint32_t)(i >> 1)) << 8)));
     return xor8(t);
 }
 
@@ -567,82 +567,18 @@ __device__ __forceinline__ TileSeg tile_seg(const uint8_t *abase, const uint8_t 
 }
 
 // ---------------------------------------------------------------------------------------
-// the prefetch wave: the worker waves of a workgroup each hold one tile in registers and load the
-// next only when the current one's CRC is done, so at 15-16 waves per CU too few bytes are in
-// flight to keep HBM busy (the workers' loads alone reach about 4.4 TB/s).  This wave walks a
-// tile ahead of every worker of its workgroup and touches the tile's 64-B sectors (one dword
-// load per sector, all of a round in flight together), so a worker's own load finds its lines in
-// L2 or the Infinity Cache.  It only reads; results never depend on it.
-// ---------------------------------------------------------------------------------------
-__device__ inline void prefetch_wave(Smem &S, const SegDesc *__restrict__ segs, const StripeDesc *__restrict__ stripes,
-                                     uint32_t n_stripes, const RedoEnt *__restrict__ redo,
-                                     const LinkResult *__restrict__ link, int redo_mode, int lane) {
-    // lane w < WPB follows worker w: the stripe it walks, as the worker computes it
-    uint32_t t_next = 0, t_end = 0, t_begin = 0;
-    uint64_t abase = 0, span = 0;
-    if (lane < WPB) {
-        const uint32_t gw = blockIdx.x * WPB + (uint32_t)lane;
-        bool have;
-        uint32_t si = gw;
-        if (redo_mode) {
-            have = gw < link->n_redo && link->status == 3;
-            if (have) si = redo[gw].stripe;
-        } else {
-            have = gw < n_stripes;
-        }
-        if (have) {
-            const StripeDesc sd = stripes[si];
-            const SegDesc sg = segs[sd.seg];
-            t_begin = sd.t_begin;
-            t_next = sd.t_begin + 1u;
-            t_end = sd.t_end < sg.n_tiles ? sd.t_end : sg.n_tiles;
-            abase = (uint64_t)(sg.base - sg.d0);
-            span = ((uint64_t)sg.d0 + sg.len + 15u) & ~15ull;   // bytes from abase the segment covers
-        }
-    }
-    uint32_t sink = 0;
-#pragma unroll 1
-    for (uint32_t guard = 0; guard < (1u << 24); ++guard) {
-        const uint32_t pr = lane < WPB ? __hip_atomic_load(&S.PROG[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                                       : PDONE;
-        if (__ballot(pr != PDONE) == 0ull) break;
-        const uint32_t at = pr > t_begin ? pr : t_begin;
-        const bool want = pr != PDONE && t_next < t_end && t_next <= at + (uint32_t)KVR_PF_DIST;
-        const uint64_t m = __ballot(want);
-        if (m == 0ull) { __builtin_amdgcn_s_sleep(2); continue; }
-        // one round: every wanted worker's next tile touched (two dwords per 128-B unit, one per
-        // 64-B sector), all loads in flight together, one wait at the end of the round
-        uint32_t t[WPB][2];
-#pragma unroll
-        for (int w = 0; w < WPB; ++w) {
-            t[w][0] = t[w][1] = 0u;
-            if ((m >> w) & 1ull) {
-                const uint64_t t0 = (uint64_t)rl32(t_next, w) * TILE;
-                const uint64_t b = rl64(abase, w) + t0, sp = rl64(span, w);
-                const int64_t nr = sp > t0 ? ((sp - t0) > (uint64_t)TILE ? TILE : (int64_t)(sp - t0)) : 0;
-                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                    (void *)b, (short)0, __builtin_amdgcn_readfirstlane((int)nr), 0x00020000);
-                t[w][0] = __builtin_amdgcn_raw_buffer_load_b32(rs, lane * SC, 0, 0);
-                t[w][1] = __builtin_amdgcn_raw_buffer_load_b32(rs, lane * SC + 64, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int w = 0; w < WPB; ++w) sink ^= t[w][0] ^ t[w][1];
-        t_next += want ? 1u : 0u;
-    }
-    S.PSINK[lane] = sink;   // (the touches' values are never used; this keeps them)
-}
-
-// ---------------------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
-                                               const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
-                                               StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
-                                               kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
-                                               Tables tb, const RedoEnt *__restrict__ redo,
-                                               const LinkResult *__restrict__ link, int redo_mode,
-                                               uint32_t pool_chunk) {
+// REDO: the re-walk pass (k_rewalk) over k_link's list, with the walk-on into later stripes; the
+// first pass (k_replay) walks every stripe once
+template <bool REDO>
+__device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
+                                            const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
+                                            StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
+                                            kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
+                                            Tables tb, const RedoEnt *__restrict__ redo,
+                                            const LinkResult *__restrict__ link, uint32_t pool_chunk) {
+    constexpr bool redo_mode = REDO;
     __shared__ Smem S;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (int i = tid; i < 256 * 64; i += RT) {
@@ -651,17 +587,13 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     }
     for (int i = tid; i < 8 * 16 * 64; i += RT)
         S.KR[i] = tb.kmul[((KSET_R + (i & 63)) * 8 + (i >> 10)) * 16 + ((i >> 6) & 15)];
-    for (int i = tid; i < 4 * 8 * 16; i += RT) S.KT[i] = tb.kmul[i];
+    for (int i = tid; i < 8 * 16 * 64; i += RT) {
+        const int q = i & 63;
+        S.KQL[i] = q < NQ ? tb.kmul[((KSET_Q + q) * 8 + (i >> 10)) * 16 + ((i >> 6) & 15)] : 0u;
+    }
     for (int i = tid; i < NQ * 8 * 16; i += RT) S.KQ[i] = tb.kmul[KSET_Q * 8 * 16 + i];
     if (tid < NIX) S.IX[tid] = tb.initx[tid];
-    if (tid < NWAVE) S.PROG[tid] = 0u;
     __syncthreads();   // the only workgroup barrier: from here on every wave is on its own
-    // (the wave index made wave-uniform first: a divergent return would leave this wave running
-    // the worker code below with EXEC = 0, and its scalar loads are not masked)
-    if (KVR_PREFETCH && __builtin_amdgcn_readfirstlane(wv) == WPB) {
-        prefetch_wave(S, segs, stripes, n_stripes, redo, link, redo_mode, lane);
-        return;
-    }
     uint32_t *const MK = S.MK[wv];   // this wave's long-value marks
 
     Crc K;
@@ -678,15 +610,20 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     const uint32_t gw = blockIdx.x * WPB + (uint32_t)__builtin_amdgcn_readfirstlane(wv);
     uint32_t si;
     uint64_t forced = NONE;
-    uint32_t *const prog = &S.PROG[wv];   // this worker's progress (read by the prefetch wave)
     if (redo_mode) {
-        if (gw >= link->n_redo || link->status != 3) { if (lane == 0) __hip_atomic_store(prog, PDONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); return; }
+        if (gw >= link->n_redo || link->status != 3) return;
         si = redo[gw].stripe;
         forced = redo[gw].entry;
     } else {
-        if (gw >= n_stripes) { if (lane == 0) __hip_atomic_store(prog, PDONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); return; }
+        if (gw >= n_stripes) return;
         si = gw;
     }
+    uint64_t chunk_base = 0, chunk_left = 0;      // this wave's pool chunk
+    // A re-walk (redo pass) walks on into the stripes after its own while their speculated entry
+    // disagrees with the chain it carries, so a run of wrong speculations (a value holding a whole
+    // segment image, say) costs one pass rather than one pass per stripe (see the end of the loop)
+#pragma unroll 1
+    for (;;) {
     const StripeDesc sd = stripes[si];
     const SegDesc sg = segs[sd.seg];
     const uint64_t len = sg.len;
@@ -700,14 +637,14 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
     bool search = entry == NONE;
     uint64_t stripe_entry = (entry != NONE && entry >= s_hi) ? NONE : entry;
     int stop = (entry != NONE && entry >= s_hi) ? 2 : 0;   // imposed entry beyond the stripe: nothing starts here
-    if (entry != NONE && (int64_t)entry < (int64_t)sd.t_begin * TILE - d0) {   // bug trap: k_link never does this
+    const bool trapped = entry != NONE && (int64_t)entry < (int64_t)sd.t_begin * TILE - d0;
+    if (trapped) {   // bug trap: k_link never does this
         stop = 2;
         stripe_entry = NONE;
         if (lane == 0) atomicOr(&ctr->overflow, 4u);
     }
     uint64_t err_pos = NONE, err_aux = 0;
     uint32_t err_kind = 0, total = 0;
-    uint64_t chunk_base = 0, chunk_left = 0;
     uint32_t stride = 0, fast_skip = 0;           // lane-parallel framing: the last record length, tiles left to skip
     uint32_t carry = 0, c_state = 0;              // 1: a long value crosses the tile start (c_state: its register);
     uint64_t c_vb = 0, c_ve = 0, c_slot = 0;      // 2: pending (its value starts in a later tile)
@@ -724,7 +661,6 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         KVR_STAMP(5);
         const bool in_stripe = k < sd.t_end;
         if (stop || (!in_stripe && !carry) || k >= sg.n_tiles) break;
-        if (KVR_PREFETCH && lane == 0) __hip_atomic_store(prog, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (!loaded) {
             load_unit(abase, d0, len, k, lane, w);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1242,15 +1178,13 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             // 4 qm bytes: A's snapshot, or all of A pushed through 4 (qm - H) bytes, then B's
             if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(KVR_FIN_PRIO);
             const uint32_t pa = kmul(ca, S.KQ + 128 * H);
-            const uint32_t ps = kmul(ca, S.KQ + 128 * (qm > H ? qm - H : 0));
             const uint32_t c = qa >= H ? cb : (pa ^ cb);
-            const uint32_t snap = qm < H ? sn : (ps ^ sn);
             KVR_STAMP(9);
-            uint32_t v = 0, f = 1;               // segment start f: no inflow from the previous unit
+            uint32_t v = 0, fm = N32;            // segment start fm (all ones): no inflow from the previous unit
             if (vx) {
                 if (a_off >= 0) v = c ^ S.IX[SC - a_off];
-                else if (lane == 0 && vx_carry) v = c ^ kmul(c_state, S.KT);   // carried register across unit 0
-                else { v = c; f = 0; }
+                else if (lane == 0 && vx_carry) v = c ^ kmul(c_state, S.KQ + 128 * (NQ - 1));   // carried register across unit 0
+                else { v = c; fm = 0u; }
             }
             // every piece pushed straight to where it is consumed (the unit before the one the
             // value ends in, or lane 63 for a value running past the tile): one multiply by
@@ -1259,45 +1193,39 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
             if (!(KVR_ABLATE & 16)) {
                 const int32_t ce = vx > TILE ? 63 : ((vx - 1) >> SC_LOG) - 1;   // (vx = 0: v = 0)
                 const int32_t dd = ce - lane;
-                const uint32_t t_ = kmulr(v, S.KR, dd > 0 ? (uint32_t)(dd - 1) : 0u);
+                const uint32_t t_ = kmul_col(v, S.KR, dd > 0 ? 4u * (uint32_t)(dd - 1) : 0u);
                 v = dd > 0 ? t_ : v;
-#define KVR_XSCAN_ROW(CTRL, D)                                               \
+                // (a lane without a source reads 0 from the DPP move -- row_shr past the row start,
+                // the rows a broadcast skips -- which adds nothing and starts no segment, so no lane
+                // test is needed: v ^= inflow unless a segment starts here, fm |= the inflow's fm)
+#define KVR_XSCAN_STEP(CTRL, RM, BC)                                         \
             {                                                                \
-                const uint32_t ov = dpp<CTRL>(v), of = dpp<CTRL>(f);         \
-                const bool ok = (lane & 15) >= (D) && !f;                    \
-                v = ok ? (v ^ ov) : v;                                       \
-                f = ok ? of : f;                                             \
+                const uint32_t ov = dpp<CTRL, RM, BC>(v);                    \
+                v = bitop3_xandn(v, ov, fm);                                 \
+                fm |= dpp<CTRL, RM, BC>(fm);                                 \
             }
-                KVR_XSCAN_ROW(0x111, 1)
-                KVR_XSCAN_ROW(0x112, 2)
-                KVR_XSCAN_ROW(0x114, 4)
-                KVR_XSCAN_ROW(0x118, 8)
-#undef KVR_XSCAN_ROW
-                {
-                    const uint32_t ov = dpp<0x142, 0xA, false>(v), of = dpp<0x142, 0xA, false>(f);
-                    const bool ok = (lane & 16) != 0 && !f;
-                    v = ok ? (v ^ ov) : v;
-                    f = ok ? of : f;
-                }
-                {
-                    const uint32_t ov = dpp<0x143, 0xC, false>(v);
-                    v = (lane >= 32 && !f) ? (v ^ ov) : v;
-                }
+                KVR_XSCAN_STEP(0x111, 0xF, true)
+                KVR_XSCAN_STEP(0x112, 0xF, true)
+                KVR_XSCAN_STEP(0x114, 0xF, true)
+                KVR_XSCAN_STEP(0x118, 0xF, true)
+                KVR_XSCAN_STEP(0x142, 0xA, false)
+#undef KVR_XSCAN_STEP
+                v = bitop3_xandn(v, dpp<0x143, 0xC, false>(v), fm);
             }
             KVR_STAMP(10);
             uint32_t sin = dpp<0x138>(v);        // wave_shr:1: the state at this unit's start
             if (lane == 0) sin = c_state;
-            // the value ending in this unit at m: its register is sin * x^(8m) ^ raw[0, m)
-            // (the x^(8m) push: a constant table for 4q bytes + r zero bytes)
+            // the value ending in this unit at m: its register is sin * x^(8m) ^ raw[0, m), and
+            // raw[0, 4 qm) is A's snapshot, or all of A pushed through 4 (qm - H) bytes ^ B's: so
+            // (base * x^(8*4q) ^ sn) with base = sin, q = qm, or base = sin * x^(8*4H) ^ A, q = qm - H
+            // (one per-lane multiply); then the r = m & 3 bytes past 4 qm, by linearity one chain
             if (!(KVR_ABLATE & 16) && m != 0) {
                 const int r = m & 3;
-                uint32_t rp = snap, cf = kmul(sin, S.KQ + 128 * qm);
-                for (int b = 0; b < r; ++b) {
-                    rp = crc1(rp, (wm >> (8 * b)) & 255u, K);
-                    cf = crc1(cf, 0u, K);
-                }
+                const uint32_t base = mb ? (kmul(sin, S.KQ + 128 * H) ^ ca) : sin;
+                uint32_t t = kmul_col(base, S.KQL, 4u * (uint32_t)(mb ? qm - H : qm)) ^ sn;
+                for (int b = 0; b < r; ++b) t = crc1(t, (wm >> (8 * b)) & 255u, K);
                 const uint64_t ms = slot_of(m_ref, m_abs);
-                if (ms < pool_cap) pool[ms].crc32 = ~(cf ^ rp);
+                if (ms < pool_cap) pool[ms].crc32 = ~t;
             }
             if (out) {                           // the value running past the tile: hand over its register
                 n_carry = 1;
@@ -1327,7 +1255,7 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         }
         KVR_STAMP(4);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain an unused prefetch before exit
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain an unused next-tile load
 #ifdef KVR_PROF
     if (lane == 0)
         for (int i = 0; i < 16; ++i) atomicAdd(&g_prof[i], prof_acc[i]);
@@ -1348,10 +1276,43 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
         r.err_kind = (err_pos != NONE) ? err_kind : 0u;
         r.count = total;
         r.forced = redo_mode ? 1u : 0u;
-        r.pad = 0;
+        r.owned = redo_mode ? 1u : 0u;
         sres[si] = r;
-        if (KVR_PREFETCH) __hip_atomic_store(prog, PDONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    // ---- redo pass: walk on into the next stripe of the segment --------------------------------
+    // while its speculated result (last pass) disagrees with the chain position this walk reached,
+    // `entry` (the walked exit, or the imposed entry a pass-through stripe keeps), as k_link would
+    // find; a stripe listed for its own re-walk in this pass (owned bit 0) is left to its wave
+    if (!REDO || err_pos != NONE || trapped) break;
+    const uint32_t nx = si + 1;
+    if (nx >= n_stripes || entry == NONE) break;
+    const StripeDesc nd = stripes[nx];
+    if (nd.seg != sd.seg) break;
+    const StripeRes nr = sres[nx];        // (no other wave writes it in this pass)
+    if (nr.owned & 1u) break;
+    const int64_t nhi_i = (int64_t)nd.t_end * TILE - d0;
+    const uint64_t n_hi = (uint64_t)nhi_i > len ? len : (uint64_t)nhi_i;
+    if (nr.entry == NONE ? entry >= n_hi : nr.entry == entry) break;   // consistent: the chain joins
+    si = nx;
+    forced = entry;
+    }
+}
+
+__global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
+                                               const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
+                                               StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
+                                               kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
+                                               Tables tb, uint32_t pool_chunk) {
+    replay_body<false>(segs, stripes, n_stripes, sres, tres, pool, pool_cap, ctr, tb, nullptr, nullptr, pool_chunk);
+}
+
+__global__ __launch_bounds__(RT) void k_rewalk(const SegDesc *__restrict__ segs,
+                                               const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
+                                               StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
+                                               kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
+                                               Tables tb, const RedoEnt *__restrict__ redo,
+                                               const LinkResult *__restrict__ link, uint32_t pool_chunk) {
+    replay_body<true>(segs, stripes, n_stripes, sres, tres, pool, pool_cap, ctr, tb, redo, link, pool_chunk);
 }
 
 }  // namespace kvr

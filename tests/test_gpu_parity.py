@@ -162,6 +162,58 @@ def test_adversarial_speculation(gctx):
     check_parity(gctx, [seg, seg[: len(seg) // 2 + 13], inner, zeros])
 
 
+def _blob_store(image_values, seed):
+    """A segment whose big values are whole segment images (valid record chains), each spanning
+    hundreds of single-tile stripes, between runs of ordinary records."""
+    rng = random.Random(seed)
+    parts = []
+    for i, v in enumerate(image_values):
+        for j in range(200):
+            parts.append(rec_set(b"k%d.%d" % (i, j), bytes(rng.getrandbits(8) for _ in range(rng.randint(0, 300)))))
+        parts.append(rec_set(b"blob%d" % i, v))
+    parts.append(rec_del(b"k0.0"))
+    return b"".join(parts)
+
+
+def test_adversarial_walk_through(gctx):
+    """Every stripe inside a value that holds a segment image speculates an entry on the image's
+    records, and those stripes agree with each other.  k_link lists only the first stripe of such
+    a run and its re-walk walks on through the rest (engine.rs:85-151 chain), so the store
+    replays in one re-walk round instead of one per stripe; timed against a store of the same
+    shape whose big values are random bytes (no wrong speculation)."""
+    import time
+    rng = random.Random(17)
+    image = b"".join(rec_set(b"in%d" % i, bytes(rng.getrandbits(8) for _ in range(rng.randint(0, 90))))
+                     for i in range(30000))                    # ~1.8 MiB of valid records
+    images = [image, image[: len(image) // 2]]
+    noise = [bytes(rng.getrandbits(8) for _ in range(len(v))) for v in images]
+    adv, clean = _blob_store(images, 3), _blob_store(noise, 3)
+    assert len(adv) == len(clean)
+    gctx.set_tiles_per_stripe(1)                               # ~350 stripes inside the big values
+    try:
+        rg = check_parity(gctx, [adv, adv[: len(adv) - 7]])
+        check_parity(gctx, [adv])
+        st = gctx.last_stats()
+        n_redo_adv = st.n_redo
+        check_parity(gctx, [clean])
+        n_redo_clean = gctx.last_stats().n_redo
+
+        def best(seg):
+            t = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                r = gctx.replay([seg])
+                t.append(time.perf_counter() - t0)
+                assert r.status == 0
+            return min(t)
+        ta, tc = best(adv), best(clean)
+    finally:
+        gctx.set_tiles_per_stripe(0)
+    print(f"adversarial: n_redo {n_redo_adv} {ta * 1e3:.2f} ms; clean: n_redo {n_redo_clean} {tc * 1e3:.2f} ms")
+    assert n_redo_adv <= 2, n_redo_adv
+    assert ta <= 2.0 * tc + 2e-3, (ta, tc)
+
+
 def test_random_truncations_and_corruptions(gctx):
     spec = K.GenSpec(seed=81, seg_bytes=400_000, val_min=1, val_max=3000, del_permille=200)
     base, _ = K.gen_segment_cpu(spec, 0)

@@ -56,6 +56,12 @@ for s in $STEPS; do
     phases)
       timeout -k 10 240 python -u tools/prof_phases.py cfg2 > "$OUT/phases_cfg2.txt" 2>&1 || { echo "phases failed"; tail -20 "$OUT/phases_cfg2.txt"; exit 1; }
       cat "$OUT/phases_cfg2.txt" ;;
+    phases4)  # the cfg4 shape (50 % DEL: two record lengths, the framing's hard case)
+      timeout -k 10 240 python -u tools/prof_phases.py cfg4 > "$OUT/phases_cfg4.txt" 2>&1 || { echo "phases4 failed"; tail -20 "$OUT/phases_cfg4.txt"; exit 1; }
+      cat "$OUT/phases_cfg4.txt" ;;
+    bench4)
+      timeout -k 10 300 python -u bench.py --config cfg4 --no-cpu --no-open --no-stream > "$OUT/bench_cfg4.json" 2> "$OUT/bench_cfg4.err" || { echo "bench cfg4 failed"; tail -20 "$OUT/bench_cfg4.err"; exit 1; }
+      cat "$OUT/bench_cfg4.json" ;;
     ablate)
       for m in ${MASKS:-0 1 2 3 7}; do
         timeout -k 10 120 python -u tools/ablate.py cfg2 0 $m >> "$OUT/ablate_cfg2.txt" 2>&1 || { echo "ablate failed"; tail -20 "$OUT/ablate_cfg2.txt"; exit 1; }
@@ -78,6 +84,9 @@ for s in $STEPS; do
     pmc)
       timeout -k 10 900 bash tools/pmc.sh "$OUT/pmc" --no-cpu --no-stream --steps 2 --warmup 1 > "$OUT/pmc.txt" 2>&1 || { echo "pmc failed"; tail -20 "$OUT/pmc.txt"; exit 1; }
       cat "$OUT/pmc.txt" ;;
+    ldpat)    # tools/ldpat.hip: the load-structure ceiling of the tile loop (built here beforehand)
+      timeout -k 10 180 ./tools/ldpat > "$OUT/ldpat.txt" 2>&1 || { echo "ldpat failed"; tail -20 "$OUT/ldpat.txt"; exit 1; }
+      cat "$OUT/ldpat.txt" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

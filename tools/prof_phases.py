@@ -56,8 +56,9 @@ for it in range(3):
     st = K.Stats()
     lib.kvr_last_stats(ctx, C.byref(st))
     lib.kvr_prof_read(prof, 0)
-names = ["setup(store+pref)", "framing", "err+hand+halo", "crc-finalize", "bookkeep", "wait(vmcnt)", "records", "err-reduce",
-         "cover-scan", "unit-crc", "scan", "search-filter", "search-plausible", "search-reduce", "search tiles x1000", "-"]
+# KVR_STAMP slots of kvr_replay_kernel.hip (unused slots print 0)
+names = ["setup(load)", "-", "framing+records", "finalize", "bookkeep", "wait(vmcnt)", "-", "-",
+         "crc-entry", "unit-loop+kmul", "scan", "-", "-", "-", "-", "-"]
 tiles = st.n_tiles
 tot_c = sum(prof[i] for i in range(16))
 print(f"{cfg}: rc={rc} n={n.value}/{nrec} bytes={tot} tiles={tiles} stripes={st.n_stripes} ms_replay={st.ms_replay:.3f}"
