@@ -101,6 +101,7 @@ VARIANTS = {
     "pf1": ["-DKVR_PREFETCH=1"],   # a prefetch wave per workgroup (cfg2 1.540 vs 1.396 ms: not kept)
     "lf0": ["-DKVR_LANEFRAME=0"],  # the scalar hop loop for every record
     "a7": ["-DKVR_ABLATE=7"],      # loads + per-tile bookkeeping only (the memory floor at 16 waves/CU)
+    "tree": ["-DKVR_TREE=1"],      # tree rounds for two recent record lengths
     "base": [],
 }
 

@@ -88,6 +88,9 @@ struct __align__(16) Smem {
 #ifndef KVR_LANEFRAME   // 1: lane-parallel framing (0: the exact scalar hop loop for every record)
 #define KVR_LANEFRAME 1
 #endif
+#ifndef KVR_TREE   // 1: the lane-parallel framing also predicts with two recent lengths (tree rounds;
+#define KVR_TREE 0     // measured slower: cfg4 2.259 vs 1.964 ms, a tree round's VALU outweighs the hops)
+#endif
 #ifndef KVR_FAST_BACKOFF   // tiles the scalar hop loop keeps after a lane-parallel round found < 3 records
 #define KVR_FAST_BACKOFF 4
 #endif
@@ -118,6 +121,8 @@ __device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 // old with lane l set to the uniform val (v_writelane_b32: one VALU instruction, no compare/select)
 __device__ __forceinline__ uint32_t wl32(uint32_t old, uint32_t val, uint32_t l) {
+    val = __builtin_amdgcn_readfirstlane(val);
+    asm("" : "+s"(val));   // (an SGPR even when val is a known constant: v_writelane takes no literal)
     asm("v_writelane_b32 %0, %1, %2" : "+v"(old) : "s"(val), "{m0}"(l));   // lane select through m0
     return old;
 }
@@ -645,7 +650,8 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
     }
     uint64_t err_pos = NONE, err_aux = 0;
     uint32_t err_kind = 0, total = 0;
-    uint32_t stride = 0, fast_skip = 0;           // lane-parallel framing: the last record length, tiles left to skip
+    uint32_t stride = 0, stride2 = 0, fast_skip = 0;   // lane-parallel framing: the two recent record lengths,
+                                                       // tiles left to skip
     uint32_t carry = 0, c_state = 0;              // 1: a long value crosses the tile start (c_state: its register);
     uint64_t c_vb = 0, c_ve = 0, c_slot = 0;      // 2: pending (its value starts in a later tile)
 
@@ -836,25 +842,37 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             if (KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
 #if KVR_LANEFRAME
             if (!huge && p < vhi_r && fast_skip == 0u) {
-                // ---- lane-parallel framing: stride prediction, verified -----------------------
-                // Lane j decodes the record that would start at cur + j L, L = the length of the
-                // last record walked (in a store of equal-sized records, every record of the tile
-                // in one round).  Each lane reads its record's header from a window of the segment
-                // bytes (opcode, key length, value length, every engine.rs framing check) and
-                // computes where its successor starts.  Lane 0's position is exact; lane j's is
-                // exact if every lane below it had a valid record whose successor was the predicted
-                // position, so the first mismatch f ends the round: records 0 .. f are the chain
-                // (f's own successor is exact, so the next round predicts from there).  A broken
-                // record, or rounds that stop finding runs of equal lengths, leave the rest of the
-                // tile to the exact scalar hop loop below.
+                // ---- lane-parallel framing: length prediction, verified ------------------------
+                // Lane j decodes the record that would start at a predicted position, from a window
+                // of the segment bytes (opcode, key length, value length, every engine.rs framing
+                // check), and computes where its successor starts.  Lane 0's position is exact; a
+                // lane's is exact if the records before it on its prediction path were valid and
+                // had the predicted lengths.  Two predictions:
+                //   stride  one recent length L: lane j at cur + j L (a store of equal-sized records
+                //           takes every record of the tile in one round); the first lane whose
+                //           successor is not the next prediction ends the round;
+                //   tree    two recent lengths L, L2 (say SETs and DELs of fixed-size keys and
+                //           values): lane n < 63 is node n of a binary tree of depth 6 in heap order,
+                //           at cur + (the lengths on its path), branch 0 = L, 1 = L2; the chain is
+                //           the path from the root that follows each record's actual length, up to
+                //           six records a round.
+                // The round's chain ends at record f (broken, or its successor unpredicted), whose
+                // own successor is exact, so the next round predicts from there.  A broken record,
+                // or rounds that find fewer than three records, leave the rest of the tile to the
+                // exact scalar hop loop below.
                 const int32_t vhiT = (int32_t)vhi_r, remT = (int32_t)rem;
                 int32_t cur = (int32_t)p;
-                uint32_t L = stride;
+                uint32_t L = stride, L2 = stride2;
 #pragma unroll 1
                 while (cur < vhiT) {
                     const bool one = L == 0u || L >= (uint32_t)TILE;   // no usable stride: lane 0 only
-                    const int32_t c = cur + (one ? 0 : lane * (int32_t)L);
-                    const bool act = lane == 0 || (!one && c < vhiT);
+                    const bool tree = KVR_TREE && !one && L2 != 0u && L2 != L && L2 < (uint32_t)TILE;
+                    // tree node n = lane: depth d = floor(log2(n + 1)), path bits = n + 1 below its top
+                    // bit (1 = the L2 branch), tb of them set
+                    const uint32_t nd = (uint32_t)lane + 1u, td = 31u - (uint32_t)__builtin_clz(nd);
+                    const uint32_t tb = (uint32_t)__builtin_popcount(nd ^ (1u << td));
+                    const int32_t c = cur + (one ? 0 : tree ? (int32_t)((td - tb) * L + tb * L2) : lane * (int32_t)L);
+                    const bool act = lane == 0 || (!one && (!tree || lane < 63) && c < vhiT);
                     const int32_t a = c & ~3;
                     const uint32_t s = (uint32_t)c & 3u;
                     uint32_t win[WINW];
@@ -891,20 +909,46 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const uint32_t vb = e + 4u;
                     ok = ok && (!need_v || vlen <= (uint32_t)remT - vb);
                     const uint32_t nx = op == 1u ? e : vb + vlen;
-                    // the first lane whose record is broken or whose successor is not the next
-                    // prediction (the last active lane's successor is unconstrained)
                     const uint64_t actm = __ballot(act);
-                    const int n = (int)__builtin_popcountll(actm);
-                    const bool mis = act && (!ok || (lane < n - 1 && nx != (uint32_t)(c + (int32_t)L)));
-                    const uint64_t mm = __ballot(mis);
-                    const int f = mm ? (int)__builtin_ctzll(mm) : n - 1;
-                    const bool okf = rl32(ok ? 1u : 0u, f) != 0u;
+                    int f;                           // the round's last chain record (a lane)
+                    bool okf;
+                    uint32_t n_on;                   // records on the chain (f's only if valid)
+                    uint64_t onm = 0;                // tree: the chain's lanes
+                    if (!tree) {
+                        // the first lane whose record is broken or whose successor is not the next
+                        // prediction (the last active lane's successor is unconstrained)
+                        const int n = (int)__builtin_popcountll(actm);
+                        const bool mis = act && (!ok || (lane < n - 1 && nx != (uint32_t)(c + (int32_t)L)));
+                        const uint64_t mm = __ballot(mis);
+                        f = mm ? (int)__builtin_ctzll(mm) : n - 1;
+                        okf = rl32(ok ? 1u : 0u, f) != 0u;
+                        n_on = okf ? (uint32_t)f + 1u : (uint32_t)f;
+                    } else {
+                        // follow each record's length down the tree: go = 1 (L) or 2 (L2) per node
+                        const uint32_t ln = nx - (uint32_t)c;
+                        const uint32_t go = ok ? (ln == L ? 1u : (ln == L2 ? 2u : 0u)) : 0u;
+                        int nn = 0;
+                        onm = 1ull;
+#pragma unroll 1
+                        for (int d = 0; d < 5; ++d) {
+                            const uint32_t g = rl32(go, nn);
+                            const int ch = 2 * nn + (int)g;
+                            if (g == 0u || !((actm >> ch) & 1ull)) break;
+                            nn = ch;
+                            onm |= 1ull << nn;
+                        }
+                        f = nn;
+                        okf = rl32(ok ? 1u : 0u, f) != 0u;
+                        if (!okf) onm &= ~(1ull << f);
+                        n_on = (uint32_t)__builtin_popcountll(onm);
+                    }
                     const uint32_t cf = rl32((uint32_t)c, f);
-                    const uint32_t n_on = okf ? (uint32_t)f + 1u : (uint32_t)f;
                     if (n_on) {
-                        // the walked records, lane j = record nrec + j
+                        // the walked records: rank rk = its index in the round's chain (the lane in
+                        // a stride round, the tree depth in a tree round); lane order is position order
                         if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
-                        const bool on = (uint32_t)lane < n_on;
+                        const bool on = tree ? ((onm >> lane) & 1ull) != 0ull : (uint32_t)lane < n_on;
+                        const uint32_t rk = tree ? td : (uint32_t)lane;
                         const uint64_t slot0 = claim(n_on);
                         const uint32_t kmx = wave_max(on ? klen : 0u);
                         uint32_t rerr = N32, rkind = 0;
@@ -922,7 +966,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                                 uint64_t vu = 0;
                                 uint32_t el = 0;
                                 if (!utf8_check(ts, kb, klen, &vu, &el)) {   // engine.rs:114
-                                    rerr = nrec + (uint32_t)lane; rkind = KVR_E_UTF8; raux = vu | ((uint64_t)el << 32);
+                                    rerr = nrec + rk; rkind = KVR_E_UTF8; raux = vu | ((uint64_t)el << 32);
                                 } else {
                                     cc = crc_long(ts, ~0u, kb, klen, K);
                                 }
@@ -938,7 +982,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                                 t.op = (uint8_t)op;
                                 t.flags = 0;
                                 t.reserved = 0;
-                                const uint64_t slot = slot0 + (uint64_t)lane;
+                                const uint64_t slot = slot0 + (uint64_t)rk;
                                 if (slot < pool_cap) pool[slot] = t;
                             }
                         }
@@ -960,9 +1004,10 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                             if (vbl >= (uint32_t)TILE) {
                                 n_carry = 2; n_vb = (uint64_t)(lo + (int64_t)vbl);
                                 n_ve = (uint64_t)(lo + (int64_t)vbl + rl32(vlen, jl));
-                                n_ref = nrec + (uint32_t)jl; n_abs = false;
+                                n_ref = nrec + (tree ? 31u - (uint32_t)__builtin_clz((uint32_t)jl + 1u) : (uint32_t)jl);
+                                n_abs = false;
                             }
-                            fold_views(lmark, (int32_t)vb, (int32_t)(vb + vlen), nrec + (uint32_t)lane);
+                            fold_views(lmark, (int32_t)vb, (int32_t)(vb + vlen), nrec + rk);
                         } else if (lvm) {
                             any_long = true;
                         }
@@ -979,7 +1024,10 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     }
                     if (!okf) { cur = (int32_t)cf; break; }    // a broken record at cf: the exact loop reports it
                     const uint32_t nf = rl32(nx, f);
-                    L = nf - cf;                                // record f's length predicts the next round
+                    // record f's length predicts the next round, with the other recent length
+                    const uint32_t lf = nf - cf;
+                    if (!KVR_TREE) L = lf;
+                    else if (lf != L && lf != L2) { L2 = L; L = lf; }
                     cur = (int32_t)nf;
                     if (err_rec != N32) break;
                     if (!one && n_on < 3u && cur < vhiT) {      // lengths vary: the scalar loop is cheaper
@@ -988,6 +1036,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     }
                 }
                 stride = L;
+                if (KVR_TREE) stride2 = L2;
                 p = cur;
             } else if (fast_skip) {
                 --fast_skip;

@@ -27,6 +27,9 @@ for s in $STEPS; do
     bench5)
       timeout -k 10 400 python -u bench.py --config cfg5 --no-cpu --no-open > "$OUT/bench_cfg5.json" 2> "$OUT/bench_cfg5.err" || { echo "bench cfg5 failed"; tail -20 "$OUT/bench_cfg5.err"; exit 1; }
       cat "$OUT/bench_cfg5.json" ;;
+    bench5c)  # cfg5 with its CPU baselines (a 4-segment sample for the faithful port, the shard for the strong one)
+      timeout -k 10 900 python -u bench.py --config cfg5 --no-open --no-stream > "$OUT/bench_cfg5_cpu.json" 2> "$OUT/bench_cfg5_cpu.err" || { echo "bench cfg5 cpu failed"; tail -20 "$OUT/bench_cfg5_cpu.err"; exit 1; }
+      cat "$OUT/bench_cfg5_cpu.json" ;;
     etag)
       timeout -k 10 300 python -u bench.py --mode etag > "$OUT/bench_etag.json" 2> "$OUT/bench_etag.err" || { echo "bench etag failed"; tail -20 "$OUT/bench_etag.err"; exit 1; }
       cat "$OUT/bench_etag.json" ;;

@@ -96,7 +96,7 @@ int main(int argc, char **argv) {
                     if (pat == 1 && depth == 2) hipLaunchKernelGGL((k_pat<1, 2>), g, t, 0, 0, buf, tps, n_stripes, d, sink);
                 };
                 launch();
-                hipDeviceSynchronize();
+                if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); return 1; }
                 float best = 1e9f;
                 for (int r = 0; r < 5; ++r) {
                     hipEventRecord(e0);
