@@ -62,16 +62,20 @@ constexpr int KEYW = 6;                   // key words the record fast path read
 constexpr int VALW = SMALL / 4;           // value words of a short value
 constexpr int WINW = KEYW + 3;            // decode window: dwords from the candidate's aligned word
 
-// The small tables come first: every table address is a lane-dependent VGPR plus a constant
-// below 64 KiB, which the ds_read instruction carries as its immediate offset.
+// Every table starts below 64 KiB, or is reached through a perm-built address that carries the
+// 64-KiB bit: a lookup is then one address VGPR plus a constant the ds_read instruction carries as
+// its 16-bit immediate offset, with no add (the byte tables C2 are the hot ones: 4 lookups a word).
 struct __align__(16) Smem {
-    uint32_t KR[8 * 16 * 64];             // [i][n][k]: (n << 4i) * x^(8*SC*(k+1)), k < 64
-    uint32_t KQL[8 * 16 * 64];            // [i][n][q]: (n << 4i) * x^(8*4q), q <= SC/4 (columns > SC/4: 0)
-    uint32_t KQ[NQ * 8 * 16];             // [q][i][n]: the same, rows by constant (a lane-uniform q)
+    uint32_t KQ[NQ * 8 * 16];             // [q][i][n]: (n << 4i) * x^(8*4q), q <= SC/4 (a lane-uniform q)
     uint32_t IX[NIX + 3];                 // 0xFFFFFFFF * x^(8j): initial register pushed through j bytes
     uint32_t MK[NWAVE][64];               // per wave: long-value marks by unit (framing)
     uint32_t C2[256 * 64];                // byte tables, row b = 256 B (64 KiB), see Crc
+    uint32_t KR[8 * 16 * 64];             // [i][n][k]: (n << 4i) * x^(8*SC*(k+1)), k < 64  (above 64 KiB,
+    uint32_t KQL[8 * 16 * 64];            // [i][n][q]: as KQ, q per lane (columns > SC/4: 0)  see kmul_col)
 };
+constexpr uint32_t KR_OFF = (uint32_t)offsetof(Smem, KR), KQL_OFF = (uint32_t)offsetof(Smem, KQL);
+static_assert(offsetof(Smem, C2) < 65536, "the byte tables' base fits a ds_read immediate");
+static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit");
 
 // wave priority (s_setprio) of the serial phases: the framing and the records phase are the
 // tile's critical path and share the CU with 15 other waves, so they issue ahead of waves in
@@ -222,18 +226,23 @@ __device__ __forceinline__ uint32_t kmul(uint32_t v, const uint32_t *K) {
     for (int i = 0; i < 8; ++i) t[i] = K[i * 16 + ((pl[i & 1] >> (8 * (i >> 1))) & 255u)];
     return xor8(t);
 }
-// v times the constant in column k (per lane) of a [i][n][k] table of 64 columns (KR, KQL): entry
-// (i, n, k) sits at byte i 4096 + n 256 + 4 k, so its address is one v_perm_b32 (byte 1 = the
-// nibble n from a plane, byte 0 = 4 k from L4k) and the ds_read immediate i 4096
-__device__ __forceinline__ uint32_t kmul_col(uint32_t v, const uint32_t *T, uint32_t L4k) {
-    uint32_t pl[2] = {v & 0x0F0F0F0Fu, (v >> 4) & 0x0F0F0F0Fu};
+// v times the constant in column k (per lane) of a [i][n][k] table of 64 columns (KR, KQL) at
+// byte OFF >= 64 KiB of Smem: entry (i, n, k) sits at OFF + i 4096 + n 256 + 4 k.  Its address is
+// one v_perm_b32: byte 0 = 4 k and byte 2 = 1 (the 64-KiB bit) from L4k, byte 1 = i << 4 | n from
+// a plane (each plane byte carries its lookup's i above the nibble), and the ds_read immediate is
+// OFF - 64 KiB
+template <uint32_t OFF>
+__device__ __forceinline__ uint32_t kmul_col(uint32_t v, const Smem &S, uint32_t k4) {
+    const uint32_t L4k = k4 | 0x10000u;
+    // plane 0: nibbles i = 0, 2, 4, 6 (byte j: i = 2j), plane 1: i = 1, 3, 5, 7
+    uint32_t pl[2] = {(v & 0x0F0F0F0Fu) | 0x60402000u, ((v >> 4) & 0x0F0F0F0Fu) | 0x70503010u};
     asm("" : "+v"(pl[0]), "+v"(pl[1]));   // keep the planes (no re-fusion into nibble shifts)
-    const uint8_t *tb = reinterpret_cast<const uint8_t *>(T);
+    const uint8_t *tb = reinterpret_cast<const uint8_t *>(&S);
     uint32_t t[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
         t[i] = *reinterpret_cast<const uint32_t *>(
-            tb + i * 4096 + __builtin_amdgcn_perm(pl[i & 1], L4k, 0x0C0C0000u | ((4u + (uint32_t)(i >> 1)) << 8)));
+            tb + (OFF - 65536u) + __builtin_amdgcn_perm(pl[i & 1], L4k, 0x0C020000u | ((4u + (uint32_t)(i >> 1)) << 8)));
     return xor8(t);
 }
 
@@ -290,6 +299,34 @@ __device__ __forceinline__ uint32_t crc_words(const uint32_t (&r)[NW + 1], const
     *bad = bd;
     return c;
 }
+// the same when n is one length for every lane of the call (wave-uniform, n <= 4 NW): whole words
+// need no byte masks, so a word is an align, a CRC step and an or (the usual case: every key of a
+// store has one length)
+template <int NW>
+__device__ __forceinline__ uint32_t crc_words_u(const uint32_t (&r)[NW + 1], const Crc &K, uint32_t sh, uint32_t n,
+                                                uint32_t *bad) {
+    uint32_t c = ~0u, bd = 0;
+    const uint32_t nf = n >> 2, rb = n & 3u;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        if ((uint32_t)i < nf) {
+            const uint32_t kw = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
+            bd |= kw & 0x80808080u;
+            c = crc4(c, kw, K);
+        }
+    }
+    if (rb) {
+        uint32_t kw = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+            if ((uint32_t)i == nf) kw = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
+        bd |= kw & ((1u << (8u * rb)) - 1u) & 0x80808080u;
+        for (uint32_t b = 0; b < rb; ++b) c = crc1(c, (kw >> (8u * b)) & 255u, K);
+    }
+    *bad = bd;
+    return c;
+}
+
 // the same over segment bytes [o, o + n) loaded here (o >= 0, o + 4 NW + 4 <= lim)
 template <int NW>
 __device__ __forceinline__ uint32_t crc_span(const TileSeg &ts, const Crc &K, int o, uint32_t n, uint32_t nw,
@@ -950,7 +987,9 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                         const bool on = tree ? ((onm >> lane) & 1ull) != 0ull : (uint32_t)lane < n_on;
                         const uint32_t rk = tree ? td : (uint32_t)lane;
                         const uint64_t slot0 = claim(n_on);
-                        const uint32_t kmx = wave_max(on ? klen : 0u);
+                        // one key length for the batch (lane 0's, ku): no per-lane byte masks
+                        const bool kuni = __ballot(on && klen != ku) == 0ull && ku <= 4u * KEYW;
+                        const uint32_t kmx = kuni ? ku : wave_max(on ? klen : 0u);
                         uint32_t rerr = N32, rkind = 0;
                         uint64_t raux = 0;
                         if (on && !(KVR_ABLATE & 1)) {
@@ -961,7 +1000,8 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                             for (int i = 0; i <= KEYW; ++i) kr[i] = s == 3u ? win[i + 2] : win[i + 1];
                             const int kb = c + 5;
                             uint32_t cc = ~0u, bad = 0x80u;
-                            if (klen <= 4u * KEYW) cc = crc_words<KEYW>(kr, K, (s + 1u) & 3u, klen, nw, &bad);
+                            if (kuni) cc = crc_words_u<KEYW>(kr, K, (s + 1u) & 3u, ku, &bad);
+                            else if (klen <= 4u * KEYW) cc = crc_words<KEYW>(kr, K, (s + 1u) & 3u, klen, nw, &bad);
                             if (bad != 0u) {              // non-ASCII or long key: the full UTF-8 check
                                 uint64_t vu = 0;
                                 uint32_t el = 0;
@@ -1047,7 +1087,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
 #pragma unroll 1
             while (p < vhi_r && !broke && err_rec == N32) {
                 // exact hops; lane j keeps record nrec + j (per-lane selects)
-                uint32_t nb = 0, kmx = 0;
+                uint32_t nb = 0, kmx = 0, kmn = N32;   // the batch's longest and shortest key
                 int32_t myrec = -1;
                 uint32_t my_op = 0, my_klen = 0, my_vlen = 0;
                 uint32_t lmark = 0, bl = 0;
@@ -1074,6 +1114,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                         ++nb;
                         if (op > 1u || remT - q < 5 || (U)klen > (U)(remT - q - 5)) { broke = true; break; }
                         kmx = klen > kmx ? klen : kmx;
+                        kmn = klen < kmn ? klen : kmn;
                         const T e = q + 5 + (T)klen;
                         if (op == 1u) { q = e; continue; }
                         if (remT - e < 4) { broke = true; break; }
@@ -1123,7 +1164,15 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                         const int kb = myrec + 5;
                         const uint32_t klen = my_klen;
                         uint32_t c = ~0u, bad = 0x80u;
-                        if (klen <= 4u * KEYW && kb + 4 * KEYW + 8 <= ts.lim) c = crc_span<KEYW>(ts, K, kb, klen, nw, &bad);
+                        if (kmn == kmx && kmx <= 4u * KEYW && kb + 4 * KEYW + 8 <= ts.lim) {   // one key length
+                            const int a = kb & ~3;
+                            uint32_t r[KEYW + 1];
+#pragma unroll
+                            for (int i = 0; i <= KEYW; ++i) r[i] = (uint32_t)i <= nw ? ts.w32a(a + 4 * i) : 0u;
+                            c = crc_words_u<KEYW>(r, K, (uint32_t)kb & 3u, kmx, &bad);
+                        } else if (klen <= 4u * KEYW && kb + 4 * KEYW + 8 <= ts.lim) {
+                            c = crc_span<KEYW>(ts, K, kb, klen, nw, &bad);
+                        }
                         if (bad != 0u) {              // non-ASCII or long key: the full UTF-8 check
                             uint64_t vu = 0;
                             uint32_t el = 0;
@@ -1242,7 +1291,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             if (!(KVR_ABLATE & 16)) {
                 const int32_t ce = vx > TILE ? 63 : ((vx - 1) >> SC_LOG) - 1;   // (vx = 0: v = 0)
                 const int32_t dd = ce - lane;
-                const uint32_t t_ = kmul_col(v, S.KR, dd > 0 ? 4u * (uint32_t)(dd - 1) : 0u);
+                const uint32_t t_ = kmul_col<KR_OFF>(v, S, dd > 0 ? 4u * (uint32_t)(dd - 1) : 0u);
                 v = dd > 0 ? t_ : v;
                 // (a lane without a source reads 0 from the DPP move -- row_shr past the row start,
                 // the rows a broadcast skips -- which adds nothing and starts no segment, so no lane
@@ -1271,7 +1320,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             if (!(KVR_ABLATE & 16) && m != 0) {
                 const int r = m & 3;
                 const uint32_t base = mb ? (kmul(sin, S.KQ + 128 * H) ^ ca) : sin;
-                uint32_t t = kmul_col(base, S.KQL, 4u * (uint32_t)(mb ? qm - H : qm)) ^ sn;
+                uint32_t t = kmul_col<KQL_OFF>(base, S, 4u * (uint32_t)(mb ? qm - H : qm)) ^ sn;
                 for (int b = 0; b < r; ++b) t = crc1(t, (wm >> (8 * b)) & 255u, K);
                 const uint64_t ms = slot_of(m_ref, m_abs);
                 if (ms < pool_cap) pool[ms].crc32 = ~t;
