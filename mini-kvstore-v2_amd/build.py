@@ -102,6 +102,7 @@ VARIANTS = {
     "lf0": ["-DKVR_LANEFRAME=0"],  # the scalar hop loop for every record
     "a7": ["-DKVR_ABLATE=7"],      # loads + per-tile bookkeeping only (the memory floor at 16 waves/CU)
     "tree": ["-DKVR_TREE=1"],      # tree rounds for two recent record lengths
+    "winpf": ["-DKVR_WINPF=1"],    # the next tile's first window loaded before this tile's CRC phase
     "base": [],
 }
 

@@ -77,11 +77,15 @@ hipError_t wait_stream(hipStream_t st, hipEvent_t ev) {
     }
 }
 
-// k_replay keeps 32-bit pool slots in LDS; KVR_POOL_LIMIT lowers the limit (test knob)
+// k_replay keeps 32-bit pool slots (the pool and its claim slack stay below 2^32 tuples);
+// KVR_POOL_LIMIT lowers the limit (test knob)
 uint64_t pool_limit() {
     const char *e = getenv("KVR_POOL_LIMIT");
-    return e ? std::max<uint64_t>(strtoull(e, nullptr, 10), 1024) : 0xFFFFFF00ull;
+    return e ? std::max<uint64_t>(strtoull(e, nullptr, 10), 1024) : 0xFFFF0000ull;
 }
+// tuples behind pool_cap that serve a claim past it (k_replay flags the overflow and writes there;
+// the host then grows the pool and runs again): one claim of the largest size
+constexpr uint64_t POOL_SLACK = (POOL_CHUNK > TILE_RECS ? POOL_CHUNK : TILE_RECS) + 64;
 
 __global__ void k_shift_seg(kvr_tuple *t, uint64_t n, uint32_t by) {   // seg_idx of a batch's tuples
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -575,7 +579,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             c->pool_need = pool_cap;
             return KVR_ENOMEM;
         }
-        if (c->pool.ensure(pool_cap)) return KVR_ENOMEM;
+        if (c->pool.ensure(pool_cap + POOL_SLACK)) return KVR_ENOMEM;
         kvr_tuple *d_out;
         uint64_t out_cap;
         if (flags & KVR_OUT_ON_DEVICE) {

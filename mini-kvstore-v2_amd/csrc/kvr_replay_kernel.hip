@@ -95,6 +95,9 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #ifndef KVR_TREE   // 1: the lane-parallel framing also predicts with two recent lengths (tree rounds;
 #define KVR_TREE 0     // measured slower: cfg4 2.259 vs 1.964 ms, a tree round's VALU outweighs the hops)
 #endif
+#ifndef KVR_WINPF   // 1: the next tile's first stride-round window is loaded before this tile's CRC phase
+#define KVR_WINPF 0    // (measured slower: cfg2 1.512-1.518 vs 1.440-1.486 ms, cfg4 1.953 vs 1.909)
+#endif
 #ifndef KVR_FAST_BACKOFF   // tiles the scalar hop loop keeps after a lane-parallel round found < 3 records
 #define KVR_FAST_BACKOFF 4
 #endif
@@ -195,14 +198,18 @@ __device__ __forceinline__ uint32_t crc4(uint32_t c, uint32_t w, const Crc &k) {
 __device__ __forceinline__ uint32_t bitop3_xandn(uint32_t a, uint32_t b, uint32_t c) {   // one v_bitop3
     return a ^ (b & ~c);
 }
-// two independent chains stepped together from their inputs x = register ^ data
-__device__ __forceinline__ void crc4x2(uint32_t &ca, uint32_t xa, uint32_t &cb, uint32_t xb, const Crc &k) {
+// the lookups of one slice-by-4 step for two chains' inputs xa, xb, all issued together: the
+// step's result is ta ^ a3 (tb ^ b3), and the next step's input that ^ the next word, one v_bitop3
+__device__ __forceinline__ void look4x2(uint32_t xa, uint32_t xb, const Crc &k, uint32_t &ta, uint32_t &a3, uint32_t &tb,
+                                        uint32_t &b3) {
     const uint32_t ra = __builtin_amdgcn_alignbit(xa, xa, k.rot), rb = __builtin_amdgcn_alignbit(xb, xb, k.rot);
-    uint32_t a0 = s4get(k, ra, 0), a1 = s4get(k, ra, 1), a2 = s4get(k, ra, 2), a3 = s4get(k, ra, 3);
-    uint32_t b0 = s4get(k, rb, 0), b1 = s4get(k, rb, 1), b2 = s4get(k, rb, 2), b3 = s4get(k, rb, 3);
-    asm("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
-    ca = xor3(a0, a1, a2) ^ a3;
-    cb = xor3(b0, b1, b2) ^ b3;
+    uint32_t a0 = s4get(k, ra, 0), a1 = s4get(k, ra, 1), a2 = s4get(k, ra, 2), a3_ = s4get(k, ra, 3);
+    uint32_t b0 = s4get(k, rb, 0), b1 = s4get(k, rb, 1), b2 = s4get(k, rb, 2), b3_ = s4get(k, rb, 3);
+    asm("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3_), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3_));
+    ta = xor3(a0, a1, a2);
+    a3 = a3_;
+    tb = xor3(b0, b1, b2);
+    b3 = b3_;
 }
 __device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
     const uint32_t x = c ^ b;
@@ -513,8 +520,8 @@ struct RecRes {          // one record's outcome on the general path
 
 // parse + emit the record at tile offset o with every engine.rs check, in engine.rs order
 // (its value, if longer than SMALL, was folded by the framing)
-__device__ inline RecRes do_record(const TileSeg &ts, const Crc &K, int64_t o, uint32_t j, uint64_t slot, uint32_t seg,
-                                   kvr_tuple *pool, uint64_t pool_cap) {
+__device__ inline RecRes do_record(const TileSeg &ts, const Crc &K, int64_t o, uint32_t j, uint32_t slot, uint32_t seg,
+                                   kvr_tuple *pool) {
     RecRes ro;
     ro.err = N32; ro.kind = 0; ro.aux = 0;
     const int64_t rem = (int64_t)ts.len - ts.lo;
@@ -547,7 +554,7 @@ __device__ inline RecRes do_record(const TileSeg &ts, const Crc &K, int64_t o, u
         t.val_len = (uint32_t)vlen;
         if (vlen <= (uint64_t)SMALL) t.crc32 = ~crc_long(ts, ~0u, q + 4, vlen, K);
     }
-    if (slot < pool_cap) pool[slot] = t;
+    pool[slot] = t;
     return ro;
 }
 
@@ -660,7 +667,11 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
         if (gw >= n_stripes) return;
         si = gw;
     }
-    uint64_t chunk_base = 0, chunk_left = 0;      // this wave's pool chunk
+    // this wave's pool chunk.  Pool slots are 32-bit (the host keeps the pool under 2^32 - 2^16
+    // tuples) and every slot a wave writes was claimed: a claim past pool_cap (the host then grows
+    // the pool and runs again) is served from the slack the host allocates behind pool_cap, so no
+    // store needs a bound check
+    uint32_t chunk_base = 0, chunk_left = 0;
     // A re-walk (redo pass) walks on into the stripes after its own while their speculated entry
     // disagrees with the chain it carries, so a run of wrong speculations (a value holding a whole
     // segment image, say) costs one pass rather than one pass per stripe (see the end of the loop)
@@ -690,8 +701,15 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
     uint32_t stride = 0, stride2 = 0, fast_skip = 0;   // lane-parallel framing: the two recent record lengths,
                                                        // tiles left to skip
     uint32_t carry = 0, c_state = 0;              // 1: a long value crosses the tile start (c_state: its register);
-    uint64_t c_vb = 0, c_ve = 0, c_slot = 0;      // 2: pending (its value starts in a later tile)
+    uint64_t c_vb = 0, c_ve = 0;                  // 2: pending (its value starts in a later tile)
+    uint32_t c_slot = 0;
 
+    // KVR_WINPF: the decode window of the next tile's first stride round, loaded a tile ahead (its
+    // latency then runs under this tile's CRC phase), and the prediction it was loaded for
+    uint32_t pw[WINW];
+    bool pw_ok = false;
+    int32_t pw_cur = 0;
+    uint32_t pw_L = 0;
     uint32_t w[UW];     // this lane's unit of the tile (the next tile's load is issued as soon as the
     bool loaded = false;   // CRC phase is done with these registers, see the end of the loop body)
     uint32_t k = sd.t_begin;
@@ -788,13 +806,14 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
         int32_t a_off = -1;                  // ... starting inside the unit at a_off
         uint32_t vx_carry = 0;               // ... the value carried in from the previous tile
         int32_t m = 0;                       // a long value ends inside this unit, at m (1 .. SC)
-        uint64_t m_ref = 0;                  // ... its tuple: a slot (m_abs) or a record index of the tile
+        uint32_t m_ref = 0;                  // ... its tuple: a slot (m_abs) or a record index of the tile
         uint32_t m_abs = 0;
         bool any_long = false;               // (uniform) some long value touches the tile
         bool out = false;                    // (uniform) a value crosses the tile end
-        uint64_t out_ve = 0, out_ref = 0;
+        uint64_t out_ve = 0;
+        uint32_t out_ref = 0;
         bool out_abs = false;
-        auto consider = [&](int32_t vb, uint64_t ve_abs, uint64_t ref, bool is_abs, bool from_carry) {
+        auto consider = [&](int32_t vb, uint64_t ve_abs, uint32_t ref, bool is_abs, bool from_carry) {
             const int64_t v64 = (int64_t)ve_abs - lo;
             const int32_t ver = v64 > FAR ? FAR : (int32_t)v64;
             if (vb < ue && ver > ue) { vx = ver; a_off = vb >= us ? vb - us : -1; vx_carry = from_carry ? 1u : 0u; }
@@ -803,7 +822,8 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             any_long = true;
         };
         uint32_t n_carry = 0;
-        uint64_t n_vb = 0, n_ve = 0, n_ref = 0;   // the next tile's carry (n_ref: a slot, or a record index)
+        uint64_t n_vb = 0, n_ve = 0;         // the next tile's carry
+        uint32_t n_ref = 0;                  // (a slot, or a record index)
         bool n_abs = true;
         if (carry == 1u) consider(-FAR, c_ve, c_slot, true, true);
         if (carry == 2u) {                   // a value whose record started in an earlier tile
@@ -811,25 +831,28 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             else { n_carry = 2; n_vb = c_vb; n_ve = c_ve; n_ref = c_slot; }   // still further on
         }
         // pool slots: the tile's records take at most two runs, [b1, b1 + c1) then [b2, ...)
-        uint64_t b1 = 0, b2 = 0;
+        uint32_t b1 = 0, b2 = 0;
         uint32_t c1 = N32;
         uint32_t nrec = 0, err_rec = N32;    // records emitted; index of the tile's first error
         // claim pool slots for nb more records of the tile (one run: a fresh chunk holds any
         // tile's rest); returns the first slot
-        auto claim = [&](uint32_t nb) -> uint64_t {
+        auto claim = [&](uint32_t nb) -> uint32_t {
             if (nb > chunk_left) {
-                const uint64_t cm = pool_chunk > TILE_RECS ? pool_chunk : TILE_RECS;
+                const uint32_t cm = pool_chunk > TILE_RECS ? pool_chunk : TILE_RECS;
                 unsigned long long bb = 0;
                 if (lane == 0) {
                     bb = atomicAdd(&ctr->pool_cursor, (unsigned long long)cm);
-                    if (bb + cm > pool_cap) atomicOr(&ctr->overflow, 1u);
+                    if (bb + cm > pool_cap) {   // past the pool: flag it, write into the slack
+                        atomicOr(&ctr->overflow, 1u);
+                        bb = pool_cap;
+                    }
                 }
-                chunk_base = uni64(bb);
+                chunk_base = uni32((uint32_t)bb);
                 chunk_left = cm;
                 if (nrec) { b2 = chunk_base; c1 = nrec; }   // the tile's second run
             }
             if (nrec == 0) b1 = chunk_base;
-            const uint64_t s0 = chunk_base;
+            const uint32_t s0 = chunk_base;
             chunk_base += nb;
             chunk_left -= nb;
             return s0;
@@ -859,7 +882,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             vx_carry = cx ? 0u : vx_carry;
             const bool cmn = pp != 0u && e2p > us && e2p <= ue;
             m = cmn ? e2p - us : m;
-            m_ref = cmn ? (uint64_t)rkp : m_ref;
+            m_ref = cmn ? rkp : m_ref;
             m_abs = cmn ? 0u : m_abs;
             // a value crossing the last unit's end runs past the tile (ue = TILE there)
             const uint32_t e63 = rl32(cx ? (uint32_t)e2c : 0u, 63);
@@ -913,8 +936,14 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const int32_t a = c & ~3;
                     const uint32_t s = (uint32_t)c & 3u;
                     uint32_t win[WINW];
+                    if (KVR_WINPF && pw_ok && !one && !tree && cur == pw_cur && L == pw_L) {
 #pragma unroll
-                    for (int i = 0; i < WINW; ++i) win[i] = act ? ts.w32a(a + 4 * i) : 0u;
+                        for (int i = 0; i < WINW; ++i) win[i] = pw[i];
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < WINW; ++i) win[i] = act ? ts.w32a(a + 4 * i) : 0u;
+                    }
+                    pw_ok = false;
                     const uint32_t x0 = __builtin_amdgcn_alignbyte(win[1], win[0], s);
                     const uint32_t x1 = __builtin_amdgcn_alignbyte(win[2], win[1], s);
                     const uint32_t op = x0 & 255u, klen = (x0 >> 8) | (x1 << 24);
@@ -986,7 +1015,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                         if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
                         const bool on = tree ? ((onm >> lane) & 1ull) != 0ull : (uint32_t)lane < n_on;
                         const uint32_t rk = tree ? td : (uint32_t)lane;
-                        const uint64_t slot0 = claim(n_on);
+                        const uint32_t slot0 = claim(n_on);
                         // one key length for the batch (lane 0's, ku): no per-lane byte masks
                         const bool kuni = __ballot(on && klen != ku) == 0ull && ku <= 4u * KEYW;
                         const uint32_t kmx = kuni ? ku : wave_max(on ? klen : 0u);
@@ -1022,8 +1051,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                                 t.op = (uint8_t)op;
                                 t.flags = 0;
                                 t.reserved = 0;
-                                const uint64_t slot = slot0 + (uint64_t)rk;
-                                if (slot < pool_cap) pool[slot] = t;
+                                pool[slot0 + rk] = t;
                             }
                         }
                         // long values crossing a unit boundary: marked at their first unit (a scatter
@@ -1147,7 +1175,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const int32_t rvb = myrec + 9 + (int32_t)my_klen, re2 = rvb + (int32_t)my_vlen;
                     fold_views(lmark, rvb, re2, nrec + (uint32_t)lane);
                 }
-                const uint64_t slot = claim(nb) + (uint64_t)lane;
+                const uint32_t slot = claim(nb) + (uint32_t)lane;
                 // the batch's records: lane j emits record nrec + j
                 uint32_t rerr = N32, rkind = 0;
                 uint64_t raux = 0;
@@ -1155,7 +1183,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
                 if (!(KVR_ABLATE & 1) && myrec >= 0) {
                     if (broke && lane == (int)nb - 1) {   // the record that broke the chain: every check
-                        const RecRes r = do_record(ts, K, myrec, j, slot, sd.seg, pool, pool_cap);
+                        const RecRes r = do_record(ts, K, myrec, j, slot, sd.seg, pool);
                         rerr = r.err; rkind = r.kind; raux = r.aux;
                         if (r.err == N32) { rerr = j; rkind = KVR_E_VAL; }   // defensive: a break is an error
                     } else {
@@ -1193,7 +1221,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                             t.op = (uint8_t)my_op;
                             t.flags = 0;
                             t.reserved = 0;
-                            if (slot < pool_cap) pool[slot] = t;
+                            pool[slot] = t;
                         }
                     }
                 }
@@ -1217,20 +1245,42 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
         // load at the loop top does not also wait for this store's ack
         if (in_stripe && lane == 0) {
             TileRes tr;
-            tr.pool_off = nrec ? b1 : 0ull;
+            tr.pool_off = nrec ? (uint64_t)b1 : 0ull;
             tr.pool_off2 = b2;
             tr.count = nrec;
             tr.count1 = c1 < nrec ? c1 : nrec;
             tres[sg.tile0 + k] = tr;
         }
         // a record index of this tile -> its pool slot
-        auto slot_of = [&](uint64_t ref, bool is_abs) -> uint64_t {
+        auto slot_of = [&](uint32_t ref, bool is_abs) -> uint32_t {
             return is_abs ? ref : (ref < c1 ? b1 + ref : b2 + (ref - c1));
         };
         if (n_carry == 2u && !n_abs) n_ref = slot_of(n_ref, false);
         // the stripe goes on past this tile (a value running past its end is carried on)
         const bool need_next = err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry || out);
         KVR_STAMP(2);
+        // the word of a value end's partial tail, for the finalize (issued first: the window loads
+        // below then return after it, and the finalize's wait for it does not wait for them)
+        uint32_t wm = 0;
+        if (!(KVR_ABLATE & 2) && any_long && m != 0 && m < SC) wm = ts.w32a(us + 4 * (m >> 2));
+        // the next tile's first stride round, predicted now (its entry is this tile's exit): its
+        // window is loaded here, so that the latency runs under this tile's CRC phase
+        pw_ok = false;
+        if (KVR_WINPF && walk && err_pos == NONE && tile_exit != ERRP && k + 1 < sd.t_end && k + 1 < sg.n_tiles &&
+            fast_skip == 0u && stride != 0u && stride < (uint32_t)TILE && rem - TILE <= 0x7FFFFFFFll) {
+            const int64_t cur1 = (int64_t)tile_exit - (lo + TILE);
+            const int64_t vhi1 = (rem - TILE) < TILE ? (rem - TILE) : TILE;
+            if (cur1 >= 0 && cur1 < vhi1) {
+                const TileSeg ts1 = tile_seg(abase, sg.base, d0, len, k + 1);
+                const int32_t c1 = (int32_t)cur1 + lane * (int32_t)stride;
+                const bool act1 = lane == 0 || c1 < (int32_t)vhi1;
+#pragma unroll
+                for (int i = 0; i < WINW; ++i) pw[i] = act1 ? ts1.w32a((c1 & ~3) + 4 * i) : 0u;
+                pw_ok = true;
+                pw_cur = (int32_t)cur1;
+                pw_L = stride;
+            }
+        }
         // ---- C. CRC of long values --------------------------------------------------------
         if (!(KVR_ABLATE & 2) && any_long) {
             KVR_STAMP(8);
@@ -1244,26 +1294,48 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             // (one compare per step: q & 15 picks the step, a loop-invariant lane mask the chain)
             const int qh = qm & (H - 1), qah = qa >= 0 ? (qa & (H - 1)) : -1;
             const bool mb = qm >= H, ab = qa >= H;
-            uint32_t ca = 0, cb = 0, sn = 0, wm = 0;
+            // The chains carry the step input x = register ^ word rather than the register: the
+            // lookups' XOR and the next word go into one v_bitop3.  A snapshot takes x at the value
+            // end's word (the register there is x ^ that word, wm, loaded before the loop), and a
+            // restart replaces x by the masked word: x = w & amask.
+            uint32_t ca = 0, cb = 0, sn = 0;
             if (KVR_ABLATE & 8) {
                 ca = w[0]; cb = w[1];
             } else if (!__ballot(m != 0 || qa >= 0)) {
-#pragma unroll
-                for (int kk = 0; kk < H; ++kk) crc4x2(ca, ca ^ w[kk], cb, cb ^ w[kk + H], K);
-            } else {
-                // the word at qm comes from memory (issued here, used after the scan), and a restart
-                // is one select of the step's input: x = restart ? (w & amask) : (c ^ w)
-                if (m & 3) wm = ts.w32a(us + 4 * qm);
+                uint32_t xa = w[0], xb = w[H];
 #pragma unroll
                 for (int kk = 0; kk < H; ++kk) {
-                    const bool s_ = kk == qh;
-                    sn = s_ ? (mb ? cb : ca) : sn;
-                    const bool r = kk == qah, ra = r && !ab, rb = r && ab;
-                    const uint32_t xa = ra ? (w[kk] & amask) : (ca ^ w[kk]);
-                    const uint32_t xb = rb ? (w[kk + H] & amask) : (cb ^ w[kk + H]);
-                    crc4x2(ca, xa, cb, xb, K);
+                    uint32_t ta, a3, tb, b3;
+                    look4x2(xa, xb, K, ta, a3, tb, b3);
+                    if (kk + 1 < H) {
+                        xa = xor3(ta, a3, w[kk + 1]);
+                        xb = xor3(tb, b3, w[kk + 1 + H]);
+                    } else {
+                        ca = ta ^ a3;
+                        cb = tb ^ b3;
+                    }
                 }
-                sn = qm == UW ? cb : sn;
+            } else {
+                uint32_t xa = (qah == 0 && !ab) ? (w[0] & amask) : w[0];
+                uint32_t xb = (qah == 0 && ab) ? (w[H] & amask) : w[H];
+                uint32_t snx = 0;
+#pragma unroll
+                for (int kk = 0; kk < H; ++kk) {
+                    snx = kk == qh ? (mb ? xb : xa) : snx;
+                    uint32_t ta, a3, tb, b3;
+                    look4x2(xa, xb, K, ta, a3, tb, b3);
+                    if (kk + 1 < H) {
+                        xa = xor3(ta, a3, w[kk + 1]);
+                        xb = xor3(tb, b3, w[kk + 1 + H]);
+                        const bool r = kk + 1 == qah;
+                        xa = (r && !ab) ? (w[kk + 1] & amask) : xa;
+                        xb = (r && ab) ? (w[kk + 1 + H] & amask) : xb;
+                    } else {
+                        ca = ta ^ a3;
+                        cb = tb ^ b3;
+                    }
+                }
+                sn = qm == UW ? cb : (snx ^ wm);
             }
             // the unit loop was the tile registers' last reader: the next tile's load is issued
             // here and its latency runs under the scan and the finalize
@@ -1322,8 +1394,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 const uint32_t base = mb ? (kmul(sin, S.KQ + 128 * H) ^ ca) : sin;
                 uint32_t t = kmul_col<KQL_OFF>(base, S, 4u * (uint32_t)(mb ? qm - H : qm)) ^ sn;
                 for (int b = 0; b < r; ++b) t = crc1(t, (wm >> (8 * b)) & 255u, K);
-                const uint64_t ms = slot_of(m_ref, m_abs);
-                if (ms < pool_cap) pool[ms].crc32 = ~t;
+                pool[slot_of(m_ref, m_abs)].crc32 = ~t;
             }
             if (out) {                           // the value running past the tile: hand over its register
                 n_carry = 1;

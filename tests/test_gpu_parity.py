@@ -162,6 +162,20 @@ def test_adversarial_speculation(gctx):
     check_parity(gctx, [seg, seg[: len(seg) // 2 + 13], inner, zeros])
 
 
+def test_pool_overflow_retry(gctx):
+    """Records far denser than the pool estimate (5-byte DELs of empty keys, few long stripes):
+    the waves' claims run past the pool, land in its slack, the overflow is flagged, and the host
+    grows the pool and replays again -- same tuples as the oracle (engine.rs:139-141 DEL records)."""
+    dense = rec_del(b"") * ((8 << 20) // 5)
+    mixed = b"".join(rec_set(b"k%d" % i, b"") + rec_del(b"") * 7 for i in range(100_000))
+    gctx.set_tiles_per_stripe(1024)
+    try:
+        check_parity(gctx, [dense, mixed, dense[:-2]])
+        check_parity(gctx, [mixed, dense])
+    finally:
+        gctx.set_tiles_per_stripe(0)
+
+
 def _blob_store(image_values, seed):
     """A segment whose big values are whole segment images (valid record chains), each spanning
     hundreds of single-tile stripes, between runs of ordinary records."""

@@ -37,6 +37,30 @@ __device__ __forceinline__ uint32_t spin(uint32_t x, int n) {
     return x;
 }
 
+// VALU issue rate: n instructions per lane as 4 independent dependent chains (ILP 4), or one chain
+template <int ILP>
+__global__ __launch_bounds__(RT) void k_valu(uint32_t *sink, int n) {
+    __shared__ uint32_t pin[100 * 1024 / 4];
+    uint32_t a = threadIdx.x, b = a * 3u, c = a * 5u, d = a * 7u;
+    if (threadIdx.x == 0) pin[0] = 0;
+#pragma unroll 1
+    for (int i = 0; i < n; i += 8) {
+        if (ILP == 4)
+            asm volatile("v_xad_u32 %0, %0, %0, %0\n v_xad_u32 %1, %1, %1, %1\n v_xad_u32 %2, %2, %2, %2\n v_xad_u32 %3, %3, %3, %3\n"
+                         "v_xad_u32 %0, %0, %0, %0\n v_xad_u32 %1, %1, %1, %1\n v_xad_u32 %2, %2, %2, %2\n v_xad_u32 %3, %3, %3, %3"
+                         : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+        else if (ILP == 2)
+            asm volatile("v_xor_b32 %0, %0, %1\n v_xor_b32 %1, %1, %0\n v_xor_b32 %2, %2, %3\n v_xor_b32 %3, %3, %2\n"
+                         "v_xor_b32 %0, %0, %1\n v_xor_b32 %1, %1, %0\n v_xor_b32 %2, %2, %3\n v_xor_b32 %3, %3, %2"
+                         : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+        else
+            asm volatile("v_xad_u32 %0, %0, %0, %0\n v_xad_u32 %0, %0, %0, %0\n v_xad_u32 %0, %0, %0, %0\n v_xad_u32 %0, %0, %0, %0\n"
+                         "v_xad_u32 %0, %0, %0, %0\n v_xad_u32 %0, %0, %0, %0\n v_xad_u32 %0, %0, %0, %0\n v_xad_u32 %0, %0, %0, %0"
+                         : "+v"(a));
+    }
+    if ((a ^ b ^ c ^ d) == 0x12345678u) sink[threadIdx.x] = a + pin[0];
+}
+
 template <int PAT, int DEPTH>
 __global__ __launch_bounds__(RT) void k_pat(const uint8_t *__restrict__ buf, uint64_t tiles_per_stripe,
                                             uint32_t n_stripes, int delay, uint32_t *sink) {
@@ -84,6 +108,31 @@ int main(int argc, char **argv) {
     hipEventCreate(&e1);
     printf("cus=%d stripes=%u tiles/stripe=%llu bytes=%llu\n", ncu, n_stripes, (unsigned long long)tps,
            (unsigned long long)(tps * n_stripes * TILE));
+    {   // VALU issue: 16 waves per CU, 1<<16 instructions per lane
+        const int n = 1 << 16;
+        for (int ilp : {1, 2, 4}) {
+            auto run = [&]() {
+                if (ilp == 1) hipLaunchKernelGGL((k_valu<1>), dim3(ncu), dim3(RT), 0, 0, sink, n);
+                if (ilp == 2) hipLaunchKernelGGL((k_valu<2>), dim3(ncu), dim3(RT), 0, 0, sink, n);
+                if (ilp == 4) hipLaunchKernelGGL((k_valu<4>), dim3(ncu), dim3(RT), 0, 0, sink, n);
+            };
+            run();
+            if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); return 1; }
+            hipEventRecord(e0);
+            run();
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms = 0;
+            hipEventElapsedTime(&ms, e0, e1);
+            // per SIMD: 4 waves x n instructions; cycles at the measured clock below
+            int khz = 0;
+            hipDeviceGetAttribute(&khz, hipDeviceAttributeClockRate, 0);
+            const double cyc = ms * 1e-3 * khz * 1e3;
+            printf("valu ilp %d (%s): %.3f ms, %.2f cycles per wave64 VALU per SIMD at %d MHz\n", ilp,
+                   ilp == 2 ? "v_xor_b32 pairs" : "v_xad_u32", ms, cyc / (4.0 * n), khz / 1000);
+            fflush(stdout);
+        }
+    }
     const int delays[] = {0, 256, 512, 1024, 2048};
     for (int pat = 0; pat < 2; ++pat)
         for (int depth = 1; depth <= 2; ++depth)
