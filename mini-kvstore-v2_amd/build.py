@@ -103,6 +103,10 @@ VARIANTS = {
     "a7": ["-DKVR_ABLATE=7"],      # loads + per-tile bookkeeping only (the memory floor at 16 waves/CU)
     "tree": ["-DKVR_TREE=1"],      # tree rounds for two recent record lengths
     "winpf": ["-DKVR_WINPF=1"],    # the next tile's first window loaded before this tile's CRC phase
+    "notop": ["-DKVR_TOPWAIT=0"],  # no wait for the tile's load at the loop top
+    "wpf2": ["-DKVR_WINPF=1", "-DKVR_TOPWAIT=0"],   # both: a tile's first round framed under its load
+    "nouni": ["-DKVR_UNIFOLD=0"],  # long-value views through LDS marks + lane permutes only
+    "rounds": ["-DKVR_ROUNDS=64"],  # lane-parallel rounds in a loop (until the tile end or a short round)
     "base": [],
 }
 

@@ -98,6 +98,15 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #ifndef KVR_WINPF   // 1: the next tile's first stride-round window is loaded before this tile's CRC phase
 #define KVR_WINPF 0    // (measured slower: cfg2 1.512-1.518 vs 1.440-1.486 ms, cfg4 1.953 vs 1.909)
 #endif
+#ifndef KVR_TOPWAIT   // 1: wait for the tile's load at the top of the loop (0: where its registers are
+#define KVR_TOPWAIT 1   // first read, so framing that reads only memory windows runs under the load)
+#endif
+#ifndef KVR_UNIFOLD   // 1: a stride round of equal SETs folds its long values into the units by arithmetic
+#define KVR_UNIFOLD 1
+#endif
+#ifndef KVR_ROUNDS   // lane-parallel rounds a tile at most (the scalar hop loop takes the rest)
+#define KVR_ROUNDS 1
+#endif
 #ifndef KVR_FAST_BACKOFF   // tiles the scalar hop loop keeps after a lane-parallel round found < 3 records
 #define KVR_FAST_BACKOFF 4
 #endif
@@ -718,13 +727,13 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
     unsigned long long prof_acc[16] = {};
 #endif
     for (;; ++k) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (KVR_TOPWAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         KVR_STAMP(5);
         const bool in_stripe = k < sd.t_end;
         if (stop || (!in_stripe && !carry) || k >= sg.n_tiles) break;
         if (!loaded) {
             load_unit(abase, d0, len, k, lane, w);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (KVR_TOPWAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         loaded = false;
         if (KVR_ABLATE & 64) {   // loads only (FETCH_SIZE calibration on a known byte count)
@@ -892,6 +901,39 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             }
             any_long = true;
         };
+        // fold_views for a round of n records of one length Ls, all SETs with one value length vu >
+        // SC (so every value crosses a unit boundary): record j's value is [vb0 + j Ls, + vu), so a
+        // unit finds the last value starting before its end (and before its start) by a division,
+        // with no marks in LDS and no lane permutes
+        auto fold_uniform = [&](int32_t vb0, int32_t Ls, uint32_t n, int32_t vu, uint32_t nbase) {
+            const float invL = 1.0f / (float)Ls;
+            auto below = [&](int32_t X) -> uint32_t {   // records with vb0 + j Ls < X (at most n)
+                const int32_t t = X - vb0 - 1;
+                int32_t q = (int32_t)((float)(t < 0 ? 0 : t) * invL);   // floor(t / Ls), then corrected
+                q += (q + 1) * Ls <= t ? 1 : 0;
+                q -= q * Ls > t ? 1 : 0;
+                const uint32_t c = t < 0 ? 0u : (uint32_t)q + 1u;
+                return c < n ? c : n;
+            };
+            const uint32_t nc = below(ue), np = below(us);
+            const int32_t vbc = vb0 + ((int32_t)nc - 1) * Ls, e2c = vbc + vu;
+            const bool cx = nc != 0u && e2c > ue;
+            vx = cx ? e2c : vx;
+            a_off = cx ? (vbc >= us ? vbc - us : -1) : a_off;
+            vx_carry = cx ? 0u : vx_carry;
+            const int32_t e2p = vb0 + ((int32_t)np - 1) * Ls + vu;
+            const bool cmn = np != 0u && e2p > us && e2p <= ue;
+            m = cmn ? e2p - us : m;
+            m_ref = cmn ? nbase + np - 1u : m_ref;
+            m_abs = cmn ? 0u : m_abs;
+            // a value crossing the last unit's end runs past the tile (ue = TILE there)
+            const uint32_t e63 = rl32(cx ? (uint32_t)e2c : 0u, 63);
+            if (e63 != 0u) {
+                out = true; out_ve = (uint64_t)(lo + (int32_t)e63);
+                out_ref = nbase + rl32(nc, 63) - 1u; out_abs = false;
+            }
+            any_long = true;
+        };
         if (walk) {
             // positions are tile-relative, in 32 bits unless the segment runs more than 2 GiB past
             // the tile (then the 64-bit copy of the exact hop loop takes the whole tile)
@@ -923,8 +965,14 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 const int32_t vhiT = (int32_t)vhi_r, remT = (int32_t)rem;
                 int32_t cur = (int32_t)p;
                 uint32_t L = stride, L2 = stride2;
+                // (KVR_ROUNDS = 1: one round a tile, the scalar loop takes any rest: no loop here, whose
+                // header made the compiler spill and reload much of the stripe state every tile)
+#if KVR_ROUNDS == 1
+                if (cur < vhiT) do {
+#else
 #pragma unroll 1
-                while (cur < vhiT) {
+                for (int round = 0; round < KVR_ROUNDS && cur < vhiT; ++round) {
+#endif
                     const bool one = L == 0u || L >= (uint32_t)TILE;   // no usable stride: lane 0 only
                     const bool tree = KVR_TREE && !one && L2 != 0u && L2 != L && L2 < (uint32_t)TILE;
                     // tree node n = lane: depth d = floor(log2(n + 1)), path bits = n + 1 below its top
@@ -1059,13 +1107,20 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                         const bool lv = on && op == 0u && vlen > (uint32_t)SMALL &&
                                         ((vb ^ (vb + vlen - 1u)) >> SC_LOG) != 0u;
                         const uint64_t lvm = __ballot(lv);
+                        // a round of SETs of one key and one value length (longer than a unit)
+                        const uint32_t vu = rl32(vlen, 0);
+                        const bool vuni = KVR_UNIFOLD && !tree && !one && vu > (uint32_t)SC &&
+                                          __ballot(on && (op != 0u || vlen != vu || klen != ku)) == 0ull;
                         if (lvm && !(KVR_ABLATE & 32)) {
-                            MK[lane] = 0u;
-                            __builtin_amdgcn_wave_barrier();
-                            if (lv && vb < (uint32_t)TILE) MK[vb >> SC_LOG] = (uint32_t)lane + 1u;
-                            __builtin_amdgcn_wave_barrier();
-                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                            const uint32_t lmark = MK[lane];
+                            uint32_t lmark = 0;
+                            if (!vuni) {
+                                MK[lane] = 0u;
+                                __builtin_amdgcn_wave_barrier();
+                                if (lv && vb < (uint32_t)TILE) MK[vb >> SC_LOG] = (uint32_t)lane + 1u;
+                                __builtin_amdgcn_wave_barrier();
+                                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                                lmark = MK[lane];
+                            }
                             // a long value starting past the tile end (only the last record): carried
                             const int jl = 63 - (int)__builtin_clzll(lvm);
                             const uint32_t vbl = rl32(vb, jl);
@@ -1075,7 +1130,8 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                                 n_ref = nrec + (tree ? 31u - (uint32_t)__builtin_clz((uint32_t)jl + 1u) : (uint32_t)jl);
                                 n_abs = false;
                             }
-                            fold_views(lmark, (int32_t)vb, (int32_t)(vb + vlen), nrec + rk);
+                            if (vuni) fold_uniform(cur + 9 + (int32_t)ku, (int32_t)L, n_on, (int32_t)vu, nrec);
+                            else fold_views(lmark, (int32_t)vb, (int32_t)(vb + vlen), nrec + rk);
                         } else if (lvm) {
                             any_long = true;
                         }
@@ -1102,7 +1158,11 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                         fast_skip = KVR_FAST_BACKOFF;
                         break;
                     }
+#if KVR_ROUNDS == 1
+                } while (0);
+#else
                 }
+#endif
                 stride = L;
                 if (KVR_TREE) stride2 = L2;
                 p = cur;
@@ -1111,6 +1171,9 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             }
 #endif
             // ---- the exact scalar hop loop: anything the lane-parallel framing left -----------
+            // (entered only when the lane-parallel round left part of the tile: the loop's spill and
+            // reload code then stays off the common path)
+            if (p < vhi_r && err_rec == N32) {
             int64_t lastq = -1;              // the last record start it walked (its length is the next stride)
 #pragma unroll 1
             while (p < vhi_r && !broke && err_rec == N32) {
@@ -1237,6 +1300,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
             }
             if (lastq >= 0 && !broke && !huge) stride = (uint32_t)(p - lastq);
+            }
             if (KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(0);
             tile_exit = broke ? ERRP : (uint64_t)(lo + p);
         }
