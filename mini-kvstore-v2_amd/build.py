@@ -98,15 +98,10 @@ VARIANTS = {
     "rt768": ["-DKVR_RT=768"],     # 12 stripes per workgroup
     "prio0": ["-DKVR_HOP_PRIO=0", "-DKVR_REC_PRIO=0"],   # no raised wave priority
     "fin0": ["-DKVR_FIN_PRIO=0"],  # the scan + finalize chain at priority 0
-    "pf1": ["-DKVR_PREFETCH=1"],   # a prefetch wave per workgroup (cfg2 1.540 vs 1.396 ms: not kept)
     "lf0": ["-DKVR_LANEFRAME=0"],  # the scalar hop loop for every record
     "a7": ["-DKVR_ABLATE=7"],      # loads + per-tile bookkeeping only (the memory floor at 16 waves/CU)
-    "tree": ["-DKVR_TREE=1"],      # tree rounds for two recent record lengths
-    "winpf": ["-DKVR_WINPF=1"],    # the next tile's first window loaded before this tile's CRC phase
     "notop": ["-DKVR_TOPWAIT=0"],  # no wait for the tile's load at the loop top
-    "wpf2": ["-DKVR_WINPF=1", "-DKVR_TOPWAIT=0"],   # both: a tile's first round framed under its load
     "nouni": ["-DKVR_UNIFOLD=0"],  # long-value views through LDS marks + lane permutes only
-    "rounds": ["-DKVR_ROUNDS=64"],  # lane-parallel rounds in a loop (until the tile end or a short round)
     "base": [],
 }
 

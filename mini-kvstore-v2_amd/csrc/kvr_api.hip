@@ -4,7 +4,7 @@
  *
  * One kvr_replay call:
  *   [H2D of host segments]  k_replay(all stripes)  k_link  k_rewalk(re-walk list)  k_link
- *   k_tsum  k_tscan  k_compact  [D2H of tuples]  — one stream, one host synchronisation in the
+ *   k_compact_s  [D2H of tuples]  — one stream, one host synchronisation in the
  *   common case; k_rewalk/k_link rounds only when a speculated stripe entry was wrong (a re-walk
  *   walks on through the wrongly speculated stripes after its own, so one round is the usual case).
  */
@@ -54,12 +54,6 @@ struct DevBuf {
 };
 
 constexpr uint32_t REDO_GRID = 1024;
-#ifndef KVR_GATHER_REC   // 1: the compaction's gather one wave per live record (0: one wave per 512-B block)
-#define KVR_GATHER_REC 1
-#endif
-#ifndef KVR_CSTRIPE   // 1: compaction per stripe from k_link's stripe offsets (0: k_tsum + k_tscan + k_compact)
-#define KVR_CSTRIPE 1
-#endif
 constexpr size_t LC_CTR = 64;                     // Counters' offset in the link + counters block
 constexpr size_t LC_BYTES = 128;
 static_assert(sizeof(LinkResult) <= LC_CTR && LC_CTR + sizeof(Counters) <= LC_BYTES, "link + counters block");
@@ -110,7 +104,6 @@ struct kvr_ctx {
     DevBuf<LinkResult> link;
     DevBuf<Counters> ctr;
     DevBuf<uint32_t> seg_bad, seg_err, expected;
-    DevBuf<uint64_t> bsum;
     DevBuf<uint64_t> soff;                 // each stripe's output offset (k_link, for k_compact_s)
     DevBuf<uint32_t> crc, kmul, initx;
     DevBuf<GenRecDev> gen;
@@ -120,7 +113,7 @@ struct kvr_ctx {
     DevBuf<uint32_t> flist, fcnt;          // collision rounds: two tuple lists, their counts
     DevBuf<uint32_t> fsz;                  // the fold table's size on the device (k_hll_size)
     bool fold_pending = false;             // deferred rounds launched, not yet checked (fold_settle)
-    DevBuf<uint32_t> cslot, cflag, cpos, cfirst;
+    DevBuf<uint32_t> cslot, cflag, cpos;
     DevBuf<uint64_t> csize, coff, l_src, l_off, ctot, ccuts;
     DevBuf<uint8_t> cout, ctmp;
     kvr_compact_stats cstats{};
@@ -337,12 +330,12 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->pool.release(); c->dense.release(); c->redo.release();
     c->link.p = nullptr; c->ctr.p = nullptr;   // (inside lcbuf)
     c->lcbuf.release();
-    c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->bsum.release(); c->soff.release();
+    c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->soff.release();
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
     c->ctup.release(); c->lout.release(); c->fent.release(); c->flist.release(); c->fcnt.release(); c->fsz.release();
     c->cslot.release(); c->cflag.release(); c->islots.release(); c->ing.release(); c->hpart.release(); c->hreg.release();
     c->koff.release(); c->klen.release(); c->kbuf.release();
-    c->cpos.release(); c->cfirst.release(); c->csize.release(); c->coff.release(); c->l_src.release();
+    c->cpos.release(); c->csize.release(); c->coff.release(); c->l_src.release();
     c->l_off.release(); c->ctot.release(); c->ccuts.release(); c->cout.release(); c->ctmp.release();
     c->c_gidx.release(); c->c_own.release(); c->c_sidx.release(); c->c_val.release(); c->c_scan.release();
     c->c_gstart.release(); c->c_hdr.release(); c->c_keys.release(); c->r_rep.release(); c->r_slot.release();
@@ -554,8 +547,6 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
     c->up_tps = tps;
     c->h_stripes_up = true;
 
-    const uint32_t nb = (n_tiles + CB - 1) / CB;
-    if (c->bsum.ensure(nb)) return KVR_ENOMEM;
 
     const uint32_t *d_exp = nullptr;
     if (expected && n_expected) {
@@ -591,18 +582,11 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             out_cap = pool_cap;
         }
         // the ordered gather pool -> output: one workgroup per stripe from the stripe offsets k_link
-        // computes (KVR_CSTRIPE), or the scan of per-tile counts then a workgroup per 256 tiles
+        // computes
         auto launch_compact = [&]() {
-            if (KVR_CSTRIPE) {
-                hipLaunchKernelGGL(k_compact_s, dim3(n_stripes), dim3(CT), 0, st, c->segs.p, c->stripes.p, c->soff.p,
-                                   c->tres.p, c->pool.p, pool_cap, d_out, out_cap, d_exp,
-                                   (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p);
-            } else {
-                hipLaunchKernelGGL(k_tsum, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->link.p);
-                hipLaunchKernelGGL(k_tscan, dim3(1), dim3(1024), 0, st, c->bsum.p, nb, c->ctr.p, c->link.p);
-                hipLaunchKernelGGL(k_compact, dim3(nb), dim3(CT), 0, st, c->tres.p, n_tiles, c->bsum.p, c->pool.p, pool_cap,
-                                   d_out, out_cap, d_exp, (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p);
-            }
+            hipLaunchKernelGGL(k_compact_s, dim3(n_stripes), dim3(CT), 0, st, c->segs.p, c->stripes.p, c->soff.p,
+                               c->tres.p, c->pool.p, pool_cap, d_out, out_cap, d_exp,
+                               (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p);
         };
         // counters and link result start at zero (the last successful call cleared them behind its
         // results, so this memset usually runs only on a context's first call or after an error)
@@ -969,11 +953,10 @@ static int compact_back(kvr_ctx *c, uint32_t flags, uint64_t seg_target, uint8_t
     HIPCHK(hipGetLastError());
     // the live bytes are at most the segment bytes: size everything by that bound, so the rest of
     // the pipeline runs without a host round trip (the kernels read the true sizes on device)
-    const uint64_t max_blocks = (bytes_in + CBLK - 1) / CBLK;
     const uint64_t max_cuts = seg_target ? bytes_in / seg_target + 1 : 1;
-    if (c->cfirst.ensure(max_blocks) || c->ccuts.ensure(max_cuts)) return KVR_ENOMEM;
+    if (c->ccuts.ensure(max_cuts)) return KVR_ENOMEM;
     hipLaunchKernelGGL(k_scatter, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p, c->csize.p, c->coff.p,
-                       c->cflag.p, c->cpos.p, c->l_src.p, c->l_off.p, c->cfirst.p);
+                       c->cflag.p, c->cpos.p, c->l_src.p, c->l_off.p);
     HIPCHK(hipGetLastError());
     if (seg_target) {
         hipLaunchKernelGGL(k_cuts, dim3((uint32_t)std::min<uint64_t>((max_cuts + 255) / 256, 1024)), dim3(256), 0, st,
@@ -990,14 +973,8 @@ static int compact_back(kvr_ctx *c, uint32_t flags, uint64_t seg_target, uint8_t
         d_out = c->cout.p;
         d_cap = bytes_in;
     }
-    const uint32_t gw = (uint32_t)std::min<uint64_t>((max_blocks + CT_GATHER / 64 - 1) / (CT_GATHER / 64),
-                                                     (uint64_t)c->n_cu * 16);
-    if (KVR_GATHER_REC)
-        hipLaunchKernelGGL(k_gather_r, dim3((uint32_t)c->n_cu * 16), dim3(CT_GATHER), 0, st, c->l_src.p, c->l_off.p,
-                           c->ctot.p, d_out, d_cap);
-    else
-        hipLaunchKernelGGL(k_gather, dim3(std::max(gw, 1u)), dim3(CT_GATHER), 0, st, c->l_src.p, c->l_off.p, c->cfirst.p,
-                           c->ctot.p, d_out, d_cap);
+    hipLaunchKernelGGL(k_gather_r, dim3((uint32_t)c->n_cu * 16), dim3(CT_GATHER), 0, st, c->l_src.p, c->l_off.p,
+                       c->ctot.p, d_out, d_cap);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[2], st));
     uint64_t tot[2] = {0, 0};

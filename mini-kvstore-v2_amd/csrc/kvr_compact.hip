@@ -26,14 +26,10 @@
  *   k_live_ent      per claimed entry: its key's last tuple is live iff it is a SET: flag, size
  *                   9 + k + v
  *   (scan)          exclusive sums of sizes (output offsets) and live flags (dense index)
- *   k_scatter       dense live list (source address, output offset) and, for every 512-B
- *                   output block, the live record holding its first byte
- *   k_gather        one wave per 512-B output block: 8 B per lane, the lane's record found by
- *                   a 6-step binary search over the wave's record ends (DPP/bpermute), the
- *                   bytes copied verbatim (the framing of engine.rs:169-173 is the record's own).
- *                   (16-B lanes over 1-KiB blocks, with aligned 16-B loads and stores, measured
- *                   slower on cfg4: 0.70 vs 0.62 ms, also with two blocks in flight per wave —
- *                   the per-block chain of dependent index loads bounds it, not the byte moves.)
+ *   k_scatter       dense live list (source address, output offset)
+ *   k_gather_r      one wave per live record: the record's bytes copied verbatim (the framing of
+ *                   engine.rs:169-173 is the record's own), its 16-B aligned output body as 16 B
+ *                   per lane, the unaligned head and tail bytes one per lane
  *   k_cuts          new-segment boundaries: a segment starts at the first live record whose
  *                   output offset is >= k * seg_target
  * Bytes moved (the roofline): live bytes read + live bytes written + 32 B per
@@ -50,10 +46,7 @@
 namespace kvr {
 
 constexpr uint32_t HT_EMPTY = 0xFFFFFFFFu;
-constexpr int CBLK = 512;            // output bytes per gather wave (8 B per lane)
-constexpr int CBLK_LOG = 9;
-static_assert(CBLK == 1 << CBLK_LOG, "block size");
-constexpr int CT_GATHER = 256;       // threads per gather workgroup (4 blocks)
+constexpr int CT_GATHER = 256;       // threads per gather workgroup (4 records at a time)
 
 __host__ __device__ __forceinline__ uint32_t ht_mix(uint32_t h) {   // the key_tag is a CRC: spread it
     h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
@@ -352,91 +345,20 @@ __global__ void k_ctotals(const uint64_t *__restrict__ size, const uint64_t *__r
     totals[1] = live;
 }
 
-// dense live list + the first live record of every output block
+// dense live list
 __global__ void k_scatter(const kvr_tuple *__restrict__ tup, uint64_t n, const SegDesc *__restrict__ segs,
                           const uint64_t *__restrict__ size, const uint64_t *__restrict__ off,
                           const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
-                          uint64_t *__restrict__ l_src, uint64_t *__restrict__ l_off, uint32_t *__restrict__ first) {
+                          uint64_t *__restrict__ l_src, uint64_t *__restrict__ l_off) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || !flag[i]) return;
     const kvr_tuple t = tup[i];
     const uint32_t j = pos[i];
-    const uint64_t s = off[i], e = s + size[i];
     l_src[j] = reinterpret_cast<uint64_t>(segs[t.seg_idx].base + t.rec_off);
-    l_off[j] = s;
-    for (uint64_t b = (s + CBLK - 1) >> CBLK_LOG; (b << CBLK_LOG) < e; ++b) first[b] = j;
+    l_off[j] = off[i];
 }
 
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int l) {
-    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, l, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64);
-    return ((uint64_t)hi << 32) | lo;
-}
-
-// one wave per 512-B output block (grid-stride over the blocks; their number comes from the
-// device totals); lane l writes output bytes [b*512 + 8l, + 8), none at or past cap
-__global__ void __launch_bounds__(CT_GATHER) k_gather(const uint64_t *__restrict__ l_src, const uint64_t *__restrict__ l_off,
-                                                      const uint32_t *__restrict__ first, const uint64_t *__restrict__ totals,
-                                                      uint8_t *__restrict__ out, uint64_t cap) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t total = totals[0];
-    const uint32_t n_live = (uint32_t)totals[1];
-    const uint64_t n_blocks = (total + CBLK - 1) >> CBLK_LOG;
-    const uint64_t lim = total < cap ? total : cap;
-    const uint64_t waves = (uint64_t)gridDim.x * (CT_GATHER / 64);
-    for (uint64_t b = (uint64_t)blockIdx.x * (CT_GATHER / 64) + (threadIdx.x >> 6); b < n_blocks; b += waves) {
-        const uint32_t j0 = first[b];
-        // lane l: the end of live record j0 + l (records are >= 9 B: at most 57 start in a block)
-        const uint32_t jl = j0 + (uint32_t)lane;
-        const uint64_t e = jl < n_live ? l_off[jl + 1] : ~0ull;
-        const uint64_t x = (b << CBLK_LOG) + 8u * (uint32_t)lane;
-        int c = 0;   // live records of the wave ending at or before x
-#pragma unroll
-        for (int step = 32; step >= 1; step >>= 1) {
-            const uint64_t ev = shfl64(e, c + step - 1);
-            if (ev <= x) c += step;
-        }
-        const uint64_t ej = shfl64(e, c);
-        if (x >= lim) continue;
-        uint32_t j = j0 + (uint32_t)c;
-        uint64_t sj = l_off[j];
-        uint32_t lo, hi;
-        if (ej - x >= 8) {   // the lane's 8 bytes lie in one record: aligned dword reads + funnel shifts
-            const uint64_t src = l_src[j] + (x - sj);
-            const uint32_t *a = reinterpret_cast<const uint32_t *>(src & ~3ull);
-            const uint32_t sh = (uint32_t)src & 3u;
-            const uint32_t w0 = a[0], w1 = a[1], w2 = sh ? a[2] : 0u;   // a[2] holds byte src + 7 when sh != 0
-            lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
-            hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-        } else {             // the lane's bytes span records: byte by byte
-            uint64_t ejj = ej, src = l_src[j];   // record base: bytes indexed by output offset - record start
-            uint8_t by[8];
-            for (int q = 0; q < 8; ++q) {
-                const uint64_t xq = x + q;
-                if (xq >= total) { by[q] = 0; continue; }
-                while (xq >= ejj) {
-                    ++j;
-                    sj = ejj;
-                    src = l_src[j];
-                    ejj = l_off[j + 1];
-                }
-                by[q] = reinterpret_cast<const uint8_t *>(src)[xq - sj];
-            }
-            lo = by[0] | (by[1] << 8) | (by[2] << 16) | ((uint32_t)by[3] << 24);
-            hi = by[4] | (by[5] << 8) | (by[6] << 16) | ((uint32_t)by[7] << 24);
-        }
-        if (x + 8 <= lim) {
-            uint2 v;
-            v.x = lo;
-            v.y = hi;
-            *reinterpret_cast<uint2 *>(out + x) = v;   // out is 8-B aligned (the host stages otherwise)
-        } else {
-            const uint64_t m = lim - x;
-            for (uint64_t q = 0; q < m; ++q) out[x + q] = (uint8_t)((q < 4 ? lo >> (8 * q) : hi >> (8 * (q - 4))) & 255u);
-        }
-    }
-}
-
-// KVR_GATHER_REC: one wave per live record (grid-stride over records): the record's source and
+// one wave per live record (grid-stride over records): the record's source and
 // output range come straight from the dense live list (two dependent loads instead of the block
 // search's four); the output's 16-B aligned body moves as 16 B per lane (five source dwords
 // funnel-shifted), the unaligned head and tail bytes one per lane.  A long record loops 4 KiB at

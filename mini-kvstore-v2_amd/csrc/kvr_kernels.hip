@@ -4,9 +4,9 @@
  *   k_link     one workgroup: verify every stripe's speculated entry against its predecessor's
  *              exit, pick the first error in (segment, offset) order (engine.rs:55-56) and
  *              list the stripes that must be re-walked from their true entry.
- *   k_tsum / k_tscan / k_compact
- *              exclusive scan of per-tile tuple counts and a gather of the pool into the dense
- *              output in (segment, offset) order, with per-record CRC verification.
+ *   k_compact_s
+ *              one workgroup per stripe: the gather of the pool into the dense output in
+ *              (segment, offset) order, with per-record CRC verification.
  *   k_gen_fill / k_gen_manifest
  *              device side of the synthetic generator (kvr_gen_common.h).
  */
@@ -240,141 +240,16 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
 }
 
 // ---------------------------------------------------------------------------------------
-// Scan of per-tile counts and the ordered gather pool -> out.
+// The ordered gather pool -> out.
 // ---------------------------------------------------------------------------------------
-#ifndef KVR_COMPACT16   // 1: k_compact moves 16-B halves of tuples (0: one 32-B tuple per thread)
-#define KVR_COMPACT16 1
-#endif
 constexpr int CT = 256;           // threads per compaction block
-constexpr int CPT = 1;            // tiles per thread
-constexpr int CB = CT * CPT;      // tiles per compaction block
-
-__global__ __launch_bounds__(CT) void k_tsum(const TileRes *__restrict__ tres, uint32_t n_tiles,
-                                             uint64_t *__restrict__ bsum, const LinkResult *__restrict__ link) {
-    if (link->status != 0) return;
-    __shared__ uint64_t red[CT];
-    const uint32_t t0 = blockIdx.x * CB + threadIdx.x * CPT;
-    uint64_t s = 0;
-    for (int i = 0; i < CPT; ++i) if (t0 + i < n_tiles) s += tres[t0 + i].count;
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int d = CT / 2; d > 0; d >>= 1) {
-        if (threadIdx.x < d) red[threadIdx.x] += red[threadIdx.x + d];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) bsum[blockIdx.x] = red[0];
-}
-
-__global__ __launch_bounds__(1024) void k_tscan(uint64_t *__restrict__ bsum, uint32_t nb, Counters *ctr,
-                                                const LinkResult *__restrict__ link) {
-    if (link->status != 0) return;
-    __shared__ uint64_t sh[1024];
-    uint64_t carry = 0;
-    for (uint32_t base = 0; base < nb; base += 1024) {
-        const uint32_t i = base + threadIdx.x;
-        const uint64_t v = i < nb ? bsum[i] : 0ull;
-        sh[threadIdx.x] = v;
-        __syncthreads();
-        for (int d = 1; d < 1024; d <<= 1) {
-            const uint64_t o = threadIdx.x >= (uint32_t)d ? sh[threadIdx.x - d] : 0ull;
-            __syncthreads();
-            sh[threadIdx.x] += o;
-            __syncthreads();
-        }
-        if (i < nb) bsum[i] = carry + sh[threadIdx.x] - v;   // exclusive
-        const uint64_t tot = sh[1023];
-        __syncthreads();
-        carry += tot;
-    }
-    if (threadIdx.x == 0) ctr->total_tuples = carry;
-}
-
-__global__ __launch_bounds__(CT) void k_compact(const TileRes *__restrict__ tres, uint32_t n_tiles,
-                                                const uint64_t *__restrict__ bsum,
-                                                const kvr_tuple *__restrict__ pool, uint64_t pool_cap,
-                                                kvr_tuple *__restrict__ out, uint64_t out_cap,
-                                                const uint32_t *__restrict__ expected, uint64_t n_expected,
-                                                Counters *ctr, const LinkResult *__restrict__ link) {
-    if (link->status != 0 || ctr->overflow) return;
-    __shared__ uint64_t off[CB + 1];
-    __shared__ uint64_t part[CT];
-    const uint32_t tb = blockIdx.x * CB;
-    uint64_t loc[CPT];
-    uint64_t s = 0;
-    for (int i = 0; i < CPT; ++i) {
-        const uint32_t t = tb + threadIdx.x * CPT + i;
-        loc[i] = s;
-        s += t < n_tiles ? tres[t].count : 0u;
-    }
-    part[threadIdx.x] = s;
-    __syncthreads();
-    for (int d = 1; d < CT; d <<= 1) {
-        const uint64_t o = threadIdx.x >= (uint32_t)d ? part[threadIdx.x - d] : 0ull;
-        __syncthreads();
-        part[threadIdx.x] += o;
-        __syncthreads();
-    }
-    const uint64_t base = bsum[blockIdx.x] + part[threadIdx.x] - s;
-    for (int i = 0; i < CPT; ++i) off[threadIdx.x * CPT + i] = base + loc[i];
-    __syncthreads();
-    // every thread moves whole 32-B tuples: tuple k of the block lives in the tile whose
-    // local offset range holds k (binary search over the block's CB tile offsets in LDS)
-    const int lane = threadIdx.x & 63;
-    const uint64_t b0 = off[0];
-    const uint32_t nt = min((uint32_t)CB, n_tiles - tb);
-    const uint64_t btotal = (tb + nt - 1 < n_tiles ? off[nt - 1] + tres[tb + nt - 1].count : b0) - b0;
-    uint32_t fails = 0;
-#if KVR_COMPACT16
-    // 16-B items: thread k2 moves half k2 & 1 of tuple k2 >> 1, so a wave's loads and stores are
-    // 1 KiB contiguous; the second half holds val_len, crc32, key_tag, op and flags, so its thread
-    // also does the expected-CRC check
-    for (uint64_t k2 = threadIdx.x; k2 < 2 * btotal; k2 += CT) {
-        const uint64_t k = k2 >> 1;
-        const uint32_t half = (uint32_t)k2 & 1u;
-        uint32_t lo_i = 0, hi_i = nt - 1;       // last tile i with off[i] - b0 <= k
-        while (lo_i < hi_i) {
-            const uint32_t mid = (lo_i + hi_i + 1) >> 1;
-            if (off[mid] - b0 <= k) lo_i = mid; else hi_i = mid - 1;
-        }
-        const uint64_t o = b0 + k;
-        const TileRes &tr = tres[tb + lo_i];
-        const uint64_t r = o - off[lo_i];
-        const uint64_t src = r < tr.count1 ? tr.pool_off + r : tr.pool_off2 + (r - tr.count1);
-        if (src >= pool_cap) continue;
-        uint4 v = reinterpret_cast<const uint4 *>(pool + src)[half];
-        if (half && expected && o < n_expected && (v.w & 255u) == 0u) {   // a SET: op in byte 0 of w
-            v.w |= KVR_TF_VERIFIED << 8;
-            if (expected[o] != v.y) { v.w |= KVR_TF_CRC_FAIL << 8; ++fails; }
-        }
-        if (o < out_cap) reinterpret_cast<uint4 *>(out + o)[half] = v;
-    }
-#else
-    for (uint64_t k = threadIdx.x; k < btotal; k += CT) {
-        uint32_t lo_i = 0, hi_i = nt - 1;       // last tile i with off[i] - b0 <= k
-        while (lo_i < hi_i) {
-            const uint32_t mid = (lo_i + hi_i + 1) >> 1;
-            if (off[mid] - b0 <= k) lo_i = mid; else hi_i = mid - 1;
-        }
-        const uint64_t o = b0 + k;
-        const TileRes &tr = tres[tb + lo_i];
-        const uint64_t r = o - off[lo_i];                    // the tuple's index in its tile
-        const uint64_t src = r < tr.count1 ? tr.pool_off + r : tr.pool_off2 + (r - tr.count1);
-        if (src >= pool_cap) continue;
-        kvr_tuple tp = pool[src];
-        if (expected && o < n_expected && tp.op == 0) {
-            tp.flags |= KVR_TF_VERIFIED;
-            if (expected[o] != tp.crc32) { tp.flags |= KVR_TF_CRC_FAIL; ++fails; }
-        }
-        if (o < out_cap) out[o] = tp;
-    }
-#endif
-    for (int d = 32; d >= 1; d >>= 1) fails += __shfl_xor(fails, d, 64);
-    if (lane == 0 && fails) atomicAdd(&ctr->crc_fail, (unsigned long long)fails);
-}
+constexpr int CB = CT;            // tiles per chunk of k_compact_s
 
 // One workgroup per stripe (the stripe's output offset from k_link, so no separate scan of the
-// tile counts): the stripe's tiles in chunks of CB, each chunk's tile offsets scanned in LDS,
-// its tuples moved as 16-B halves (see k_compact) with the expected-CRC check.
+// tile counts): the stripe's tiles in chunks of CB, each chunk's tile offsets scanned in LDS.
+// Thread k2 moves half k2 & 1 of tuple k2 >> 1 as one 16-B load and store, so a wave's loads and
+// stores are 1 KiB contiguous; the second half holds val_len, crc32, key_tag, op and flags, so
+// its thread also does the expected-CRC check.
 __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ segs, const StripeDesc *__restrict__ stripes,
                                                   const uint64_t *__restrict__ soff, const TileRes *__restrict__ tres,
                                                   const kvr_tuple *__restrict__ pool, uint64_t pool_cap,

@@ -92,20 +92,11 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #ifndef KVR_LANEFRAME   // 1: lane-parallel framing (0: the exact scalar hop loop for every record)
 #define KVR_LANEFRAME 1
 #endif
-#ifndef KVR_TREE   // 1: the lane-parallel framing also predicts with two recent lengths (tree rounds;
-#define KVR_TREE 0     // measured slower: cfg4 2.259 vs 1.964 ms, a tree round's VALU outweighs the hops)
-#endif
-#ifndef KVR_WINPF   // 1: the next tile's first stride-round window is loaded before this tile's CRC phase
-#define KVR_WINPF 0    // (measured slower: cfg2 1.512-1.518 vs 1.440-1.486 ms, cfg4 1.953 vs 1.909)
-#endif
 #ifndef KVR_TOPWAIT   // 1: wait for the tile's load at the top of the loop (0: where its registers are
 #define KVR_TOPWAIT 1   // first read, so framing that reads only memory windows runs under the load)
 #endif
 #ifndef KVR_UNIFOLD   // 1: a stride round of equal SETs folds its long values into the units by arithmetic
 #define KVR_UNIFOLD 1
-#endif
-#ifndef KVR_ROUNDS   // lane-parallel rounds a tile at most (the scalar hop loop takes the rest)
-#define KVR_ROUNDS 1
 #endif
 #ifndef KVR_FAST_BACKOFF   // tiles the scalar hop loop keeps after a lane-parallel round found < 3 records
 #define KVR_FAST_BACKOFF 4
@@ -707,18 +698,12 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
     }
     uint64_t err_pos = NONE, err_aux = 0;
     uint32_t err_kind = 0, total = 0;
-    uint32_t stride = 0, stride2 = 0, fast_skip = 0;   // lane-parallel framing: the two recent record lengths,
-                                                       // tiles left to skip
+    uint32_t stride = 0, fast_skip = 0;           // lane-parallel framing: the last record length, tiles
+                                                  // left to the scalar hop loop
     uint32_t carry = 0, c_state = 0;              // 1: a long value crosses the tile start (c_state: its register);
     uint64_t c_vb = 0, c_ve = 0;                  // 2: pending (its value starts in a later tile)
     uint32_t c_slot = 0;
 
-    // KVR_WINPF: the decode window of the next tile's first stride round, loaded a tile ahead (its
-    // latency then runs under this tile's CRC phase), and the prediction it was loaded for
-    uint32_t pw[WINW];
-    bool pw_ok = false;
-    int32_t pw_cur = 0;
-    uint32_t pw_L = 0;
     uint32_t w[UW];     // this lane's unit of the tile (the next tile's load is issued as soon as the
     bool loaded = false;   // CRC phase is done with these registers, see the end of the loop body)
     uint32_t k = sd.t_begin;
@@ -944,54 +929,29 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             if (KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
 #if KVR_LANEFRAME
             if (!huge && p < vhi_r && fast_skip == 0u) {
-                // ---- lane-parallel framing: length prediction, verified ------------------------
-                // Lane j decodes the record that would start at a predicted position, from a window
-                // of the segment bytes (opcode, key length, value length, every engine.rs framing
-                // check), and computes where its successor starts.  Lane 0's position is exact; a
-                // lane's is exact if the records before it on its prediction path were valid and
-                // had the predicted lengths.  Two predictions:
-                //   stride  one recent length L: lane j at cur + j L (a store of equal-sized records
-                //           takes every record of the tile in one round); the first lane whose
-                //           successor is not the next prediction ends the round;
-                //   tree    two recent lengths L, L2 (say SETs and DELs of fixed-size keys and
-                //           values): lane n < 63 is node n of a binary tree of depth 6 in heap order,
-                //           at cur + (the lengths on its path), branch 0 = L, 1 = L2; the chain is
-                //           the path from the root that follows each record's actual length, up to
-                //           six records a round.
-                // The round's chain ends at record f (broken, or its successor unpredicted), whose
-                // own successor is exact, so the next round predicts from there.  A broken record,
-                // or rounds that find fewer than three records, leave the rest of the tile to the
-                // exact scalar hop loop below.
+                // ---- lane-parallel framing: stride prediction, verified --------------------------
+                // Lane j decodes the record that would start at cur + j L (L = the last record's
+                // length) from a window of the segment bytes: opcode, key length, value length, every
+                // engine.rs framing check, and where its successor starts.  Lane 0's position is
+                // exact; lane j's is exact if records 0 .. j-1 were valid and L long.  The first lane
+                // whose record is broken or whose successor is not the next prediction ends the
+                // round (record f): the records up to f are the exact chain, and f's own successor
+                // is exact.  A store of equal-sized records takes every record of the tile in one
+                // round.  One round a tile (a loop here made the compiler spill and reload much of
+                // the stripe state every tile): a broken record, or a round that found fewer than
+                // three records, leaves the rest of the tile to the exact scalar hop loop below.
                 const int32_t vhiT = (int32_t)vhi_r, remT = (int32_t)rem;
                 int32_t cur = (int32_t)p;
-                uint32_t L = stride, L2 = stride2;
-                // (KVR_ROUNDS = 1: one round a tile, the scalar loop takes any rest: no loop here, whose
-                // header made the compiler spill and reload much of the stripe state every tile)
-#if KVR_ROUNDS == 1
-                if (cur < vhiT) do {
-#else
-#pragma unroll 1
-                for (int round = 0; round < KVR_ROUNDS && cur < vhiT; ++round) {
-#endif
+                uint32_t L = stride;
+                do {
                     const bool one = L == 0u || L >= (uint32_t)TILE;   // no usable stride: lane 0 only
-                    const bool tree = KVR_TREE && !one && L2 != 0u && L2 != L && L2 < (uint32_t)TILE;
-                    // tree node n = lane: depth d = floor(log2(n + 1)), path bits = n + 1 below its top
-                    // bit (1 = the L2 branch), tb of them set
-                    const uint32_t nd = (uint32_t)lane + 1u, td = 31u - (uint32_t)__builtin_clz(nd);
-                    const uint32_t tb = (uint32_t)__builtin_popcount(nd ^ (1u << td));
-                    const int32_t c = cur + (one ? 0 : tree ? (int32_t)((td - tb) * L + tb * L2) : lane * (int32_t)L);
-                    const bool act = lane == 0 || (!one && (!tree || lane < 63) && c < vhiT);
+                    const int32_t c = cur + (one ? 0 : lane * (int32_t)L);
+                    const bool act = lane == 0 || (!one && c < vhiT);
                     const int32_t a = c & ~3;
                     const uint32_t s = (uint32_t)c & 3u;
                     uint32_t win[WINW];
-                    if (KVR_WINPF && pw_ok && !one && !tree && cur == pw_cur && L == pw_L) {
 #pragma unroll
-                        for (int i = 0; i < WINW; ++i) win[i] = pw[i];
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < WINW; ++i) win[i] = act ? ts.w32a(a + 4 * i) : 0u;
-                    }
-                    pw_ok = false;
+                    for (int i = 0; i < WINW; ++i) win[i] = act ? ts.w32a(a + 4 * i) : 0u;
                     const uint32_t x0 = __builtin_amdgcn_alignbyte(win[1], win[0], s);
                     const uint32_t x1 = __builtin_amdgcn_alignbyte(win[2], win[1], s);
                     const uint32_t op = x0 & 255u, klen = (x0 >> 8) | (x1 << 24);
@@ -1023,46 +983,21 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const uint32_t vb = e + 4u;
                     ok = ok && (!need_v || vlen <= (uint32_t)remT - vb);
                     const uint32_t nx = op == 1u ? e : vb + vlen;
-                    const uint64_t actm = __ballot(act);
-                    int f;                           // the round's last chain record (a lane)
-                    bool okf;
-                    uint32_t n_on;                   // records on the chain (f's only if valid)
-                    uint64_t onm = 0;                // tree: the chain's lanes
-                    if (!tree) {
-                        // the first lane whose record is broken or whose successor is not the next
-                        // prediction (the last active lane's successor is unconstrained)
-                        const int n = (int)__builtin_popcountll(actm);
-                        const bool mis = act && (!ok || (lane < n - 1 && nx != (uint32_t)(c + (int32_t)L)));
-                        const uint64_t mm = __ballot(mis);
-                        f = mm ? (int)__builtin_ctzll(mm) : n - 1;
-                        okf = rl32(ok ? 1u : 0u, f) != 0u;
-                        n_on = okf ? (uint32_t)f + 1u : (uint32_t)f;
-                    } else {
-                        // follow each record's length down the tree: go = 1 (L) or 2 (L2) per node
-                        const uint32_t ln = nx - (uint32_t)c;
-                        const uint32_t go = ok ? (ln == L ? 1u : (ln == L2 ? 2u : 0u)) : 0u;
-                        int nn = 0;
-                        onm = 1ull;
-#pragma unroll 1
-                        for (int d = 0; d < 5; ++d) {
-                            const uint32_t g = rl32(go, nn);
-                            const int ch = 2 * nn + (int)g;
-                            if (g == 0u || !((actm >> ch) & 1ull)) break;
-                            nn = ch;
-                            onm |= 1ull << nn;
-                        }
-                        f = nn;
-                        okf = rl32(ok ? 1u : 0u, f) != 0u;
-                        if (!okf) onm &= ~(1ull << f);
-                        n_on = (uint32_t)__builtin_popcountll(onm);
-                    }
+                    // the first lane whose record is broken or whose successor is not the next
+                    // prediction (the last active lane's successor is unconstrained)
+                    const int n = (int)__builtin_popcountll(__ballot(act));
+                    const bool mis = act && (!ok || (lane < n - 1 && nx != (uint32_t)(c + (int32_t)L)));
+                    const uint64_t mm = __ballot(mis);
+                    const int f = mm ? (int)__builtin_ctzll(mm) : n - 1;   // the round's last chain record
+                    const bool okf = rl32(ok ? 1u : 0u, f) != 0u;
+                    const uint32_t n_on = okf ? (uint32_t)f + 1u : (uint32_t)f;   // records on the chain
                     const uint32_t cf = rl32((uint32_t)c, f);
                     if (n_on) {
-                        // the walked records: rank rk = its index in the round's chain (the lane in
-                        // a stride round, the tree depth in a tree round); lane order is position order
+                        // the walked records: lane j < n_on emits record nrec + j (lane order is
+                        // position order)
                         if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
-                        const bool on = tree ? ((onm >> lane) & 1ull) != 0ull : (uint32_t)lane < n_on;
-                        const uint32_t rk = tree ? td : (uint32_t)lane;
+                        const bool on = (uint32_t)lane < n_on;
+                        const uint32_t rk = (uint32_t)lane;
                         const uint32_t slot0 = claim(n_on);
                         // one key length for the batch (lane 0's, ku): no per-lane byte masks
                         const bool kuni = __ballot(on && klen != ku) == 0ull && ku <= 4u * KEYW;
@@ -1109,7 +1044,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                         const uint64_t lvm = __ballot(lv);
                         // a round of SETs of one key and one value length (longer than a unit)
                         const uint32_t vu = rl32(vlen, 0);
-                        const bool vuni = KVR_UNIFOLD && !tree && !one && vu > (uint32_t)SC &&
+                        const bool vuni = KVR_UNIFOLD && !one && vu > (uint32_t)SC &&
                                           __ballot(on && (op != 0u || vlen != vu || klen != ku)) == 0ull;
                         if (lvm && !(KVR_ABLATE & 32)) {
                             uint32_t lmark = 0;
@@ -1127,7 +1062,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                             if (vbl >= (uint32_t)TILE) {
                                 n_carry = 2; n_vb = (uint64_t)(lo + (int64_t)vbl);
                                 n_ve = (uint64_t)(lo + (int64_t)vbl + rl32(vlen, jl));
-                                n_ref = nrec + (tree ? 31u - (uint32_t)__builtin_clz((uint32_t)jl + 1u) : (uint32_t)jl);
+                                n_ref = nrec + (uint32_t)jl;
                                 n_abs = false;
                             }
                             if (vuni) fold_uniform(cur + 9 + (int32_t)ku, (int32_t)L, n_on, (int32_t)vu, nrec);
@@ -1148,23 +1083,15 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     }
                     if (!okf) { cur = (int32_t)cf; break; }    // a broken record at cf: the exact loop reports it
                     const uint32_t nf = rl32(nx, f);
-                    // record f's length predicts the next round, with the other recent length
-                    const uint32_t lf = nf - cf;
-                    if (!KVR_TREE) L = lf;
-                    else if (lf != L && lf != L2) { L2 = L; L = lf; }
+                    L = nf - cf;                               // record f's length predicts the next tile
                     cur = (int32_t)nf;
                     if (err_rec != N32) break;
                     if (!one && n_on < 3u && cur < vhiT) {      // lengths vary: the scalar loop is cheaper
                         fast_skip = KVR_FAST_BACKOFF;
                         break;
                     }
-#if KVR_ROUNDS == 1
                 } while (0);
-#else
-                }
-#endif
                 stride = L;
-                if (KVR_TREE) stride2 = L2;
                 p = cur;
             } else if (fast_skip) {
                 --fast_skip;
@@ -1323,28 +1250,9 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
         // the stripe goes on past this tile (a value running past its end is carried on)
         const bool need_next = err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry || out);
         KVR_STAMP(2);
-        // the word of a value end's partial tail, for the finalize (issued first: the window loads
-        // below then return after it, and the finalize's wait for it does not wait for them)
+        // the word of a value end's partial tail, for the finalize (its latency runs under the unit loop)
         uint32_t wm = 0;
         if (!(KVR_ABLATE & 2) && any_long && m != 0 && m < SC) wm = ts.w32a(us + 4 * (m >> 2));
-        // the next tile's first stride round, predicted now (its entry is this tile's exit): its
-        // window is loaded here, so that the latency runs under this tile's CRC phase
-        pw_ok = false;
-        if (KVR_WINPF && walk && err_pos == NONE && tile_exit != ERRP && k + 1 < sd.t_end && k + 1 < sg.n_tiles &&
-            fast_skip == 0u && stride != 0u && stride < (uint32_t)TILE && rem - TILE <= 0x7FFFFFFFll) {
-            const int64_t cur1 = (int64_t)tile_exit - (lo + TILE);
-            const int64_t vhi1 = (rem - TILE) < TILE ? (rem - TILE) : TILE;
-            if (cur1 >= 0 && cur1 < vhi1) {
-                const TileSeg ts1 = tile_seg(abase, sg.base, d0, len, k + 1);
-                const int32_t c1 = (int32_t)cur1 + lane * (int32_t)stride;
-                const bool act1 = lane == 0 || c1 < (int32_t)vhi1;
-#pragma unroll
-                for (int i = 0; i < WINW; ++i) pw[i] = act1 ? ts1.w32a((c1 & ~3) + 4 * i) : 0u;
-                pw_ok = true;
-                pw_cur = (int32_t)cur1;
-                pw_L = stride;
-            }
-        }
         // ---- C. CRC of long values --------------------------------------------------------
         if (!(KVR_ABLATE & 2) && any_long) {
             KVR_STAMP(8);
