@@ -100,6 +100,11 @@ struct kvr_ctx {
     DevBuf<StripeRes> sres;
     DevBuf<TileRes> tres;
     DevBuf<kvr_tuple> pool, dense;
+    // key prefixes for the fold: k_replay writes them per pool slot when kout is set, k_compact_s
+    // moves them into kout (parallel to the output tuples); compact_front points kout at ckeys
+    DevBuf<uint4> kpool, ckeys;
+    uint4 *kout = nullptr;
+    bool ckeys_ok = false;                 // ckeys holds the prefixes of ctup[0, c_nt)
     DevBuf<RedoEnt> redo;
     DevBuf<LinkResult> link;
     DevBuf<Counters> ctr;
@@ -332,6 +337,7 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->lcbuf.release();
     c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->soff.release();
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
+    c->kpool.release(); c->ckeys.release();
     c->ctup.release(); c->lout.release(); c->fent.release(); c->flist.release(); c->fcnt.release(); c->fsz.release();
     c->cslot.release(); c->cflag.release(); c->islots.release(); c->ing.release(); c->hpart.release(); c->hreg.release();
     c->koff.release(); c->klen.release(); c->kbuf.release();
@@ -439,6 +445,7 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
     if (rc != KVR_ENOMEM || !c->pool_need) return rc;
     need = c->pool_need;   // the pool this input needs exceeds 32-bit slots: batch it
     c->pool_need = 0;
+    c->kout = nullptr;     // (batches write their own outputs: no key prefixes, the fold reads keys)
     c->pool_hint = 0;
     return replay_batched(c, segs, n, flags, expected, n_expected, out, cap, n_out, err, need);
 }
@@ -571,6 +578,11 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             return KVR_ENOMEM;
         }
         if (c->pool.ensure(pool_cap + POOL_SLACK)) return KVR_ENOMEM;
+        uint4 *kp = nullptr;               // key prefixes (calls that fold, device output only)
+        if (c->kout && (flags & KVR_OUT_ON_DEVICE)) {
+            if (c->kpool.ensure(pool_cap + POOL_SLACK)) return KVR_ENOMEM;
+            kp = c->kpool.p;
+        }
         kvr_tuple *d_out;
         uint64_t out_cap;
         if (flags & KVR_OUT_ON_DEVICE) {
@@ -586,7 +598,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         auto launch_compact = [&]() {
             hipLaunchKernelGGL(k_compact_s, dim3(n_stripes), dim3(CT), 0, st, c->segs.p, c->stripes.p, c->soff.p,
                                c->tres.p, c->pool.p, pool_cap, d_out, out_cap, d_exp,
-                               (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p);
+                               (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p, kp, kp ? c->kout : nullptr);
         };
         // counters and link result start at zero (the last successful call cleared them behind its
         // results, so this memset usually runs only on a context's first call or after an error)
@@ -594,7 +606,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         c->lc_zero = false;
         HIPCHK(hipEventRecord(c->ev[0], st));
         hipLaunchKernelGGL(KR_KERNEL, dim3((n_stripes + KR_WPB - 1) / KR_WPB), dim3(KR_RT), 0, st, c->segs.p, c->stripes.p, n_stripes,
-                           c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, pool_chunk);
+                           c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, pool_chunk, kp);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[1], st));
         hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
@@ -642,7 +654,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         while (c->h_link->status == 3 && guard++ < n_stripes + 4) {
             hipLaunchKernelGGL(k_rewalk, dim3((std::max(1u, std::min(c->h_link->n_redo, (uint32_t)c->redo.n)) + KR_WPB - 1) / KR_WPB), dim3(KR_RT),
                                0, st, c->segs.p, c->stripes.p, n_stripes, c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p,
-                               tb, c->redo.p, c->link.p, pool_chunk);
+                               tb, c->redo.p, c->link.p, pool_chunk, kp);
             hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes,
                                c->sres.p, c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p, (uint32_t)KR_TILE,
                                c->soff.p, c->ctr.p);
@@ -748,13 +760,18 @@ static int compact_front(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t
     if (n == 0) return KVR_OK;
     // 1. replay into context-resident tuples; the segment bytes stay in HBM (c->segs)
     size_t nt = 0;
-    if (c->ctup.ensure(bytes_in / 64 + 1024)) return KVR_ENOMEM;
+    c->ckeys_ok = false;
+    if (c->ctup.ensure(bytes_in / 64 + 1024) || c->ckeys.ensure(c->ctup.n)) return KVR_ENOMEM;
     const uint32_t rflags = (flags & KVR_SEGS_ON_DEVICE) | KVR_OUT_ON_DEVICE;
+    c->kout = c->ckeys.p;   // the tuples' key prefixes alongside them (k_fold_claim / k_fold_verify)
     int rc = kvr_replay(c, segs, n, rflags, nullptr, 0, c->ctup.p, c->ctup.n, &nt, err);
     if (rc == KVR_CAPACITY) {
-        if (c->ctup.ensure(nt)) return KVR_ENOMEM;
+        if (c->ctup.ensure(nt) || c->ckeys.ensure(c->ctup.n)) { c->kout = nullptr; return KVR_ENOMEM; }
+        c->kout = c->ckeys.p;
         rc = kvr_replay(c, segs, n, rflags, nullptr, 0, c->ctup.p, c->ctup.n, &nt, err);
     }
+    c->ckeys_ok = c->kout != nullptr;   // (a batched replay dropped them)
+    c->kout = nullptr;
     if (rc != KVR_OK) return rc;
     cs->ms_replay = c->stats.ms_total;
     cs->n_tuples = nt;
@@ -814,18 +831,20 @@ static int fold_launch(kvr_ctx *c, size_t nt, bool deferred) {
     }
     HIPCHK(hipGetLastError());
     static const bool pre = getenv("KVR_CLAIM_PRELOAD") && atoi(getenv("KVR_CLAIM_PRELOAD"));   // timing knob
+    static const bool nokeys = getenv("KVR_FOLD_SEGKEYS") != nullptr;   // test/timing knob: keys from the segments
+    const uint4 *kd = (c->ckeys_ok && !nokeys) ? c->ckeys.p : nullptr;
     // one probe round over m tuples (list: null = all, in round 0); counters cnt[0] tuples left for
     // the next round, cnt[1] claims that found the table full
     auto round = [&](uint64_t m, const uint32_t *n_dev, const uint32_t *list, uint32_t *next, uint32_t *cnt) {
         const uint32_t g = (uint32_t)((m + 255) / 256);
         if (pre)
             hipLaunchKernelGGL(k_fold_claim<true>, dim3(g), dim3(256), 0, st, c->ctup.p, m, n_dev, list, c->segs.p,
-                               c->fent.p, c->fsz.p, c->cslot.p, cnt + 1);
+                               c->fent.p, c->fsz.p, c->cslot.p, cnt + 1, kd);
         else
             hipLaunchKernelGGL(k_fold_claim<false>, dim3(g), dim3(256), 0, st, c->ctup.p, m, n_dev, list, c->segs.p,
-                               c->fent.p, c->fsz.p, c->cslot.p, cnt + 1);
+                               c->fent.p, c->fsz.p, c->cslot.p, cnt + 1, kd);
         hipLaunchKernelGGL(k_fold_verify, dim3(g), dim3(256), 0, st, c->ctup.p, m, n_dev, list, c->segs.p, c->fent.p,
-                           c->fsz.p, c->cslot.p, next, cnt);
+                           c->fsz.p, c->cslot.p, next, cnt, kd);
     };
 again:
     hipLaunchKernelGGL(k_fent_clear, dim3(fold_grid(c)), dim3(256), 0, st, c->fent.p, c->fsz.p);

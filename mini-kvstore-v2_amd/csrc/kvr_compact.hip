@@ -230,11 +230,13 @@ __global__ void k_fent_clear(FoldEnt *__restrict__ ent, const uint32_t *__restri
 // here) or holds its tag (verified by k_fold_verify)
 // (n_dev: a later round launched before the host knows its size reads it here; n caps it at the
 // grid, and the host checks afterwards that no round was larger)
+// (kd: the tuples' key prefixes, which k_replay wrote when the call asked for them: one sequential
+// 16-B read instead of reading the key in the segment bytes at random; null: from the segments)
 template <bool PRE>
 __global__ void k_fold_claim(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ n_dev,
                              const uint32_t *__restrict__ list, const SegDesc *__restrict__ segs,
                              FoldEnt *__restrict__ ent, const uint32_t *__restrict__ fsz,
-                             uint32_t *__restrict__ slot, uint32_t *__restrict__ full) {
+                             uint32_t *__restrict__ slot, uint32_t *__restrict__ full, const uint4 *__restrict__ kd) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (n_dev && *n_dev < n) n = *n_dev;
     if (g >= n) return;
@@ -246,13 +248,18 @@ __global__ void k_fold_claim(const kvr_tuple *__restrict__ tup, uint64_t n, cons
     uint32_t h = list ? slot[i] : (ht_mix(t.key_tag) & mask);
     const unsigned long long mine = ((unsigned long long)t.key_tag << 32) | i;
     uint32_t w[4];   // PRE: the key prefix, loaded alongside the probe (only a claimer stores it)
-    if (PRE) key_prefix16(segs[t.seg_idx], t, w);
+    if (PRE && !kd) key_prefix16(segs[t.seg_idx], t, w);
     for (uint32_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
         unsigned long long v = __hip_atomic_load(&ent[h].tagrep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (v == FE_EMPTY) {
             v = atomicCAS(&ent[h].tagrep, FE_EMPTY, mine);
             if (v == FE_EMPTY) {   // claimed: this tuple represents its key in entry h
-                if (!PRE) key_prefix16(segs[t.seg_idx], t, w);
+                if (kd) {
+                    const uint4 q = kd[i];
+                    w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
+                } else if (!PRE) {
+                    key_prefix16(segs[t.seg_idx], t, w);
+                }
                 ent[h].best = ~i;   // nobody else writes best during the claims
                 ent[h].klen = t.key_len;
                 *reinterpret_cast<uint4 *>(ent[h].key) = make_uint4(w[0], w[1], w[2], w[3]);
@@ -273,7 +280,8 @@ __global__ void k_fold_claim(const kvr_tuple *__restrict__ tup, uint64_t n, cons
 __global__ void k_fold_verify(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ n_dev,
                               const uint32_t *__restrict__ list, const SegDesc *__restrict__ segs,
                               FoldEnt *__restrict__ ent, const uint32_t *__restrict__ fsz,
-                              uint32_t *__restrict__ slot, uint32_t *__restrict__ next, uint32_t *__restrict__ n_next) {
+                              uint32_t *__restrict__ slot, uint32_t *__restrict__ next, uint32_t *__restrict__ n_next,
+                              const uint4 *__restrict__ kd) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (n_dev && *n_dev < n) n = *n_dev;
     if (g >= n) return;
@@ -290,7 +298,12 @@ __global__ void k_fold_verify(const kvr_tuple *__restrict__ tup, uint64_t n, con
         if (a.w == t.key_len) {
             const uint4 k = reinterpret_cast<const uint4 *>(&ent[h])[1];
             uint32_t w[4];
-            key_prefix16(segs[t.seg_idx], t, w);
+            if (kd) {
+                const uint4 q = kd[i];
+                w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
+            } else {
+                key_prefix16(segs[t.seg_idx], t, w);
+            }
             same = ((w[0] ^ k.x) | (w[1] ^ k.y) | (w[2] ^ k.z) | (w[3] ^ k.w)) == 0u;
             if (same && t.key_len > 16u)
                 same = bytes_eq(key_ptr(segs, tup[rep]) + 16, key_ptr(segs, t) + 16, t.key_len - 16u);

@@ -249,13 +249,15 @@ constexpr int CB = CT;            // tiles per chunk of k_compact_s
 // tile counts): the stripe's tiles in chunks of CB, each chunk's tile offsets scanned in LDS.
 // Thread k2 moves half k2 & 1 of tuple k2 >> 1 as one 16-B load and store, so a wave's loads and
 // stores are 1 KiB contiguous; the second half holds val_len, crc32, key_tag, op and flags, so
-// its thread also does the expected-CRC check.
+// its thread also does the expected-CRC check, and moves the key prefix when the call keeps one
+// (kpool -> kout, the fold's keys).
 __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ segs, const StripeDesc *__restrict__ stripes,
                                                   const uint64_t *__restrict__ soff, const TileRes *__restrict__ tres,
                                                   const kvr_tuple *__restrict__ pool, uint64_t pool_cap,
                                                   kvr_tuple *__restrict__ out, uint64_t out_cap,
                                                   const uint32_t *__restrict__ expected, uint64_t n_expected,
-                                                  Counters *ctr, const LinkResult *__restrict__ link) {
+                                                  Counters *ctr, const LinkResult *__restrict__ link,
+                                                  const uint4 *__restrict__ kpool, uint4 *__restrict__ kout) {
     if (link->status != 0 || ctr->overflow) return;
     __shared__ uint64_t off[CB + 1];
     __shared__ uint64_t part[CT];
@@ -298,7 +300,10 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
                 v.w |= KVR_TF_VERIFIED << 8;
                 if (expected[o] != v.y) { v.w |= KVR_TF_CRC_FAIL << 8; ++fails; }
             }
-            if (o < out_cap) reinterpret_cast<uint4 *>(out + o)[half] = v;
+            if (o < out_cap) {
+                reinterpret_cast<uint4 *>(out + o)[half] = v;
+                if (half && kout) kout[o] = kpool[src];
+            }
         }
         carry += ctotal;
         __syncthreads();   // (off and part are rewritten by the next chunk)

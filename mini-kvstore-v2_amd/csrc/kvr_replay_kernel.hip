@@ -513,6 +513,34 @@ __device__ inline bool plausible(const TS &ts, int64_t o) {
 // ---------------------------------------------------------------------------------------
 // records
 // ---------------------------------------------------------------------------------------
+// the first min(klen, 16) key bytes as four little-endian words, zero padded (the fold's key
+// prefix, kvr_compact.hip FoldEnt::key), from the key words x[0..4] that start sh bytes into x[0]
+__device__ __forceinline__ uint4 key_prefix_words(const uint32_t *x, uint32_t sh, uint32_t klen) {
+    uint32_t k[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t v = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);
+        const uint32_t n = klen > 4u * j ? klen - 4u * j : 0u;   // key bytes in this word
+        k[j] = n >= 4u ? v : (v & ((1u << (8u * n)) - 1u));
+    }
+    return make_uint4(k[0], k[1], k[2], k[3]);
+}
+// the same from the segment bytes at tile offset kb (o >= 0 inside the tile's resource, or any
+// segment position through single-byte reads)
+__device__ inline uint4 key_prefix_mem(const TileSeg &ts, int64_t kb, uint32_t klen) {
+    if (kb >= 0 && kb + 24 <= ts.lim) {
+        const int a = (int)kb & ~3;
+        uint32_t x[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) x[i] = ts.w32a(a + 4 * i);
+        return key_prefix_words(x, (uint32_t)kb & 3u, klen);
+    }
+    uint32_t k[4] = {0u, 0u, 0u, 0u};
+    const uint32_t m = klen < 16u ? klen : 16u;
+    for (uint32_t i = 0; i < m; ++i) k[i >> 2] |= ts.b8(kb + (int64_t)i) << (8u * (i & 3u));
+    return make_uint4(k[0], k[1], k[2], k[3]);
+}
+
 struct RecRes {          // one record's outcome on the general path
     uint32_t err, kind;  // record index of an error (N32: none) and its KVR_E_* kind
     uint64_t aux;
@@ -521,7 +549,7 @@ struct RecRes {          // one record's outcome on the general path
 // parse + emit the record at tile offset o with every engine.rs check, in engine.rs order
 // (its value, if longer than SMALL, was folded by the framing)
 __device__ inline RecRes do_record(const TileSeg &ts, const Crc &K, int64_t o, uint32_t j, uint32_t slot, uint32_t seg,
-                                   kvr_tuple *pool) {
+                                   kvr_tuple *pool, uint4 *kpool) {
     RecRes ro;
     ro.err = N32; ro.kind = 0; ro.aux = 0;
     const int64_t rem = (int64_t)ts.len - ts.lo;
@@ -555,6 +583,7 @@ __device__ inline RecRes do_record(const TileSeg &ts, const Crc &K, int64_t o, u
         if (vlen <= (uint64_t)SMALL) t.crc32 = ~crc_long(ts, ~0u, q + 4, vlen, K);
     }
     pool[slot] = t;
+    if (kpool) kpool[slot] = key_prefix_mem(ts, kb, (uint32_t)klen);
     return ro;
 }
 
@@ -626,7 +655,8 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                                             StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
                                             kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
                                             Tables tb, const RedoEnt *__restrict__ redo,
-                                            const LinkResult *__restrict__ link, uint32_t pool_chunk) {
+                                            const LinkResult *__restrict__ link, uint32_t pool_chunk,
+                                            uint4 *__restrict__ kpool) {
     constexpr bool redo_mode = REDO;
     __shared__ Smem S;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1035,6 +1065,8 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                                 t.flags = 0;
                                 t.reserved = 0;
                                 pool[slot0 + rk] = t;
+                                // the key prefix for the fold (only calls that fold ask for it)
+                                if (kpool) kpool[slot0 + rk] = key_prefix_words(kr, (s + 1u) & 3u, klen);
                             }
                         }
                         // long values crossing a unit boundary: marked at their first unit (a scatter
@@ -1173,7 +1205,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
                 if (!(KVR_ABLATE & 1) && myrec >= 0) {
                     if (broke && lane == (int)nb - 1) {   // the record that broke the chain: every check
-                        const RecRes r = do_record(ts, K, myrec, j, slot, sd.seg, pool);
+                        const RecRes r = do_record(ts, K, myrec, j, slot, sd.seg, pool, kpool);
                         rerr = r.err; rkind = r.kind; raux = r.aux;
                         if (r.err == N32) { rerr = j; rkind = KVR_E_VAL; }   // defensive: a break is an error
                     } else {
@@ -1212,6 +1244,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                             t.flags = 0;
                             t.reserved = 0;
                             pool[slot] = t;
+                            if (kpool) kpool[slot] = key_prefix_mem(ts, kb, klen);
                         }
                     }
                 }
@@ -1443,8 +1476,8 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                                                const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
                                                StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
                                                kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
-                                               Tables tb, uint32_t pool_chunk) {
-    replay_body<false>(segs, stripes, n_stripes, sres, tres, pool, pool_cap, ctr, tb, nullptr, nullptr, pool_chunk);
+                                               Tables tb, uint32_t pool_chunk, uint4 *__restrict__ kpool) {
+    replay_body<false>(segs, stripes, n_stripes, sres, tres, pool, pool_cap, ctr, tb, nullptr, nullptr, pool_chunk, kpool);
 }
 
 __global__ __launch_bounds__(RT) void k_rewalk(const SegDesc *__restrict__ segs,
@@ -1452,8 +1485,9 @@ __global__ __launch_bounds__(RT) void k_rewalk(const SegDesc *__restrict__ segs,
                                                StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
                                                kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
                                                Tables tb, const RedoEnt *__restrict__ redo,
-                                               const LinkResult *__restrict__ link, uint32_t pool_chunk) {
-    replay_body<true>(segs, stripes, n_stripes, sres, tres, pool, pool_cap, ctr, tb, redo, link, pool_chunk);
+                                               const LinkResult *__restrict__ link, uint32_t pool_chunk,
+                                               uint4 *__restrict__ kpool) {
+    replay_body<true>(segs, stripes, n_stripes, sres, tres, pool, pool_cap, ctr, tb, redo, link, pool_chunk, kpool);
 }
 
 }  // namespace kvr
