@@ -392,13 +392,33 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
 
 // a replay whose tuples exceed the pool's 32-bit slots (dense small records: more than about
 // 4 G records in one call) runs as consecutive batches of whole segments, each its own
-// pipeline, the tuples appended in order — the same output, errors and return codes
+// pipeline, the tuples appended in order — the same output, errors and return codes.  Host
+// segments are first copied into the arena all at once (the batches then replay them in place),
+// so that every segment stays resident and, at the end, the segment descriptors on the device
+// describe the whole input: the fold, the key arena and the compaction's gather read keys and
+// records of any batch.  Key prefixes (kout) are appended per batch like the tuples.
 static int replay_batched(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, const uint32_t *expected,
                           size_t n_expected, kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err, uint64_t need) {
     uint64_t total = 0;
     for (size_t i = 0; i < n; ++i) total += segs[i].len;
     const uint64_t parts = need / (pool_limit() / 2) + 1;
     const uint64_t budget = total / parts + 1;
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<kvr_segment> dsegs(segs, segs + n);
+    if (!(flags & KVR_SEGS_ON_DEVICE)) {
+        uint64_t arena = 256;
+        for (size_t i = 0; i < n; ++i) arena += (segs[i].len + 255) & ~255ull;
+        if (c->arena.ensure(arena)) return KVR_ENOMEM;
+        uint64_t off = 0;
+        for (size_t i = 0; i < n; ++i) {
+            dsegs[i].bytes = c->arena.p + off;
+            if (segs[i].len)
+                HIPCHK(hipMemcpyAsync(c->arena.p + off, segs[i].bytes, segs[i].len, hipMemcpyHostToDevice, c->stream));
+            off += (segs[i].len + 255) & ~255ull;
+        }
+        flags |= KVR_SEGS_ON_DEVICE;
+    }
+    uint4 *const kout = (flags & KVR_OUT_ON_DEVICE) ? c->kout : nullptr;
     size_t done = 0;
     kvr_stats sum{};
     for (size_t s0 = 0; s0 < n;) {
@@ -410,7 +430,8 @@ static int replay_batched(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_
         const size_t room = done < cap ? cap - done : 0;
         size_t nb = 0;
         kvr_error e{};
-        const int rc = kvr_replay(c, segs + s0, s1 - s0, flags, expected ? expected + e0 : nullptr,
+        c->kout = kout && room ? kout + done : nullptr;
+        const int rc = kvr_replay(c, dsegs.data() + s0, s1 - s0, flags, expected ? expected + e0 : nullptr,
                                   expected ? n_expected - e0 : 0, room ? out + done : nullptr, room, &nb, &e);
         sum.ms_total += c->stats.ms_total; sum.ms_replay += c->stats.ms_replay; sum.ms_link += c->stats.ms_link;
         sum.ms_compact += c->stats.ms_compact; sum.bytes_in += c->stats.bytes_in; sum.n_records += c->stats.n_records;
@@ -419,9 +440,10 @@ static int replay_batched(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_
         if (rc == KVR_CORRUPTED) {   // batches run in (segment, offset) order: the store's first error
             if (err) { *err = e; err->seg_idx += (uint32_t)s0; }
             c->stats = sum;
+            c->kout = kout;
             return rc;
         }
-        if (rc != KVR_OK && rc != KVR_CAPACITY) return rc;
+        if (rc != KVR_OK && rc != KVR_CAPACITY) { c->kout = kout; return rc; }
         if (s0 && !(flags & KVR_OUT_ON_DEVICE)) {   // seg_idx into the caller's segs[]
             for (size_t t = 0, m = std::min(nb, room); t < m; ++t) out[done + t].seg_idx += (uint32_t)s0;
         } else if (s0 && nb) {
@@ -432,6 +454,22 @@ static int replay_batched(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_
         done += nb;
         s0 = s1;
     }
+    c->kout = done <= cap ? kout : nullptr;   // (prefixes past the output's room were not written)
+    // the descriptors of every segment (only base and len are read after the replay), and the
+    // per-call upload caches invalidated
+    if (c->segs.ensure(n)) return KVR_ENOMEM;
+    std::vector<SegDesc> all(n);
+    for (size_t i = 0; i < n; ++i) {
+        all[i] = SegDesc{};
+        all[i].base = dsegs[i].bytes;
+        all[i].len = dsegs[i].len;
+        all[i].d0 = (uint32_t)(reinterpret_cast<uintptr_t>(dsegs[i].bytes) & 15u);
+    }
+    HIPCHK(hipMemcpyAsync(c->segs.p, all.data(), n * sizeof(SegDesc), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->up_segs_p = nullptr;
+    c->up_stripes_p = nullptr;
+    c->h_stripes_up = false;
     c->stats = sum;
     *n_out = done;
     return done > cap ? KVR_CAPACITY : KVR_OK;
@@ -445,7 +483,6 @@ int kvr_replay(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, co
     if (rc != KVR_ENOMEM || !c->pool_need) return rc;
     need = c->pool_need;   // the pool this input needs exceeds 32-bit slots: batch it
     c->pool_need = 0;
-    c->kout = nullptr;     // (batches write their own outputs: no key prefixes, the fold reads keys)
     c->pool_hint = 0;
     return replay_batched(c, segs, n, flags, expected, n_expected, out, cap, n_out, err, need);
 }
@@ -770,7 +807,7 @@ static int compact_front(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t
         c->kout = c->ckeys.p;
         rc = kvr_replay(c, segs, n, rflags, nullptr, 0, c->ctup.p, c->ctup.n, &nt, err);
     }
-    c->ckeys_ok = c->kout != nullptr;   // (a batched replay dropped them)
+    c->ckeys_ok = c->kout != nullptr;   // (a batched replay past the output capacity drops them)
     c->kout = nullptr;
     if (rc != KVR_OK) return rc;
     cs->ms_replay = c->stats.ms_total;
@@ -831,7 +868,7 @@ static int fold_launch(kvr_ctx *c, size_t nt, bool deferred) {
     }
     HIPCHK(hipGetLastError());
     static const bool pre = getenv("KVR_CLAIM_PRELOAD") && atoi(getenv("KVR_CLAIM_PRELOAD"));   // timing knob
-    static const bool nokeys = getenv("KVR_FOLD_SEGKEYS") != nullptr;   // test/timing knob: keys from the segments
+    const bool nokeys = getenv("KVR_FOLD_SEGKEYS") != nullptr;   // test/timing knob: keys from the segments
     const uint4 *kd = (c->ckeys_ok && !nokeys) ? c->ckeys.p : nullptr;
     // one probe round over m tuples (list: null = all, in round 0); counters cnt[0] tuples left for
     // the next round, cnt[1] claims that found the table full

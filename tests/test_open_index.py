@@ -155,6 +155,31 @@ def test_fold_table_redo(gctx, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("source", ["prefixes", "segments", "batched"])
+def test_fold_key_sources(gctx, monkeypatch, source):
+    """The fold compares keys through the 16-B prefixes k_replay wrote beside the tuples (the
+    default for calls that fold), or through the segment bytes (KVR_FOLD_SEGKEYS, and a replay
+    batched past the pool-slot limit, which writes no prefixes): the same live index, CRC-32
+    collisions and short keys included, and the rewrite built on it replays to the same map."""
+    segs, pairs = collision_store()
+    spec = K.GenSpec(seed=105, seg_bytes=200_000, key_space_log2=10, val_min=0, val_max=300, del_permille=300)
+    segs = segs + [K.gen_segment_cpu(spec, s)[0].tobytes() for s in range(6)]
+    want, nk, _ = expect(segs)
+    if source == "segments":
+        monkeypatch.setenv("KVR_FOLD_SEGKEYS", "1")
+    if source == "batched":
+        monkeypatch.setenv("KVR_POOL_LIMIT", "200000")
+    r = gctx.replay_live(segs)
+    assert r.status == 0 and np.array_equal(r.tuples, want)
+    idx = gctx.replay_index(segs)
+    assert np.array_equal(idx.live, want) and idx.stats.n_live == nk
+    c = gctx.compact(segs)
+    rc, t2, _ = O.replay(c.segments())
+    assert rc == 0 and len(t2) == nk
+    assert sorted(keys_of(c.segments(), t2)) == sorted(keys_of(segs, want))
+
+
+@pytest.mark.gpu
 def test_fold_table_estimate(gctx):
     """cfg-like input with many more tuples than keys: the table is sized from the HyperLogLog
     estimate (within a few percent of the true key count), not from the tuples."""
