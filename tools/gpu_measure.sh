@@ -18,6 +18,9 @@ for s in $STEPS; do
       timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread --durations=15 \
         > "$OUT/tests.log" 2>&1 || { echo "tests failed"; tail -40 "$OUT/tests.log"; exit 1; }
       tail -3 "$OUT/tests.log" ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.txt" 2>&1 || { echo "smoke failed"; tail -20 "$OUT/smoke.txt"; exit 1; }
+      tail -1 "$OUT/smoke.txt" ;;
     bench)
       timeout -k 10 300 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; tail -20 "$OUT/bench.err"; exit 1; }
       cat "$OUT/bench.json" ;;
