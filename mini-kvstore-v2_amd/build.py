@@ -100,7 +100,8 @@ VARIANTS = {
     "fin0": ["-DKVR_FIN_PRIO=0"],  # the scan + finalize chain at priority 0
     "lf0": ["-DKVR_LANEFRAME=0"],  # the scalar hop loop for every record
     "a7": ["-DKVR_ABLATE=7"],      # loads + per-tile bookkeeping only (the memory floor at 16 waves/CU)
-    "notop": ["-DKVR_TOPWAIT=0"],  # no wait for the tile's load at the loop top
+    "top": ["-DKVR_TOPWAIT=1"],    # wait for the tile's load at the loop top (round 3 default before)
+    "bo4": ["-DKVR_FAST_BACKOFF=4"],     # 4 tiles of scalar hops after a short lane-parallel round
     "nouni": ["-DKVR_UNIFOLD=0"],  # long-value views through LDS marks + lane permutes only
     "base": [],
 }

@@ -93,13 +93,13 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #define KVR_LANEFRAME 1
 #endif
 #ifndef KVR_TOPWAIT   // 1: wait for the tile's load at the top of the loop (0: where its registers are
-#define KVR_TOPWAIT 1   // first read, so framing that reads only memory windows runs under the load)
-#endif
+#define KVR_TOPWAIT 0   // first read, so the framing round's window loads go out under the tile's load;
+#endif                  // cfg2 1.326-1.332 vs 1.334-1.342 ms, cfg4 1.805-1.819 vs 1.813-1.857, medians)
 #ifndef KVR_UNIFOLD   // 1: a stride round of equal SETs folds its long values into the units by arithmetic
 #define KVR_UNIFOLD 1
 #endif
 #ifndef KVR_FAST_BACKOFF   // tiles the scalar hop loop keeps after a lane-parallel round found < 3 records
-#define KVR_FAST_BACKOFF 4
+#define KVR_FAST_BACKOFF 16   // (4: cfg4 1.80 ms; 16: 1.75 with the loop-top change, r03_topwait_backoff_ab.txt)
 #endif
 #ifndef KVR_ABLATE
 #define KVR_ABLATE 0   // diagnostic builds only: 1 skip records, 2 skip value CRC, 4 skip framing,
