@@ -90,6 +90,9 @@ for s in $STEPS; do
     pmc)
       timeout -k 10 900 bash tools/pmc.sh "$OUT/pmc" --no-cpu --no-stream --steps 2 --warmup 1 > "$OUT/pmc.txt" 2>&1 || { echo "pmc failed"; tail -20 "$OUT/pmc.txt"; exit 1; }
       cat "$OUT/pmc.txt" ;;
+    pmce)     # PMC counters of the batch ETag bench (k_etag_chunk)
+      timeout -k 10 900 bash tools/pmc.sh "$OUT/pmce" --mode etag --steps 2 --warmup 1 > "$OUT/pmce.txt" 2>&1 || { echo "pmce failed"; tail -20 "$OUT/pmce.txt"; exit 1; }
+      cat "$OUT/pmce.txt" ;;
     pmc4)     # PMC counters of the cfg4-shape bench (two record lengths, the hop loop's case)
       timeout -k 10 900 bash tools/pmc.sh "$OUT/pmc4" --config cfg4 --no-cpu --no-stream --no-open --steps 2 --warmup 1 > "$OUT/pmc4.txt" 2>&1 || { echo "pmc4 failed"; tail -20 "$OUT/pmc4.txt"; exit 1; }
       cat "$OUT/pmc4.txt" ;;
