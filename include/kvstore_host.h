@@ -76,7 +76,12 @@ int kvs_open(const char *dir, kvr_ctx *ctx, kvs_store **out, kvr_error *err, cha
  * exceeds the fold's 2^31-tuple limit (KVR_EINVAL), the host-fold path takes over:
  * kvr_replay_stream in batches, kvh_fold_parallel, kvr_index_build_host.  Both give the same index.
  * An unopenable segment k is reported (KVR_E_OPEN) only when segments 0 .. k-1 replay cleanly,
- * as engine.rs:55-57 opens the files one after the other. */
+ * as engine.rs:55-57 opens the files one after the other.
+ * Segment files must not be truncated by another process while the store is open: a mapped page
+ * past the new end of file raises SIGBUS when it is touched (later DMA re-reads, compaction).  The
+ * store itself only appends to the active file, and kvs_compact writes new files and unlinks the
+ * old ones (an unlinked file's mapping keeps its pages), so its own mappings never lose bytes;
+ * KVS_OPEN_PREAD copies the bytes and is immune to outside truncation. */
 #define KVS_OPEN_HOST_FOLD  0x1u   /* force the host-fold path                         */
 #define KVS_OPEN_NO_PIN     0x2u   /* no kvr_host_register: HIP stages the transfers    */
 #define KVS_OPEN_PREAD      0x4u   /* read the files into an arena instead of mapping   */
