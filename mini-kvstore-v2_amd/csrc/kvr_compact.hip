@@ -320,6 +320,190 @@ __global__ void k_fold_verify(const kvr_tuple *__restrict__ tup, uint64_t n, con
     }
 }
 
+// ---- the partitioned fold: the table's ranges folded in LDS ----
+// Bucket b is the table's slot range [b S, (b + 1) S) (S = FP_S, or the whole table when it is
+// smaller).  k_fold_part files every tuple (index, tag, length, 16-B key prefix) under the range of
+// its home slot; k_fold_lds folds one bucket per workgroup in an LDS copy of its range, with the
+// global claim's probe order (linear from the home slot, first free entry or the key's own), and
+// writes the range out, free entries included (no clear).  The random traffic of the claims and
+// checks then stays in LDS: HBM sees the tuples once, the records twice and the table once.  A
+// tuple whose probe runs off the end of its range, or that found its bucket full, goes to the
+// global rounds (k_fold_claim / k_fold_verify over a list), which go on probing in the table from
+// where it stopped: every entry it passed is taken, so the linear-probing invariant holds.
+constexpr uint32_t FP_S = 2048, FP_T = 1024, FP_PER = 8, FP_PMAX = 16384;
+struct __align__(16) FPRec {
+    uint32_t i, tag, klen, pad;
+    uint4 key;   // the first 16 key bytes, zero padded
+};
+static_assert(sizeof(FPRec) == 32, "partition record");
+struct FPGeom {
+    uint32_t mask, s, shift, p;
+    uint64_t cap;   // records per bucket
+};
+// the partition geometry of the table size on the device (k_hll_size / k_fold_setsize): P ranges
+// of S = min(slots, s_lim) entries (s_lim: FP_S, a power of two), bucket capacity 1.25 n / P + 512
+// (P cap <= 1.25 n + 512 P records in all), or cap_lim when that is smaller (a test knob)
+__device__ __forceinline__ FPGeom fp_geom(const uint32_t *fsz, uint64_t n, uint32_t s_lim, uint32_t cap_lim) {
+    FPGeom g;
+    g.mask = fsz[0];
+    const uint64_t slots = (uint64_t)g.mask + 1;
+    g.s = slots < s_lim ? (uint32_t)slots : s_lim;
+    g.shift = (uint32_t)__builtin_ctz(g.s);
+    g.p = (uint32_t)(slots >> g.shift);
+    g.cap = n / g.p + n / (4ull * g.p) + 512;
+    if (cap_lim && cap_lim < g.cap) g.cap = cap_lim;
+    return g;
+}
+
+// one workgroup per FP_T * FP_PER tuples: an LDS histogram over the buckets, one global
+// reservation per non-empty bucket, then each tuple's record at its reserved place.  A tuple past
+// its bucket's capacity goes to the overflow list (ovl / ovn) with its home slot.
+__global__ void __launch_bounds__(FP_T) k_fold_part(const kvr_tuple *__restrict__ tup, uint64_t n,
+                                                    const SegDesc *__restrict__ segs, const uint4 *__restrict__ kd,
+                                                    const uint32_t *__restrict__ fsz, uint32_t *__restrict__ gcur,
+                                                    FPRec *__restrict__ rec, uint32_t *__restrict__ ovl,
+                                                    uint32_t *__restrict__ ovn, uint32_t *__restrict__ slot,
+                                                    uint32_t s_lim, uint32_t cap_lim) {
+    __shared__ uint32_t hist[FP_PMAX];
+    const FPGeom G = fp_geom(fsz, n, s_lim, cap_lim);
+    for (uint32_t j = threadIdx.x; j < G.p; j += FP_T) hist[j] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * (FP_T * FP_PER) + threadIdx.x;
+    uint32_t home[FP_PER], rk[FP_PER], tag[FP_PER], kl[FP_PER];
+#pragma unroll
+    for (int u = 0; u < FP_PER; ++u) {
+        const uint64_t i = base + (uint64_t)u * FP_T;
+        if (i < n) {
+            tag[u] = tup[i].key_tag;
+            kl[u] = tup[i].key_len;
+            home[u] = ht_mix(tag[u]) & G.mask;
+            rk[u] = atomicAdd(&hist[home[u] >> G.shift], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < G.p; j += FP_T)
+        if (hist[j]) hist[j] = atomicAdd(&gcur[j], hist[j]);   // this workgroup's first place in bucket j
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < FP_PER; ++u) {
+        const uint64_t i = base + (uint64_t)u * FP_T;
+        if (i >= n) continue;
+        const uint32_t b = home[u] >> G.shift;
+        const uint64_t pos = (uint64_t)hist[b] + rk[u];
+        if (pos >= G.cap) {
+            ovl[atomicAdd(ovn, 1u)] = (uint32_t)i;
+            slot[i] = home[u];
+            continue;
+        }
+        FPRec r;
+        r.i = (uint32_t)i;
+        r.tag = tag[u];
+        r.klen = kl[u];
+        r.pad = 0;
+        if (kd) {
+            r.key = kd[i];
+        } else {
+            const kvr_tuple t = tup[i];
+            uint32_t w[4];
+            key_prefix16(segs[t.seg_idx], t, w);
+            r.key = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        rec[(uint64_t)b * G.cap + pos] = r;
+    }
+}
+
+// one workgroup per bucket: the range's entries in LDS, the bucket's records FP_T at a time.  A
+// probe step (claim a free entry, stop at an entry with the tuple's tag, or move on) needs no key
+// bytes; after a barrier a tuple that stopped at its tag compares its key with the entry's (the
+// claimer wrote it before the barrier) and keeps the larger index, or moves on.  Barrier-synchronous
+// rounds until no tuple of the chunk is probing.  slot_all: every tuple's entry to slot[]
+// (is_last, the sharded compaction); the overflow tuples' restart entries always.
+__global__ void __launch_bounds__(FP_T) k_fold_lds(const kvr_tuple *__restrict__ tup, uint64_t n,
+                                                   const SegDesc *__restrict__ segs, const uint32_t *__restrict__ fsz,
+                                                   const uint32_t *__restrict__ gcur, const FPRec *__restrict__ rec,
+                                                   FoldEnt *__restrict__ ent, uint32_t *__restrict__ ovl,
+                                                   uint32_t *__restrict__ ovn, uint32_t *__restrict__ slot,
+                                                   uint32_t slot_all, uint32_t s_lim, uint32_t cap_lim) {
+    __shared__ unsigned long long s_tr[FP_S];
+    __shared__ uint32_t s_best[FP_S], s_klen[FP_S];
+    __shared__ uint4 s_key[FP_S];
+    const FPGeom G = fp_geom(fsz, n, s_lim, cap_lim);
+    const uint32_t b = blockIdx.x;
+    if (b >= G.p) return;
+    for (uint32_t j = threadIdx.x; j < G.s; j += FP_T) s_tr[j] = FE_EMPTY;
+    const uint64_t cnt = gcur[b] < G.cap ? gcur[b] : G.cap;
+    const FPRec *rb = rec + (uint64_t)b * G.cap;
+    const uint32_t first = b << G.shift;
+    enum : uint32_t { ST_DONE = 0, ST_PROBE = 1, ST_CHECK = 2, ST_OVER = 3 };
+    FPRec nx{};
+    if (threadIdx.x < cnt) nx = rb[threadIdx.x];
+    __syncthreads();
+    for (uint64_t c0 = 0; c0 < cnt; c0 += FP_T) {
+        const FPRec r = nx;
+        const bool have = c0 + threadIdx.x < cnt;
+        if (c0 + FP_T + threadIdx.x < cnt) nx = rb[c0 + FP_T + threadIdx.x];   // the next chunk's record
+        uint32_t st = have ? (uint32_t)ST_PROBE : (uint32_t)ST_DONE;
+        uint32_t h = have ? (ht_mix(r.tag) & G.mask & (G.s - 1)) : 0u;
+        const unsigned long long mine = ((unsigned long long)r.tag << 32) | r.i;
+        for (;;) {
+            if (st == ST_PROBE) {
+                for (;;) {
+                    unsigned long long v = s_tr[h];
+                    if (v == FE_EMPTY) {
+                        v = atomicCAS(&s_tr[h], FE_EMPTY, mine);
+                        if (v == FE_EMPTY) {   // claimed: this tuple represents its key in entry h
+                            s_best[h] = r.i;
+                            s_klen[h] = r.klen;
+                            s_key[h] = r.key;
+                            st = ST_DONE;
+                            break;
+                        }
+                    }
+                    if ((uint32_t)(v >> 32) == r.tag) { st = ST_CHECK; break; }
+                    if (++h == G.s) { st = ST_OVER; break; }
+                }
+            }
+            __syncthreads();
+            if (st == ST_CHECK) {
+                const uint4 k = s_key[h];
+                bool same = s_klen[h] == r.klen &&
+                            ((k.x ^ r.key.x) | (k.y ^ r.key.y) | (k.z ^ r.key.z) | (k.w ^ r.key.w)) == 0u;
+                if (same && r.klen > 16u) {
+                    const uint32_t rep = (uint32_t)s_tr[h];
+                    same = bytes_eq(key_ptr(segs, tup[rep]) + 16, key_ptr(segs, tup[r.i]) + 16, r.klen - 16u);
+                }
+                if (same) {
+                    atomicMax(&s_best[h], r.i);   // the fold's last writer: the largest index
+                    st = ST_DONE;
+                } else {
+                    st = ++h == G.s ? (uint32_t)ST_OVER : (uint32_t)ST_PROBE;
+                }
+            }
+            if (!__syncthreads_or(st == ST_PROBE)) break;
+        }
+        if (st == ST_OVER) {   // on into the next range (the global rounds)
+            ovl[atomicAdd(ovn, 1u)] = r.i;
+            slot[r.i] = (first + G.s) & G.mask;
+        } else if (have && slot_all) {
+            slot[r.i] = first + h;
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < G.s; j += FP_T) {
+        const unsigned long long v = s_tr[j];
+        uint4 a, k;
+        if (v == FE_EMPTY) {
+            a = make_uint4(~0u, ~0u, ~0u, ~0u);
+            k = a;
+        } else {
+            a = make_uint4((uint32_t)v, (uint32_t)(v >> 32), ~s_best[j], s_klen[j]);
+            k = s_key[j];
+        }
+        reinterpret_cast<uint4 *>(&ent[first + j])[0] = a;
+        reinterpret_cast<uint4 *>(&ent[first + j])[1] = k;
+    }
+}
+
 __device__ __forceinline__ bool is_last(const FoldEnt *ent, const uint32_t *slot, uint64_t i) {
     const uint32_t s = slot[i];
     return s != HT_EMPTY && ~ent[s].best == (uint32_t)i;

@@ -124,8 +124,12 @@ def test_index_build_host_and_find():
 
 # ---- device index --------------------------------------------------------------------------------
 @pytest.mark.gpu
-def test_fold_tag_collisions(gctx):
-    """Distinct keys with equal CRC-32 (short, and long with equal 16-B prefixes) fold exactly."""
+@pytest.mark.parametrize("path", ["lds", "global"])
+def test_fold_tag_collisions(gctx, monkeypatch, path):
+    """Distinct keys with equal CRC-32 (short, and long with equal 16-B prefixes) fold exactly, in
+    the partitioned fold's LDS ranges and in the global claim rounds (KVR_FOLD_GLOBAL)."""
+    if path == "global":
+        monkeypatch.setenv("KVR_FOLD_GLOBAL", "1")
     segs, pairs = collision_store()
     want, nk, tb = expect(segs)
     r = gctx.replay_live(segs)
@@ -133,7 +137,8 @@ def test_fold_tag_collisions(gctx):
     idx = gctx.replay_index(segs)
     live_keys = set(keys_of(segs, want))
     check_index(idx, segs, want, [k for p in pairs for k in p if k not in live_keys])
-    assert idx.stats.fold_rounds >= 2 and idx.stats.n_live == nk
+    # the global claims take a collision to a further round; the LDS ranges resolve it in place
+    assert idx.stats.fold_rounds >= (2 if path == "global" else 1) and idx.stats.n_live == nk
     # the rewrite uses the same fold: its output replays to the same map
     c = gctx.compact(segs)
     rc, t2, _ = O.replay(c.segments())
@@ -173,6 +178,37 @@ def test_fold_key_sources(gctx, monkeypatch, source):
     assert r.status == 0 and np.array_equal(r.tuples, want)
     idx = gctx.replay_index(segs)
     assert np.array_equal(idx.live, want) and idx.stats.n_live == nk
+    c = gctx.compact(segs)
+    rc, t2, _ = O.replay(c.segments())
+    assert rc == 0 and len(t2) == nk
+    assert sorted(keys_of(c.segments(), t2)) == sorted(keys_of(segs, want))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["global", "range16", "range64", "bucket32", "range16-bucket32"])
+def test_fold_partition_overflow(gctx, monkeypatch, path):
+    """The partitioned fold hands a tuple to the global rounds when its probe runs off the end of
+    its LDS range (KVR_FOLD_RANGE: ranges of 16 / 64 entries) or its bucket is full
+    (KVR_FOLD_BUCKET: 32 records); those rounds go on probing in the table the ranges wrote.  Same
+    live index (CRC-32 collisions included) and rewrite as the reference fold."""
+    segs, pairs = collision_store()
+    spec = K.GenSpec(seed=107, seg_bytes=150_000, key_space_log2=11, val_min=0, val_max=200, del_permille=250)
+    segs = segs + [K.gen_segment_cpu(spec, s)[0].tobytes() for s in range(5)]
+    want, nk, _ = expect(segs)
+    if path == "global":
+        monkeypatch.setenv("KVR_FOLD_GLOBAL", "1")
+    if "range" in path:
+        monkeypatch.setenv("KVR_FOLD_RANGE", path.split("-")[0][5:])
+    if "bucket" in path:
+        monkeypatch.setenv("KVR_FOLD_BUCKET", "32")
+    r = gctx.replay_live(segs)
+    assert r.status == 0 and np.array_equal(r.tuples, want)
+    idx = gctx.replay_index(segs)
+    live_keys = set(keys_of(segs, want))
+    check_index(idx, segs, want, [k for p in pairs for k in p if k not in live_keys])
+    assert idx.stats.n_live == nk
+    if path != "global" and path != "range64":   # (64-entry ranges may hold every probe)
+        assert idx.stats.fold_rounds >= 2   # some tuples went on to the global rounds
     c = gctx.compact(segs)
     rc, t2, _ = O.replay(c.segments())
     assert rc == 0 and len(t2) == nk
