@@ -104,6 +104,7 @@ VARIANTS = {
     "bo4": ["-DKVR_FAST_BACKOFF=4"],     # 4 tiles of scalar hops after a short lane-parallel round
     "nouni": ["-DKVR_UNIFOLD=0"],  # long-value views through LDS marks + lane permutes only
     "base": [],
+    "fp4": ["-DKVR_FP_PER=4"],   # k_fold_part: 4 tuples per thread (4096-record regions; neutral)
 }
 
 

@@ -116,8 +116,8 @@ struct kvr_ctx {
     DevBuf<kvr_tuple> ctup, lout;
     DevBuf<FoldEnt> fent;                  // the fold table (k_fold_claim / k_fold_verify)
     DevBuf<uint32_t> flist, fcnt;          // collision rounds: two tuple lists, their counts
-    DevBuf<FPRec> frec;                    // the partitioned fold's bucket records (k_fold_part)
-    DevBuf<uint32_t> fcur;                 // ... and the buckets' fill counts
+    DevBuf<FPRec> frec;                    // the partitioned fold's records (k_fold_part), per region
+    DevBuf<uint32_t> fwoff;                // ... and each region's bucket offsets
     DevBuf<uint32_t> fsz;                  // the fold table's size on the device (k_hll_size)
     bool fold_pending = false;             // deferred rounds launched, not yet checked (fold_settle)
     DevBuf<uint32_t> cslot, cflag, cpos;
@@ -341,7 +341,7 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
     c->kpool.release(); c->ckeys.release();
     c->ctup.release(); c->lout.release(); c->fent.release(); c->flist.release(); c->fcnt.release(); c->fsz.release();
-    c->frec.release(); c->fcur.release();
+    c->frec.release(); c->fwoff.release();
     c->cslot.release(); c->cflag.release(); c->islots.release(); c->ing.release(); c->hpart.release(); c->hreg.release();
     c->koff.release(); c->klen.release(); c->kbuf.release();
     c->cpos.release(); c->csize.release(); c->coff.release(); c->l_src.release();
@@ -889,8 +889,8 @@ static int fold_launch(kvr_ctx *c, size_t nt, bool deferred) {
     // round 0: the partitioned fold (k_fold_part / k_fold_lds) when the buckets of the largest
     // table fit the LDS histogram, its overflow tuples being round 1's list; else the global claims
     // over every tuple (KVR_FOLD_GLOBAL forces them: A/B and test knob)
-    // (test knobs: KVR_FOLD_RANGE, a smaller range (a power of two >= 16), and KVR_FOLD_BUCKET, a
-    // smaller bucket capacity, send many tuples on to the global rounds)
+    // (test knobs: KVR_FOLD_RANGE, a smaller range (a power of two >= 16), and KVR_FOLD_BUCKET, at
+    // most that many records of a bucket folded in LDS, send many tuples on to the global rounds)
     uint32_t s_lim = FP_S, cap_lim = 0;
     if (const char *e = getenv("KVR_FOLD_RANGE")) {
         const uint32_t v = (uint32_t)atoi(e);
@@ -898,19 +898,18 @@ static int fold_launch(kvr_ctx *c, size_t nt, bool deferred) {
     }
     if (const char *e = getenv("KVR_FOLD_BUCKET")) cap_lim = (uint32_t)atoi(e);
     const uint64_t p_host = std::max<uint64_t>(1, full_slots / s_lim);   // >= the ranges of any table size
-    const bool part = p_host <= FP_PMAX && getenv("KVR_FOLD_GLOBAL") == nullptr;
-    if (part && (c->frec.ensure(nt + nt / 4 + 513 * p_host + 16) || c->fcur.ensure(p_host))) return KVR_ENOMEM;
+    const uint64_t nwg = (nt + FP_CH - 1) / FP_CH;                       // k_fold_part's regions
+    const bool part = p_host <= FP_PMAX && nwg <= FP_WMAX && getenv("KVR_FOLD_GLOBAL") == nullptr;
+    if (part && (c->frec.ensure(nwg * FP_CH) || c->fwoff.ensure(nwg * (p_host + 1)))) return KVR_ENOMEM;
 again:
     HIPCHK(hipMemsetAsync(c->fcnt.p, 0, FOLD_CNT * FOLD_SPEC_ROUNDS * sizeof(uint32_t), st));
     if (part) {
-        HIPCHK(hipMemsetAsync(c->fcur.p, 0, p_host * sizeof(uint32_t), st));
-        hipLaunchKernelGGL(k_fold_part, dim3((uint32_t)((nt + FP_T * FP_PER - 1) / (FP_T * FP_PER))), dim3(FP_T), 0, st,
-                           c->ctup.p, (uint64_t)nt, c->segs.p, kd, c->fsz.p, c->fcur.p, c->frec.p, c->flist.p,
-                           c->fcnt.p, c->cslot.p, s_lim, cap_lim);
+        hipLaunchKernelGGL(k_fold_part, dim3((uint32_t)nwg), dim3(FP_T), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p, kd,
+                           c->fsz.p, s_lim, c->frec.p, c->fwoff.p);
         // (a synced fold serves kvr_compact_stage, whose k_cand reads every tuple's entry)
-        hipLaunchKernelGGL(k_fold_lds, dim3((uint32_t)p_host), dim3(FP_T), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p,
-                           c->fsz.p, c->fcur.p, c->frec.p, c->fent.p, c->flist.p, c->fcnt.p, c->cslot.p,
-                           deferred ? 0u : 1u, s_lim, cap_lim);
+        hipLaunchKernelGGL(k_fold_lds, dim3((uint32_t)p_host), dim3(FP_T), 0, st, c->ctup.p, c->segs.p, c->fsz.p, s_lim,
+                           c->frec.p, c->fwoff.p, (uint32_t)nwg, c->fent.p, c->flist.p, c->fcnt.p, c->cslot.p,
+                           deferred ? 0u : 1u, cap_lim);
     } else {
         hipLaunchKernelGGL(k_fent_clear, dim3(fold_grid(c)), dim3(256), 0, st, c->fent.p, c->fsz.p);
         round(nt, nullptr, nullptr, c->flist.p, c->fcnt.p);

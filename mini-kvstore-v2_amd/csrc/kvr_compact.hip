@@ -23,6 +23,9 @@
  *                   atomics execute at the memory side, about 20 G/s chip-wide).  A tag collision between two keys sends the tuple to the
  *                   next round, which resumes its probe one entry further (rounds until no tuple
  *                   is left; distinct keys sharing a CRC-32 are a few hundred per million keys)
+ *   k_fold_part / k_fold_lds   (the default first round, below) the same fold per 2048-entry
+ *                   range of the table in one workgroup's LDS; the claim and verify kernels then
+ *                   only take the few tuples whose probe leaves their range
  *   k_live_ent      per claimed entry: its key's last tuple is live iff it is a SET: flag, size
  *                   9 + k + v
  *   (scan)          exclusive sums of sizes (output offsets) and live flags (dense index)
@@ -322,15 +325,24 @@ __global__ void k_fold_verify(const kvr_tuple *__restrict__ tup, uint64_t n, con
 
 // ---- the partitioned fold: the table's ranges folded in LDS ----
 // Bucket b is the table's slot range [b S, (b + 1) S) (S = FP_S, or the whole table when it is
-// smaller).  k_fold_part files every tuple (index, tag, length, 16-B key prefix) under the range of
-// its home slot; k_fold_lds folds one bucket per workgroup in an LDS copy of its range, with the
-// global claim's probe order (linear from the home slot, first free entry or the key's own), and
-// writes the range out, free entries included (no clear).  The random traffic of the claims and
-// checks then stays in LDS: HBM sees the tuples once, the records twice and the table once.  A
-// tuple whose probe runs off the end of its range, or that found its bucket full, goes to the
-// global rounds (k_fold_claim / k_fold_verify over a list), which go on probing in the table from
-// where it stopped: every entry it passed is taken, so the linear-probing invariant holds.
-constexpr uint32_t FP_S = 2048, FP_T = 1024, FP_PER = 8, FP_PMAX = 16384;
+// smaller).  k_fold_part takes FP_CH tuples per workgroup and writes their records (index, tag,
+// length, 16-B key prefix) into the workgroup's own FP_CH-record region, grouped by bucket (whole
+// cache lines, no atomics outside LDS), with the region's bucket offsets beside it.  k_fold_lds
+// folds one bucket per workgroup in an LDS copy of its range, gathering the bucket's runs from
+// every region, with the global claim's probe order (linear from the home slot, first free entry
+// or the key's own), and writes the range out, free entries included (no clear).  The random
+// traffic of the claims and checks stays in LDS: HBM sees the tuples once, the records twice and
+// the table once.  A tuple whose probe runs off the end of its range goes to the global rounds
+// (k_fold_claim / k_fold_verify over a list), which go on probing in the table from where it
+// stopped: every entry it passed is taken, so the linear-probing invariant holds.
+#ifndef KVR_FP_PER
+#define KVR_FP_PER 8   // tuples per thread of k_fold_part (build knob)
+#endif
+// (FP_WMAX: k_fold_lds keeps two words per region in LDS; 1984 lets two 1024-thread workgroups
+// share a CU's 160 KiB)
+constexpr uint32_t FP_S = 2048, FP_T = 1024, FP_PER = KVR_FP_PER, FP_CH = FP_T * FP_PER, FP_PMAX = 16384,
+                   FP_WMAX = 1984;
+static_assert(FP_CH <= 8192 && FP_PMAX <= 1u << 19, "k_fold_part packs bucket and rank in 32 bits");
 struct __align__(16) FPRec {
     uint32_t i, tag, klen, pad;
     uint4 key;   // the first 16 key bytes, zero padded
@@ -338,63 +350,90 @@ struct __align__(16) FPRec {
 static_assert(sizeof(FPRec) == 32, "partition record");
 struct FPGeom {
     uint32_t mask, s, shift, p;
-    uint64_t cap;   // records per bucket
 };
 // the partition geometry of the table size on the device (k_hll_size / k_fold_setsize): P ranges
-// of S = min(slots, s_lim) entries (s_lim: FP_S, a power of two), bucket capacity 1.25 n / P + 512
-// (P cap <= 1.25 n + 512 P records in all), or cap_lim when that is smaller (a test knob)
-__device__ __forceinline__ FPGeom fp_geom(const uint32_t *fsz, uint64_t n, uint32_t s_lim, uint32_t cap_lim) {
+// of S = min(slots, s_lim) entries (s_lim: FP_S, or a smaller power of two as a test knob)
+__device__ __forceinline__ FPGeom fp_geom(const uint32_t *fsz, uint32_t s_lim) {
     FPGeom g;
     g.mask = fsz[0];
     const uint64_t slots = (uint64_t)g.mask + 1;
     g.s = slots < s_lim ? (uint32_t)slots : s_lim;
     g.shift = (uint32_t)__builtin_ctz(g.s);
     g.p = (uint32_t)(slots >> g.shift);
-    g.cap = n / g.p + n / (4ull * g.p) + 512;
-    if (cap_lim && cap_lim < g.cap) g.cap = cap_lim;
     return g;
 }
 
-// one workgroup per FP_T * FP_PER tuples: an LDS histogram over the buckets, one global
-// reservation per non-empty bucket, then each tuple's record at its reserved place.  A tuple past
-// its bucket's capacity goes to the overflow list (ovl / ovn) with its home slot.
-__global__ void __launch_bounds__(FP_T) k_fold_part(const kvr_tuple *__restrict__ tup, uint64_t n,
-                                                    const SegDesc *__restrict__ segs, const uint4 *__restrict__ kd,
-                                                    const uint32_t *__restrict__ fsz, uint32_t *__restrict__ gcur,
-                                                    FPRec *__restrict__ rec, uint32_t *__restrict__ ovl,
-                                                    uint32_t *__restrict__ ovn, uint32_t *__restrict__ slot,
-                                                    uint32_t s_lim, uint32_t cap_lim) {
-    __shared__ uint32_t hist[FP_PMAX];
-    const FPGeom G = fp_geom(fsz, n, s_lim, cap_lim);
-    for (uint32_t j = threadIdx.x; j < G.p; j += FP_T) hist[j] = 0;
+// exclusive prefix sum of a[0, n) in LDS, in place, by the whole block (FP_T threads, each a
+// contiguous run of ceil(n / FP_T) entries; wave scans by shuffles, then the FP_T / 64 wave
+// totals); returns the sum
+__device__ uint32_t block_excl_scan(uint32_t *a, uint32_t n, uint32_t *wsum) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, per = (n + FP_T - 1) / FP_T;
+    const uint32_t lo = t * per < n ? t * per : n, hi = lo + per < n ? lo + per : n;
+    uint32_t s = 0;
+    for (uint32_t j = lo; j < hi; ++j) s += a[j];
+    uint32_t x = s;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63u) wsum[t >> 6] = x;
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * (FP_T * FP_PER) + threadIdx.x;
-    uint32_t home[FP_PER], rk[FP_PER], tag[FP_PER], kl[FP_PER];
+    if (t < 64u) {
+        uint32_t w = t < FP_T / 64 ? wsum[t] : 0u;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(w, d, 64);
+            if (lane >= d) w += y;
+        }
+        if (t < FP_T / 64) wsum[t] = w;
+    }
+    __syncthreads();
+    uint32_t before = x - s + ((t >> 6) ? wsum[(t >> 6) - 1] : 0u);
+    const uint32_t total = wsum[FP_T / 64 - 1];
+    for (uint32_t j = lo; j < hi; ++j) {
+        const uint32_t v = a[j];
+        a[j] = before;
+        before += v;
+    }
+    __syncthreads();
+    return total;
+}
+
+// workgroup w: tuples [w FP_CH, (w + 1) FP_CH) -> records rec[w FP_CH ..), grouped by bucket;
+// woff[w (P + 1) + b] = the first record of bucket b in the region (b = P: the region's count).
+// An LDS histogram gives each tuple its rank in its bucket, its prefix sum the buckets' offsets.
+__global__ void __launch_bounds__(FP_T, 8) k_fold_part(const kvr_tuple *__restrict__ tup, uint64_t n,
+                                                       const SegDesc *__restrict__ segs, const uint4 *__restrict__ kd,
+                                                       const uint32_t *__restrict__ fsz, uint32_t s_lim,
+                                                       FPRec *__restrict__ rec, uint32_t *__restrict__ woff) {
+    __shared__ uint32_t hist[FP_PMAX + 1];
+    __shared__ uint32_t wsum[FP_T / 64];
+    const FPGeom G = fp_geom(fsz, s_lim);
+    for (uint32_t j = threadIdx.x; j <= G.p; j += FP_T) hist[j] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * FP_CH + threadIdx.x;
+    // bk: bucket << 13 | rank in the region's share of it
+    uint32_t bk[FP_PER], tag[FP_PER], kl[FP_PER];
 #pragma unroll
     for (int u = 0; u < FP_PER; ++u) {
         const uint64_t i = base + (uint64_t)u * FP_T;
         if (i < n) {
             tag[u] = tup[i].key_tag;
             kl[u] = tup[i].key_len;
-            home[u] = ht_mix(tag[u]) & G.mask;
-            rk[u] = atomicAdd(&hist[home[u] >> G.shift], 1u);
+            const uint32_t b = (ht_mix(tag[u]) & G.mask) >> G.shift;
+            bk[u] = b << 13 | atomicAdd(&hist[b], 1u);
         }
     }
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < G.p; j += FP_T)
-        if (hist[j]) hist[j] = atomicAdd(&gcur[j], hist[j]);   // this workgroup's first place in bucket j
-    __syncthreads();
+    block_excl_scan(hist, G.p + 1, wsum);
+    uint32_t *wo = woff + (uint64_t)blockIdx.x * (G.p + 1);
+    for (uint32_t j = threadIdx.x; j <= G.p; j += FP_T) wo[j] = hist[j];
+    FPRec *rg = rec + (uint64_t)blockIdx.x * FP_CH;
 #pragma unroll
     for (int u = 0; u < FP_PER; ++u) {
         const uint64_t i = base + (uint64_t)u * FP_T;
         if (i >= n) continue;
-        const uint32_t b = home[u] >> G.shift;
-        const uint64_t pos = (uint64_t)hist[b] + rk[u];
-        if (pos >= G.cap) {
-            ovl[atomicAdd(ovn, 1u)] = (uint32_t)i;
-            slot[i] = home[u];
-            continue;
-        }
         FPRec r;
         r.i = (uint32_t)i;
         r.tag = tag[u];
@@ -408,42 +447,78 @@ __global__ void __launch_bounds__(FP_T) k_fold_part(const kvr_tuple *__restrict_
             key_prefix16(segs[t.seg_idx], t, w);
             r.key = make_uint4(w[0], w[1], w[2], w[3]);
         }
-        rec[(uint64_t)b * G.cap + pos] = r;
+        rg[hist[bk[u] >> 13] + (bk[u] & 8191u)] = r;
     }
 }
 
-// one workgroup per bucket: the range's entries in LDS, the bucket's records FP_T at a time.  A
-// probe step (claim a free entry, stop at an entry with the tuple's tag, or move on) needs no key
-// bytes; after a barrier a tuple that stopped at its tag compares its key with the entry's (the
-// claimer wrote it before the barrier) and keeps the larger index, or moves on.  Barrier-synchronous
-// rounds until no tuple of the chunk is probing.  slot_all: every tuple's entry to slot[]
-// (is_last, the sharded compaction); the overflow tuples' restart entries always.
-__global__ void __launch_bounds__(FP_T) k_fold_lds(const kvr_tuple *__restrict__ tup, uint64_t n,
-                                                   const SegDesc *__restrict__ segs, const uint32_t *__restrict__ fsz,
-                                                   const uint32_t *__restrict__ gcur, const FPRec *__restrict__ rec,
-                                                   FoldEnt *__restrict__ ent, uint32_t *__restrict__ ovl,
-                                                   uint32_t *__restrict__ ovn, uint32_t *__restrict__ slot,
-                                                   uint32_t slot_all, uint32_t s_lim, uint32_t cap_lim) {
+// bytes 16 .. klen of two keys equal (the rare long-key check, out of line: its unrolled loads
+// would otherwise hold registers through k_fold_lds)
+__device__ __attribute__((noinline)) bool key_tail_eq(const SegDesc *segs, const kvr_tuple *tup, uint32_t a,
+                                                      uint32_t b, uint32_t klen) {
+    return bytes_eq(key_ptr(segs, tup[a]) + 16, key_ptr(segs, tup[b]) + 16, klen - 16u);
+}
+
+// one workgroup per bucket: the range's entries in LDS; the bucket's records (its run in each of
+// the nwg regions, located by a prefix sum over the runs' lengths and a binary search) FP_T at a
+// time.  A probe step (claim a free entry, stop at an entry with the tuple's tag, or move on)
+// needs no key bytes; after a barrier a tuple that stopped at its tag compares its key with the
+// entry's (the claimer wrote it before the barrier) and keeps the larger index, or moves on.
+// Barrier-synchronous rounds until no tuple of the chunk is probing.  slot_all: every tuple's
+// entry to slot[] (is_last, the sharded compaction); the overflow tuples' restart entries always.
+// cap_lim (test knob): records of the bucket past cap_lim go to the global rounds from their home.
+__global__ void __launch_bounds__(FP_T, 8) k_fold_lds(const kvr_tuple *__restrict__ tup, const SegDesc *__restrict__ segs,
+                                                      const uint32_t *__restrict__ fsz, uint32_t s_lim,
+                                                      const FPRec *__restrict__ rec, const uint32_t *__restrict__ woff,
+                                                      uint32_t nwg, FoldEnt *__restrict__ ent, uint32_t *__restrict__ ovl,
+                                                      uint32_t *__restrict__ ovn, uint32_t *__restrict__ slot,
+                                                      uint32_t slot_all, uint32_t cap_lim) {
     __shared__ unsigned long long s_tr[FP_S];
     __shared__ uint32_t s_best[FP_S], s_klen[FP_S];
     __shared__ uint4 s_key[FP_S];
-    const FPGeom G = fp_geom(fsz, n, s_lim, cap_lim);
+    __shared__ uint32_t wsc[FP_WMAX + 1];   // the bucket's first record in run w (prefix sum)
+    __shared__ uint32_t wrb[FP_WMAX];       // run w's first record in rec[]
+    __shared__ uint32_t wsum[FP_T / 64];
+    const FPGeom G = fp_geom(fsz, s_lim);
     const uint32_t b = blockIdx.x;
     if (b >= G.p) return;
     for (uint32_t j = threadIdx.x; j < G.s; j += FP_T) s_tr[j] = FE_EMPTY;
-    const uint64_t cnt = gcur[b] < G.cap ? gcur[b] : G.cap;
-    const FPRec *rb = rec + (uint64_t)b * G.cap;
-    const uint32_t first = b << G.shift;
-    enum : uint32_t { ST_DONE = 0, ST_PROBE = 1, ST_CHECK = 2, ST_OVER = 3 };
-    FPRec nx{};
-    if (threadIdx.x < cnt) nx = rb[threadIdx.x];
+    const uint64_t stride = (uint64_t)G.p + 1;
+    for (uint32_t w = threadIdx.x; w <= nwg; w += FP_T) {
+        uint32_t len = 0;
+        if (w < nwg) {
+            const uint32_t o0 = woff[w * stride + b];
+            len = woff[w * stride + b + 1] - o0;
+            wrb[w] = w * FP_CH + o0;
+        }
+        wsc[w] = len;
+    }
     __syncthreads();
-    for (uint64_t c0 = 0; c0 < cnt; c0 += FP_T) {
-        const FPRec r = nx;
-        const bool have = c0 + threadIdx.x < cnt;
-        if (c0 + FP_T + threadIdx.x < cnt) nx = rb[c0 + FP_T + threadIdx.x];   // the next chunk's record
-        uint32_t st = have ? (uint32_t)ST_PROBE : (uint32_t)ST_DONE;
+    const uint32_t cnt = block_excl_scan(wsc, nwg + 1, wsum);
+    const uint32_t first = b << G.shift;
+    // record k of the bucket: the last run starting at or before k, by binary search
+    auto locate = [&](uint32_t k) -> FPRec {
+        uint32_t lo = 0, hi = nwg - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (wsc[mid] <= k) lo = mid;
+            else hi = mid - 1;
+        }
+        return rec[wrb[lo] + (k - wsc[lo])];
+    };
+    enum : uint32_t { ST_DONE = 0, ST_PROBE = 1, ST_CHECK = 2, ST_OVER = 3 };
+    // (loading the next chunk's record ahead measured slower: 141 vs 132 us on cfg4)
+    for (uint32_t c0 = 0; c0 < cnt; c0 += FP_T) {
+        const uint32_t k = c0 + threadIdx.x;
+        bool have = k < cnt;
+        FPRec r{};
+        if (have) r = locate(k);
         uint32_t h = have ? (ht_mix(r.tag) & G.mask & (G.s - 1)) : 0u;
+        if (have && cap_lim && k >= cap_lim) {   // (test knob) on to the global rounds from its home
+            ovl[atomicAdd(ovn, 1u)] = r.i;
+            slot[r.i] = first + h;
+            have = false;
+        }
+        uint32_t st = have ? (uint32_t)ST_PROBE : (uint32_t)ST_DONE;
         const unsigned long long mine = ((unsigned long long)r.tag << 32) | r.i;
         for (;;) {
             if (st == ST_PROBE) {
@@ -465,13 +540,10 @@ __global__ void __launch_bounds__(FP_T) k_fold_lds(const kvr_tuple *__restrict__
             }
             __syncthreads();
             if (st == ST_CHECK) {
-                const uint4 k = s_key[h];
+                const uint4 q = s_key[h];
                 bool same = s_klen[h] == r.klen &&
-                            ((k.x ^ r.key.x) | (k.y ^ r.key.y) | (k.z ^ r.key.z) | (k.w ^ r.key.w)) == 0u;
-                if (same && r.klen > 16u) {
-                    const uint32_t rep = (uint32_t)s_tr[h];
-                    same = bytes_eq(key_ptr(segs, tup[rep]) + 16, key_ptr(segs, tup[r.i]) + 16, r.klen - 16u);
-                }
+                            ((q.x ^ r.key.x) | (q.y ^ r.key.y) | (q.z ^ r.key.z) | (q.w ^ r.key.w)) == 0u;
+                if (same && r.klen > 16u) same = key_tail_eq(segs, tup, (uint32_t)s_tr[h], r.i, r.klen);
                 if (same) {
                     atomicMax(&s_best[h], r.i);   // the fold's last writer: the largest index
                     st = ST_DONE;
@@ -491,16 +563,16 @@ __global__ void __launch_bounds__(FP_T) k_fold_lds(const kvr_tuple *__restrict__
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < G.s; j += FP_T) {
         const unsigned long long v = s_tr[j];
-        uint4 a, k;
+        uint4 a, q;
         if (v == FE_EMPTY) {
             a = make_uint4(~0u, ~0u, ~0u, ~0u);
-            k = a;
+            q = a;
         } else {
             a = make_uint4((uint32_t)v, (uint32_t)(v >> 32), ~s_best[j], s_klen[j]);
-            k = s_key[j];
+            q = s_key[j];
         }
         reinterpret_cast<uint4 *>(&ent[first + j])[0] = a;
-        reinterpret_cast<uint4 *>(&ent[first + j])[1] = k;
+        reinterpret_cast<uint4 *>(&ent[first + j])[1] = q;
     }
 }
 

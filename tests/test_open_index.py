@@ -188,8 +188,8 @@ def test_fold_key_sources(gctx, monkeypatch, source):
 @pytest.mark.parametrize("path", ["global", "range16", "range64", "bucket32", "range16-bucket32"])
 def test_fold_partition_overflow(gctx, monkeypatch, path):
     """The partitioned fold hands a tuple to the global rounds when its probe runs off the end of
-    its LDS range (KVR_FOLD_RANGE: ranges of 16 / 64 entries) or its bucket is full
-    (KVR_FOLD_BUCKET: 32 records); those rounds go on probing in the table the ranges wrote.  Same
+    its LDS range (KVR_FOLD_RANGE: ranges of 16 / 64 entries) or it comes after the first 32
+    records of its bucket (KVR_FOLD_BUCKET); those rounds go on probing in the table the ranges wrote.  Same
     live index (CRC-32 collisions included) and rewrite as the reference fold."""
     segs, pairs = collision_store()
     spec = K.GenSpec(seed=107, seg_bytes=150_000, key_space_log2=11, val_min=0, val_max=200, del_permille=250)
