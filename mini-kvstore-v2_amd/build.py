@@ -104,6 +104,8 @@ VARIANTS = {
     "bo4": ["-DKVR_FAST_BACKOFF=4"],     # 4 tiles of scalar hops after a short lane-parallel round
     "nouni": ["-DKVR_UNIFOLD=0"],  # long-value views through LDS marks + lane permutes only
     "base": [],
+    "u1": ["-DKVR_FP_U=1"],      # k_fold_lds: one record per thread and step
+    "u2": ["-DKVR_FP_U=2"],
     "fp4": ["-DKVR_FP_PER=4"],   # k_fold_part: 4 tuples per thread (4096-record regions; neutral)
 }
 

@@ -118,6 +118,7 @@ struct kvr_ctx {
     DevBuf<uint32_t> flist, fcnt;          // collision rounds: two tuple lists, their counts
     DevBuf<FPRec> frec;                    // the partitioned fold's records (k_fold_part), per region
     DevBuf<uint32_t> fwoff;                // ... and each region's bucket offsets
+    DevBuf<uint32_t> fhot;                 // ... and the hot buckets (k_fold_lds -> k_fold_hot)
     DevBuf<uint32_t> fsz;                  // the fold table's size on the device (k_hll_size)
     bool fold_pending = false;             // deferred rounds launched, not yet checked (fold_settle)
     DevBuf<uint32_t> cslot, cflag, cpos;
@@ -341,7 +342,7 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
     c->kpool.release(); c->ckeys.release();
     c->ctup.release(); c->lout.release(); c->fent.release(); c->flist.release(); c->fcnt.release(); c->fsz.release();
-    c->frec.release(); c->fwoff.release();
+    c->frec.release(); c->fwoff.release(); c->fhot.release();
     c->cslot.release(); c->cflag.release(); c->islots.release(); c->ing.release(); c->hpart.release(); c->hreg.release();
     c->koff.release(); c->klen.release(); c->kbuf.release();
     c->cpos.release(); c->csize.release(); c->coff.release(); c->l_src.release();
@@ -851,7 +852,7 @@ static int fold_launch(kvr_ctx *c, size_t nt, bool deferred) {
     uint64_t full_slots = 1;
     while (full_slots < 2 * (uint64_t)nt) full_slots <<= 1;
     if (c->fent.ensure(full_slots) || c->cslot.ensure(nt) || c->flist.ensure(2 * nt) ||
-        c->fcnt.ensure(FOLD_CNT * FOLD_SPEC_ROUNDS) || c->fsz.ensure(4))
+        c->fcnt.ensure(FOLD_CNT * FOLD_SPEC_ROUNDS + 1) || c->fsz.ensure(4))
         return KVR_ENOMEM;
     c->fold_rounds = 0;
     c->fold_redo = 0;
@@ -890,7 +891,8 @@ static int fold_launch(kvr_ctx *c, size_t nt, bool deferred) {
     // table fit the LDS histogram, its overflow tuples being round 1's list; else the global claims
     // over every tuple (KVR_FOLD_GLOBAL forces them: A/B and test knob)
     // (test knobs: KVR_FOLD_RANGE, a smaller range (a power of two >= 16), and KVR_FOLD_BUCKET, at
-    // most that many records of a bucket folded in LDS, send many tuples on to the global rounds)
+    // most that many records of a bucket folded in LDS (the rest through k_fold_hot), send many
+    // tuples on to the global rounds)
     uint32_t s_lim = FP_S, cap_lim = 0;
     if (const char *e = getenv("KVR_FOLD_RANGE")) {
         const uint32_t v = (uint32_t)atoi(e);
@@ -900,16 +902,24 @@ static int fold_launch(kvr_ctx *c, size_t nt, bool deferred) {
     const uint64_t p_host = std::max<uint64_t>(1, full_slots / s_lim);   // >= the ranges of any table size
     const uint64_t nwg = (nt + FP_CH - 1) / FP_CH;                       // k_fold_part's regions
     const bool part = p_host <= FP_PMAX && nwg <= FP_WMAX && getenv("KVR_FOLD_GLOBAL") == nullptr;
-    if (part && (c->frec.ensure(nwg * FP_CH) || c->fwoff.ensure(nwg * (p_host + 1)))) return KVR_ENOMEM;
+    const uint64_t hot_max = p_host / 4 + 2;   // hot buckets (cnt > cap >= 4 nt / P) and their run arrays
+    if (part && (c->frec.ensure(nwg * FP_CH) || c->fwoff.ensure(nwg * (p_host + 1)) ||
+                 c->fhot.ensure(hot_max * 2 + hot_max * 2 * (nwg + 1))))
+        return KVR_ENOMEM;
 again:
-    HIPCHK(hipMemsetAsync(c->fcnt.p, 0, FOLD_CNT * FOLD_SPEC_ROUNDS * sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(c->fcnt.p, 0, (FOLD_CNT * FOLD_SPEC_ROUNDS + 1) * sizeof(uint32_t), st));
     if (part) {
         hipLaunchKernelGGL(k_fold_part, dim3((uint32_t)nwg), dim3(FP_T), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p, kd,
                            c->fsz.p, s_lim, c->frec.p, c->fwoff.p);
         // (a synced fold serves kvr_compact_stage, whose k_cand reads every tuple's entry)
         hipLaunchKernelGGL(k_fold_lds, dim3((uint32_t)p_host), dim3(FP_T), 0, st, c->ctup.p, c->segs.p, c->fsz.p, s_lim,
                            c->frec.p, c->fwoff.p, (uint32_t)nwg, c->fent.p, c->flist.p, c->fcnt.p, c->cslot.p,
-                           deferred ? 0u : 1u, cap_lim);
+                           deferred ? 0u : 1u, (uint64_t)nt, cap_lim, c->fhot.p, c->fhot.p + hot_max * 2,
+                           c->fcnt.p + FOLD_CNT * FOLD_SPEC_ROUNDS, (uint32_t)hot_max);
+        hipLaunchKernelGGL(k_fold_hot, dim3((uint32_t)c->n_cu * 4), dim3(256), 0, st, c->ctup.p, c->segs.p, c->fsz.p,
+                           c->frec.p, (uint32_t)nwg, c->fent.p, c->fhot.p, c->fhot.p + hot_max * 2,
+                           c->fcnt.p + FOLD_CNT * FOLD_SPEC_ROUNDS, c->flist.p, c->fcnt.p, c->cslot.p,
+                           deferred ? 0u : 1u, (uint32_t)hot_max);
     } else {
         hipLaunchKernelGGL(k_fent_clear, dim3(fold_grid(c)), dim3(256), 0, st, c->fent.p, c->fsz.p);
         round(nt, nullptr, nullptr, c->flist.p, c->fcnt.p);

@@ -458,20 +458,44 @@ __device__ __attribute__((noinline)) bool key_tail_eq(const SegDesc *segs, const
     return bytes_eq(key_ptr(segs, tup[a]) + 16, key_ptr(segs, tup[b]) + 16, klen - 16u);
 }
 
+// append v to list (count *n) from the active lanes of a wave: one atomic per wave
+__device__ __forceinline__ void list_push(uint32_t *__restrict__ list, uint32_t *__restrict__ n, uint32_t v) {
+    const uint64_t m = __ballot(1);
+    const uint32_t lane = __lane_id();
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(n, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)leader);
+    list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = v;
+}
+
 // one workgroup per bucket: the range's entries in LDS; the bucket's records (its run in each of
-// the nwg regions, located by a prefix sum over the runs' lengths and a binary search) FP_T at a
-// time.  A probe step (claim a free entry, stop at an entry with the tuple's tag, or move on)
-// needs no key bytes; after a barrier a tuple that stopped at its tag compares its key with the
-// entry's (the claimer wrote it before the barrier) and keeps the larger index, or moves on.
-// Barrier-synchronous rounds until no tuple of the chunk is probing.  slot_all: every tuple's
-// entry to slot[] (is_last, the sharded compaction); the overflow tuples' restart entries always.
-// cap_lim (test knob): records of the bucket past cap_lim go to the global rounds from their home.
+// the nwg regions, located by a prefix sum over the runs' lengths and a binary search), each thread
+// its own records, latest first, with no barrier between them.  A probe step claims a free entry
+// (64-bit LDS CAS; the claimer writes the key length and prefix, then publishes its index as the
+// entry's best), stops at an entry with the tuple's tag, or moves on.  A tuple that stopped waits
+// for the entry to be published (its claimer has done the CAS and writes on without waiting, and
+// a claimer of the same wave finishes its writes in the same probe step, before any lane of the
+// wave waits), compares its key, and keeps the larger index (an atomicMax only when it is larger:
+// latest first, a hot key's later tuples skip it), or probes on.  slot_all: every tuple's entry
+// to slot[] (is_last, the sharded compaction); the overflow tuples' restart entries always.
+// A bucket folds its latest cap records in LDS (cap_lim, or 4 times the mean bucket, at least
+// 16 Ki); a longer bucket (a hot key's) leaves its earlier records to k_fold_hot, which the whole
+// device runs: it gets the bucket (hb: bucket, count) and its run arrays (hw), fewer than P / 4
+// buckets (cap >= 4 n / P).
+#ifndef KVR_FP_U
+#define KVR_FP_U 2   // records per thread and step of k_fold_lds (build knob; 4 spills)
+#endif
+constexpr uint32_t FP_U = KVR_FP_U;
+constexpr uint32_t FP_UNPUB = 0xFFFFFFFFu;   // s_best of a claimed entry not yet published (indices < 2^31)
 __global__ void __launch_bounds__(FP_T, 8) k_fold_lds(const kvr_tuple *__restrict__ tup, const SegDesc *__restrict__ segs,
                                                       const uint32_t *__restrict__ fsz, uint32_t s_lim,
                                                       const FPRec *__restrict__ rec, const uint32_t *__restrict__ woff,
                                                       uint32_t nwg, FoldEnt *__restrict__ ent, uint32_t *__restrict__ ovl,
                                                       uint32_t *__restrict__ ovn, uint32_t *__restrict__ slot,
-                                                      uint32_t slot_all, uint32_t cap_lim) {
+                                                      uint32_t slot_all, uint64_t n, uint32_t cap_lim,
+                                                      uint32_t *__restrict__ hb, uint32_t *__restrict__ hw,
+                                                      uint32_t *__restrict__ hn, uint32_t hot_cap) {
     __shared__ unsigned long long s_tr[FP_S];
     __shared__ uint32_t s_best[FP_S], s_klen[FP_S];
     __shared__ uint4 s_key[FP_S];
@@ -481,7 +505,10 @@ __global__ void __launch_bounds__(FP_T, 8) k_fold_lds(const kvr_tuple *__restric
     const FPGeom G = fp_geom(fsz, s_lim);
     const uint32_t b = blockIdx.x;
     if (b >= G.p) return;
-    for (uint32_t j = threadIdx.x; j < G.s; j += FP_T) s_tr[j] = FE_EMPTY;
+    for (uint32_t j = threadIdx.x; j < G.s; j += FP_T) {
+        s_tr[j] = FE_EMPTY;
+        s_best[j] = FP_UNPUB;
+    }
     const uint64_t stride = (uint64_t)G.p + 1;
     for (uint32_t w = threadIdx.x; w <= nwg; w += FP_T) {
         uint32_t len = 0;
@@ -495,6 +522,28 @@ __global__ void __launch_bounds__(FP_T, 8) k_fold_lds(const kvr_tuple *__restric
     __syncthreads();
     const uint32_t cnt = block_excl_scan(wsc, nwg + 1, wsum);
     const uint32_t first = b << G.shift;
+    const uint64_t mean4 = 4 * (n / G.p);
+    const uint32_t cap = cap_lim ? cap_lim : (uint32_t)(mean4 > 16384 ? (mean4 < 0x7FFFFFFF ? mean4 : 0x7FFFFFFF) : 16384);
+    uint32_t n_lds = cnt;   // the bucket's latest records, k in [cnt - n_lds, cnt), fold here
+    if (cnt > cap) {   // a hot bucket: its records [0, cnt - cap) to k_fold_hot, with the run arrays
+        __shared__ uint32_t s_j;
+        if (threadIdx.x == 0) {
+            s_j = atomicAdd(hn, 1u);
+            if (s_j < hot_cap) {
+                hb[2 * s_j] = b;
+                hb[2 * s_j + 1] = cnt - cap;
+            }
+        }
+        __syncthreads();
+        if (s_j < hot_cap) {   // (else, beyond the room for hot buckets: all of it here)
+            uint32_t *dst = hw + (uint64_t)s_j * 2 * (nwg + 1);
+            for (uint32_t w = threadIdx.x; w <= nwg; w += FP_T) {
+                dst[w] = wsc[w];
+                if (w < nwg) dst[nwg + 1 + w] = wrb[w];
+            }
+            n_lds = cap;
+        }
+    }
     // record k of the bucket: the last run starting at or before k, by binary search
     auto locate = [&](uint32_t k) -> FPRec {
         uint32_t lo = 0, hi = nwg - 1;
@@ -505,60 +554,69 @@ __global__ void __launch_bounds__(FP_T, 8) k_fold_lds(const kvr_tuple *__restric
         }
         return rec[wrb[lo] + (k - wsc[lo])];
     };
-    enum : uint32_t { ST_DONE = 0, ST_PROBE = 1, ST_CHECK = 2, ST_OVER = 3 };
-    // (loading the next chunk's record ahead measured slower: 141 vs 132 us on cfg4)
-    for (uint32_t c0 = 0; c0 < cnt; c0 += FP_T) {
-        const uint32_t k = c0 + threadIdx.x;
-        bool have = k < cnt;
-        FPRec r{};
-        if (have) r = locate(k);
-        uint32_t h = have ? (ht_mix(r.tag) & G.mask & (G.s - 1)) : 0u;
-        if (have && cap_lim && k >= cap_lim) {   // (test knob) on to the global rounds from its home
-            ovl[atomicAdd(ovn, 1u)] = r.i;
-            slot[r.i] = first + h;
-            have = false;
-        }
-        uint32_t st = have ? (uint32_t)ST_PROBE : (uint32_t)ST_DONE;
+    // FP_U records per thread and step, their loads issued together (a hot key's bucket is long)
+    for (uint32_t q0 = threadIdx.x; q0 < n_lds; q0 += FP_T * FP_U) {
+      FPRec rr[FP_U];
+#pragma unroll
+      for (uint32_t u = 0; u < FP_U; ++u)
+        if (q0 + u * FP_T < n_lds) rr[u] = locate(cnt - 1 - (q0 + u * FP_T));
+#pragma unroll
+      for (uint32_t u = 0; u < FP_U; ++u) {
+        if (q0 + u * FP_T >= n_lds) break;
+        const uint32_t k = cnt - 1 - (q0 + u * FP_T);   // latest first (regions in tuple order)
+        const FPRec &r = rr[u];
+        uint32_t h = ht_mix(r.tag) & G.mask & (G.s - 1);
         const unsigned long long mine = ((unsigned long long)r.tag << 32) | r.i;
+        uint32_t restart = HT_EMPTY;   // set: on to the global rounds from this entry
         for (;;) {
-            if (st == ST_PROBE) {
-                for (;;) {
-                    unsigned long long v = s_tr[h];
-                    if (v == FE_EMPTY) {
-                        v = atomicCAS(&s_tr[h], FE_EMPTY, mine);
-                        if (v == FE_EMPTY) {   // claimed: this tuple represents its key in entry h
-                            s_best[h] = r.i;
-                            s_klen[h] = r.klen;
-                            s_key[h] = r.key;
-                            st = ST_DONE;
-                            break;
-                        }
+            // probe: claim (fill, then publish) or stop at the tuple's tag.  The wave leaves this
+            // loop only when all its lanes have, so a claimer of the same wave has published
+            // before any lane of the wave waits below.
+            bool match = false;
+            unsigned long long v;
+            for (;;) {
+                v = __hip_atomic_load(&s_tr[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (v == FE_EMPTY) {
+                    v = atomicCAS(&s_tr[h], FE_EMPTY, mine);
+                    if (v == FE_EMPTY) {   // this tuple represents its key in entry h
+                        s_klen[h] = r.klen;
+                        s_key[h] = r.key;
+                        __hip_atomic_store(&s_best[h], r.i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        break;
                     }
-                    if ((uint32_t)(v >> 32) == r.tag) { st = ST_CHECK; break; }
-                    if (++h == G.s) { st = ST_OVER; break; }
                 }
+                if ((uint32_t)(v >> 32) == r.tag) { match = true; break; }
+                if (++h == G.s) { restart = (first + G.s) & G.mask; break; }   // on into the next range
             }
-            __syncthreads();
-            if (st == ST_CHECK) {
-                const uint4 q = s_key[h];
-                bool same = s_klen[h] == r.klen &&
-                            ((q.x ^ r.key.x) | (q.y ^ r.key.y) | (q.z ^ r.key.z) | (q.w ^ r.key.w)) == 0u;
-                if (same && r.klen > 16u) same = key_tail_eq(segs, tup, (uint32_t)s_tr[h], r.i, r.klen);
-                if (same) {
-                    atomicMax(&s_best[h], r.i);   // the fold's last writer: the largest index
-                    st = ST_DONE;
-                } else {
-                    st = ++h == G.s ? (uint32_t)ST_OVER : (uint32_t)ST_PROBE;
-                }
+            if (!match) break;
+            uint32_t best, spins = 0;
+            while ((best = __hip_atomic_load(&s_best[h], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == FP_UNPUB &&
+                   ++spins < (1u << 20)) {
             }
-            if (!__syncthreads_or(st == ST_PROBE)) break;
+            if (best == FP_UNPUB) {   // (a bound on the wait, never reached in practice: the global
+                restart = first + h;   // rounds take the tuple from this entry)
+                break;
+            }
+            const uint4 e = s_key[h];
+            bool same = s_klen[h] == r.klen &&
+                        ((e.x ^ r.key.x) | (e.y ^ r.key.y) | (e.z ^ r.key.z) | (e.w ^ r.key.w)) == 0u;
+            if (same && r.klen > 16u) same = key_tail_eq(segs, tup, (uint32_t)v, r.i, r.klen);
+            if (same) {
+                if (best < r.i) atomicMax(&s_best[h], r.i);   // the fold's last writer: the largest index
+                break;
+            }
+            if (++h == G.s) {   // another key with this tag: probe on
+                restart = (first + G.s) & G.mask;
+                break;
+            }
         }
-        if (st == ST_OVER) {   // on into the next range (the global rounds)
-            ovl[atomicAdd(ovn, 1u)] = r.i;
-            slot[r.i] = (first + G.s) & G.mask;
-        } else if (have && slot_all) {
+        if (restart != HT_EMPTY) {
+            list_push(ovl, ovn, r.i);
+            slot[r.i] = restart;
+        } else if (slot_all) {
             slot[r.i] = first + h;
         }
+      }
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < G.s; j += FP_T) {
@@ -573,6 +631,53 @@ __global__ void __launch_bounds__(FP_T, 8) k_fold_lds(const kvr_tuple *__restric
         }
         reinterpret_cast<uint4 *>(&ent[first + j])[0] = a;
         reinterpret_cast<uint4 *>(&ent[first + j])[1] = q;
+    }
+}
+
+// the hot buckets' earlier records (k_fold_lds: buckets longer than their LDS cap), over the
+// whole device, bucket after bucket: each record looks its key up in the table the ranges wrote,
+// with plain loads (a hot entry stays in every L2); a key already there with a later tuple as its
+// best needs nothing more.  Any other tuple goes to the global rounds from its home entry.
+__global__ void k_fold_hot(const kvr_tuple *__restrict__ tup, const SegDesc *__restrict__ segs,
+                           const uint32_t *__restrict__ fsz, const FPRec *__restrict__ rec, uint32_t nwg,
+                           const FoldEnt *__restrict__ ent, const uint32_t *__restrict__ hb,
+                           const uint32_t *__restrict__ hw, const uint32_t *__restrict__ hn, uint32_t *__restrict__ ovl,
+                           uint32_t *__restrict__ ovn, uint32_t *__restrict__ slot, uint32_t slot_all,
+                           uint32_t hot_cap) {
+    const uint32_t nh = *hn < hot_cap ? *hn : hot_cap, mask = fsz[0];
+    for (uint32_t j = 0; j < nh; ++j) {
+        const uint32_t m = hb[2 * j + 1];
+        const uint32_t *wsc = hw + (uint64_t)j * 2 * (nwg + 1), *wrb = wsc + nwg + 1;
+        for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < m; k += gridDim.x * blockDim.x) {
+            uint32_t lo = 0, hi = nwg - 1;   // the last run starting at or before k
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (wsc[mid] <= k) lo = mid;
+                else hi = mid - 1;
+            }
+            const FPRec r = rec[wrb[lo] + (k - wsc[lo])];
+            const uint32_t home = ht_mix(r.tag) & mask;
+            uint32_t h = home;
+            bool done = false;
+            for (uint32_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+                const uint4 a = reinterpret_cast<const uint4 *>(&ent[h])[0];
+                if (a.x == 0xFFFFFFFFu && a.y == 0xFFFFFFFFu) break;   // free: the key is not in the table
+                if (a.y != r.tag || a.w != r.klen) continue;
+                const uint4 q = reinterpret_cast<const uint4 *>(&ent[h])[1];
+                bool same = ((r.key.x ^ q.x) | (r.key.y ^ q.y) | (r.key.z ^ q.z) | (r.key.w ^ q.w)) == 0u;
+                if (same && r.klen > 16u) same = key_tail_eq(segs, tup, a.x, r.i, r.klen);
+                if (same) {
+                    done = ~a.z > r.i;   // a later tuple of the key is its best already
+                    break;
+                }
+            }
+            if (done) {
+                if (slot_all) slot[r.i] = h;
+            } else {
+                list_push(ovl, ovn, r.i);
+                slot[r.i] = home;
+            }
+        }
     }
 }
 
