@@ -216,6 +216,31 @@ def test_fold_partition_overflow(gctx, monkeypatch, path):
 
 
 @pytest.mark.gpu
+def test_fold_hot_keys(gctx, monkeypatch):
+    """Log-uniform keys over 2^20 (kvr_gen_common.h key_dist 1: key 0 alone is 1/20 of the
+    records, keys 1-2 1/40 each, ...) in 2 M small records: the hot keys' table ranges pass their
+    LDS cap and leave their earlier records to k_fold_hot.  The live list, the key table and the
+    rewrite equal the oracle's; the global claims (KVR_FOLD_GLOBAL) give the same live list and a
+    key table as valid."""
+    spec = K.GenSpec(seed=211, seg_bytes=8 << 20, key_space_log2=20, key_dist=1, val_min=0, val_max=16,
+                     del_permille=300)
+    segs = [K.gen_segment_cpu(spec, s)[0] for s in range(8)]
+    want, nk, _ = expect(segs)
+    r = gctx.replay_live(segs)
+    assert r.status == 0 and np.array_equal(r.tuples, want)
+    idx = gctx.replay_index(segs)
+    check_index(idx, segs, want, [b"no-such-key"])
+    assert idx.stats.n_tuples > 2_000_000 and idx.stats.n_live == nk
+    monkeypatch.setenv("KVR_FOLD_GLOBAL", "1")
+    idx_g = gctx.replay_index(segs)
+    check_index(idx_g, segs, want, [b"no-such-key"])   # (entries may sit elsewhere: another claim order)
+    monkeypatch.delenv("KVR_FOLD_GLOBAL")
+    c = gctx.compact(segs, 4 << 20)
+    rc, want_c, ends, _ = O.compact(segs, 4 << 20)
+    assert rc == 0 and c.status == 0 and c.seg_ends == ends and c.data == want_c
+
+
+@pytest.mark.gpu
 def test_fold_table_estimate(gctx):
     """cfg-like input with many more tuples than keys: the table is sized from the HyperLogLog
     estimate (within a few percent of the true key count), not from the tuples."""
