@@ -1020,36 +1020,50 @@ static int fold_settle(kvr_ctx *c, size_t nt, bool *redone, uint32_t *last2) {
 
 // live flags (and, for a rewrite, record sizes) of the tuples from the fold table
 // (keep_del: the last record of every key, tombstones included)
-static hipError_t live_flags(kvr_ctx *c, size_t nt, bool sizes, bool keep_del = false) {
+static hipError_t live_flags(kvr_ctx *c, size_t nt, bool sizes, bool keep_del = false, bool packed = false) {
     hipStream_t st = c->stream;
-    hipError_t e = hipMemsetAsync(c->cflag.p, 0, nt * 4, st);
-    if (e == hipSuccess && sizes) e = hipMemsetAsync(c->csize.p, 0, nt * 8, st);
+    hipError_t e = packed ? hipSuccess : hipMemsetAsync(c->cflag.p, 0, nt * 4, st);
+    if (e == hipSuccess && (sizes || packed)) e = hipMemsetAsync(c->csize.p, 0, nt * 8, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_live_ent, dim3(fold_grid(c)), dim3(256), 0, st, c->fent.p, c->fsz.p, c->ctup.p,
-                       sizes ? c->csize.p : nullptr, c->cflag.p, keep_del ? 1u : 0u);
+                       (sizes || packed) ? c->csize.p : nullptr, packed ? nullptr : c->cflag.p, keep_del ? 1u : 0u);
     return hipGetLastError();
+}
+// kvr_compact's sizes and live flags in one word (size << 24 | live), one scan for both
+static bool compact_packed(const kvr_ctx *c, size_t nt) {
+    return nt < (1ull << 24) && c->cstats.bytes_in < (1ull << 40) && getenv("KVR_COMPACT_TWO_SCANS") == nullptr;
 }
 
 // sizes and live flags are in csize / cflag: scans, dense live list, cuts, gather, output
 static int compact_back(kvr_ctx *c, uint32_t flags, uint64_t seg_target, uint8_t *out, uint64_t out_cap,
-                        uint64_t *out_len, uint64_t *seg_ends, size_t seg_cap, size_t *n_out_segs) {
+                        uint64_t *out_len, uint64_t *seg_ends, size_t seg_cap, size_t *n_out_segs,
+                        bool packed = false) {
     const size_t nt = c->c_nt;
     const uint64_t bytes_in = c->cstats.bytes_in;
     hipStream_t st = c->stream;
     const uint32_t g = (uint32_t)((nt + 255) / 256);
     size_t tb = c->ctmp.n;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->csize.p, c->coff.p, (int)nt, st));
-    tb = c->ctmp.n;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->cflag.p, c->cpos.p, (int)nt, st));
-    hipLaunchKernelGGL(k_ctotals, dim3(1), dim3(64), 0, st, c->csize.p, c->coff.p, c->cflag.p, c->cpos.p, (uint64_t)nt,
-                       c->l_off.p, c->ctot.p);
+    if (packed) {
+        hipLaunchKernelGGL(k_ctotals_p, dim3(1), dim3(64), 0, st, c->csize.p, c->coff.p, (uint64_t)nt, c->l_off.p,
+                           c->ctot.p);
+    } else {
+        tb = c->ctmp.n;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->cflag.p, c->cpos.p, (int)nt, st));
+        hipLaunchKernelGGL(k_ctotals, dim3(1), dim3(64), 0, st, c->csize.p, c->coff.p, c->cflag.p, c->cpos.p,
+                           (uint64_t)nt, c->l_off.p, c->ctot.p);
+    }
     HIPCHK(hipGetLastError());
     // the live bytes are at most the segment bytes: size everything by that bound, so the rest of
     // the pipeline runs without a host round trip (the kernels read the true sizes on device)
     const uint64_t max_cuts = seg_target ? bytes_in / seg_target + 1 : 1;
     if (c->ccuts.ensure(max_cuts)) return KVR_ENOMEM;
-    hipLaunchKernelGGL(k_scatter, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p, c->csize.p, c->coff.p,
-                       c->cflag.p, c->cpos.p, c->l_src.p, c->l_off.p);
+    if (packed)
+        hipLaunchKernelGGL(k_scatter_p, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p, c->csize.p,
+                           c->coff.p, c->l_src.p, c->l_off.p);
+    else
+        hipLaunchKernelGGL(k_scatter, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p, c->csize.p,
+                           c->coff.p, c->cflag.p, c->cpos.p, c->l_src.p, c->l_off.p);
     HIPCHK(hipGetLastError());
     if (seg_target) {
         hipLaunchKernelGGL(k_cuts, dim3((uint32_t)std::min<uint64_t>((max_cuts + 255) / 256, 1024)), dim3(256), 0, st,
@@ -1114,11 +1128,12 @@ int kvr_compact(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, u
     size_t nt = 0;
     const int rc = compact_front(c, segs, n, flags, err, &nt, true, &c->cstats, true);   // deferred rounds
     if (rc != KVR_OK || nt == 0) return rc;
-    HIPCHK(live_flags(c, nt, true));
-    int rb = compact_back(c, flags, seg_target, out, out_cap, out_len, seg_ends, seg_cap, n_out_segs);
+    const bool packed = compact_packed(c, nt);
+    HIPCHK(live_flags(c, nt, true, false, packed));
+    int rb = compact_back(c, flags, seg_target, out, out_cap, out_len, seg_ends, seg_cap, n_out_segs, packed);
     if (rb == FOLD_REDONE) {
-        HIPCHK(live_flags(c, nt, true));
-        rb = compact_back(c, flags, seg_target, out, out_cap, out_len, seg_ends, seg_cap, n_out_segs);
+        HIPCHK(live_flags(c, nt, true, false, packed));
+        rb = compact_back(c, flags, seg_target, out, out_cap, out_len, seg_ends, seg_cap, n_out_segs, packed);
     }
     return rb;
 }

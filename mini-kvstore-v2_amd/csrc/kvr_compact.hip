@@ -702,6 +702,10 @@ __global__ void k_live_ent(const FoldEnt *__restrict__ ent, const uint32_t *__re
         const uint32_t j = ~a.z;
         const kvr_tuple t = tup[j];
         if (t.op != 0 && !keep_del) continue;
+        if (!flag) {   // packed (kvr_compact): size << 24 | 1, one scan gives offsets and positions
+            size[j] = (9ull + t.key_len + t.val_len) << 24 | 1ull;
+            continue;
+        }
         flag[j] = 1u;
         if (size) size[j] = 9ull + t.key_len + t.val_len;   // SET framing, engine.rs:169-173
     }
@@ -730,6 +734,29 @@ __global__ void k_scatter(const kvr_tuple *__restrict__ tup, uint64_t n, const S
     const uint32_t j = pos[i];
     l_src[j] = reinterpret_cast<uint64_t>(segs[t.seg_idx].base + t.rec_off);
     l_off[j] = off[i];
+}
+
+// the packed forms (kvr_compact when n < 2^24 and the bytes < 2^40): sz[i] = size << 24 | live,
+// its exclusive scan off[i] = offset << 24 | position
+__global__ void k_ctotals_p(const uint64_t *__restrict__ sz, const uint64_t *__restrict__ off, uint64_t n,
+                            uint64_t *__restrict__ l_off, uint64_t *__restrict__ totals) {
+    if (threadIdx.x || blockIdx.x) return;
+    const uint64_t e = n ? off[n - 1] + sz[n - 1] : 0;
+    const uint64_t bytes = e >> 24, live = e & 0xFFFFFFull;
+    l_off[live] = bytes;
+    totals[0] = bytes;
+    totals[1] = live;
+}
+__global__ void k_scatter_p(const kvr_tuple *__restrict__ tup, uint64_t n, const SegDesc *__restrict__ segs,
+                            const uint64_t *__restrict__ sz, const uint64_t *__restrict__ off,
+                            uint64_t *__restrict__ l_src, uint64_t *__restrict__ l_off) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !(sz[i] & 1ull)) return;
+    const kvr_tuple t = tup[i];
+    const uint64_t o = off[i];
+    const uint64_t j = o & 0xFFFFFFull;
+    l_src[j] = reinterpret_cast<uint64_t>(segs[t.seg_idx].base + t.rec_off);
+    l_off[j] = o >> 24;
 }
 
 // one wave per live record (grid-stride over records): the record's source and
