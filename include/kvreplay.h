@@ -216,6 +216,11 @@ int  kvr_ingest_begin(kvr_ctx *ctx, uint64_t total_bytes, size_t n_segs);
 int  kvr_ingest_push(kvr_ctx *ctx, uint64_t seg_id, const uint8_t *bytes, uint64_t len);
 int  kvr_ingest_index(kvr_ctx *ctx, uint32_t flags, kvr_tuple *live, size_t live_cap, uint32_t *slots,
                       uint64_t slot_cap, size_t *n_live, uint64_t *n_slots, kvr_error *err);
+/* Abandon an ingest: waits until every copy kvr_ingest_push queued has read its host bytes, then
+ * forgets the pushed segments.  A caller that gives up between push and index (a file that
+ * vanished while the store was read, engine.rs:80-83) calls it before it frees or unregisters the
+ * host buffers it pushed. */
+int  kvr_ingest_abort(kvr_ctx *ctx);
 /* Pinned (page-locked) host memory for segment bytes: hipHostMalloc / hipHostFree.  Or register
  * existing host memory for DMA (hipHostRegister / hipHostUnregister; cheap once its pages exist)
  * and pass it as pinned. */

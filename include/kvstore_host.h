@@ -103,6 +103,8 @@ typedef struct kvs_open_stats {
     uint32_t mode;           /* KVS_LOAD_MMAP or KVS_LOAD_PREAD                                     */
     uint32_t pad;
 } kvs_open_stats;
+/* ctx may be NULL: the store then opens on the host only, which succeeds only when its segments
+ * hold no bytes (a new or emptied store); a store with records returns KVR_EINVAL. */
 int kvs_open_ex(const char *dir, kvr_ctx *ctx, uint32_t flags, kvs_store **out, kvr_error *err, char *msg,
                 size_t msg_cap);
 int kvs_last_open_stats(const kvs_store *s, kvs_open_stats *out);

@@ -396,11 +396,13 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
 
 // a replay whose tuples exceed the pool's 32-bit slots (dense small records: more than about
 // 4 G records in one call) runs as consecutive batches of whole segments, each its own
-// pipeline, the tuples appended in order — the same output, errors and return codes.  Host
-// segments are first copied into the arena all at once (the batches then replay them in place),
-// so that every segment stays resident and, at the end, the segment descriptors on the device
-// describe the whole input: the fold, the key arena and the compaction's gather read keys and
-// records of any batch.  Key prefixes (kout) are appended per batch like the tuples.
+// pipeline, the tuples appended in order — the same output, errors and return codes.  When a
+// fold or the compaction's gather reads the segments afterwards, host segments are first copied
+// into the arena all at once (the batches then replay them in place), so that every segment stays
+// resident and, at the end, the segment descriptors on the device describe the whole input: the
+// fold, the key arena and the gather read keys and records of any batch.  A plain replay stages
+// each batch on its own (no more HBM than one batch).  Key prefixes (kout) are appended per batch
+// like the tuples.
 static int replay_batched(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t flags, const uint32_t *expected,
                           size_t n_expected, kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err, uint64_t need) {
     uint64_t total = 0;
@@ -409,7 +411,11 @@ static int replay_batched(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_
     const uint64_t budget = total / parts + 1;
     HIPCHK(hipSetDevice(c->device));
     std::vector<kvr_segment> dsegs(segs, segs + n);
-    if (!(flags & KVR_SEGS_ON_DEVICE)) {
+    // host segments go resident all at once only when something reads them after the replay: a
+    // fold (key prefixes requested, c->kout) or a device-side consumer of the output (the
+    // compaction's gather, KVR_OUT_ON_DEVICE); a plain replay stages each batch's segments itself
+    const bool resident = !(flags & KVR_SEGS_ON_DEVICE) && (c->kout || (flags & KVR_OUT_ON_DEVICE));
+    if (resident) {
         uint64_t arena = 256;
         for (size_t i = 0; i < n; ++i) arena += (segs[i].len + 255) & ~255ull;
         if (c->arena.ensure(arena)) return KVR_ENOMEM;
@@ -459,6 +465,14 @@ static int replay_batched(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_
         s0 = s1;
     }
     c->kout = done <= cap ? kout : nullptr;   // (prefixes past the output's room were not written)
+    if (!(flags & KVR_SEGS_ON_DEVICE)) {   // staged per batch: nothing describes the whole input
+        c->up_segs_p = nullptr;
+        c->up_stripes_p = nullptr;
+        c->h_stripes_up = false;
+        c->stats = sum;
+        *n_out = done;
+        return done > cap ? KVR_CAPACITY : KVR_OK;
+    }
     // the descriptors of every segment (only base and len are read after the replay), and the
     // per-call upload caches invalidated
     if (c->segs.ensure(n)) return KVR_ENOMEM;

@@ -324,10 +324,11 @@ int index_host_fold(kvs_store *s, kvr_ctx *ctx, uint32_t stream_flags, kvr_error
     const size_t n = s->segs.size();
     uint64_t total = 0;
     for (const kvr_segment &g : s->segs) total += g.len;
+    if (!ctx && total) return KVR_EINVAL;   // records to replay, and no device to replay them on
     std::vector<kvr_tuple> t((size_t)(total / 256) + 16);
     size_t nt = 0;
     kvr_error e{};
-    int rc = n ? kvr_replay_stream(ctx, s->segs.data(), n, stream_flags, 0, nullptr, 0, t.data(), t.size(), &nt, &e)
+    int rc = n && total ? kvr_replay_stream(ctx, s->segs.data(), n, stream_flags, 0, nullptr, 0, t.data(), t.size(), &nt, &e)
                : KVR_OK;
     if (rc == KVR_CAPACITY) {
         t.resize(nt);
@@ -577,7 +578,7 @@ static int write_file_sync(const std::string &path, const uint8_t *p, size_t n) 
 
 int kvs_open_ex(const char *dir, kvr_ctx *ctx, uint32_t flags, kvs_store **out, kvr_error *err, char *msg,
                 size_t msg_cap) {
-    if (!dir || !ctx || !out) return KVR_EINVAL;
+    if (!dir || !out) return KVR_EINVAL;   // (ctx NULL: host only, see kvstore_host.h)
     *out = nullptr;
     if (err) memset(err, 0, sizeof(*err));
     if (msg && msg_cap) msg[0] = 0;
@@ -613,6 +614,12 @@ int kvs_open_ex(const char *dir, kvr_ctx *ctx, uint32_t flags, kvs_store **out, 
         close(fd);
         sizes.push_back(dir_like ? 0 : (uint64_t)fs.st_size);
     }
+    // test knob: segment i's file disappears between discovery and the read (the race that
+    // test_open_vanished_segment drives deterministically)
+    if (const char *vn = getenv("KVS_TEST_VANISH")) {
+        const size_t vi = (size_t)strtoull(vn, nullptr, 10);
+        if (vi < n_ok) unlink(paths[vi].c_str());
+    }
 
     std::unique_ptr<kvs_store> s(new kvs_store());
     s->dir = dir;
@@ -621,8 +628,16 @@ int kvs_open_ex(const char *dir, kvr_ctx *ctx, uint32_t flags, kvs_store **out, 
     s->ost.n_segments = n_ok;
     s->segs.resize(n_ok);
     for (size_t i = 0; i < n_ok; ++i) s->segs[i] = kvr_segment{ids[i], nullptr, sizes[i]};
-    const bool device = !(flags & KVS_OPEN_HOST_FOLD) && kvr_ingest_begin(ctx, page_up(std::accumulate(
+    const bool device = ctx && !(flags & KVS_OPEN_HOST_FOLD) && kvr_ingest_begin(ctx, page_up(std::accumulate(
                             sizes.begin(), sizes.end(), (uint64_t)0, [](uint64_t a, uint64_t b) { return a + page_up(b); })), n_ok) == KVR_OK;
+    // declared after the store, so destroyed before it: on every return from here on, the copies
+    // queued by kvr_ingest_push have finished reading the store's host bytes before those are
+    // unregistered and unmapped (an early return, e.g. a file that vanished, leaves them in flight)
+    struct IngestGuard {
+        kvr_ctx *c;
+        bool on;
+        ~IngestGuard() { if (on) kvr_ingest_abort(c); }
+    } ingest_guard{ctx, device};
     const bool reg = !(flags & KVS_OPEN_NO_PIN);
     const uint32_t n_threads = (uint32_t)std::min<uint64_t>(16, std::max(1u, std::thread::hardware_concurrency()));
     s->ost.read_threads = n_threads;

@@ -290,6 +290,15 @@ int kvr_ingest_push(kvr_ctx *c, uint64_t seg_id, const uint8_t *bytes, uint64_t 
     return KVR_OK;
 }
 
+int kvr_ingest_abort(kvr_ctx *c) {
+    if (!c) return KVR_EINVAL;
+    HIPCHK(hipSetDevice(c->device));
+    if (c->copy) HIPCHK(hipStreamSynchronize(c->copy));   // every queued DMA has read its host bytes
+    c->ing_segs.clear();
+    c->ing_off = 0;
+    return KVR_OK;
+}
+
 int kvr_ingest_index(kvr_ctx *c, uint32_t flags, kvr_tuple *live, size_t live_cap, uint32_t *slots, uint64_t slot_cap,
                      size_t *n_live, uint64_t *n_slots, kvr_error *err) {
     if (!c || !c->copy) return KVR_EINVAL;

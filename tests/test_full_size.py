@@ -123,3 +123,97 @@ def test_full_size_cfg4_compaction(gctx):
     assert rco == rg.status == 0 and np.array_equal(rg.tuples, ro)
     # every record of the new segments is a SET, and there is exactly one per live key
     assert (ro["op"] == 0).all() and len(ro) == r.stats.n_live
+
+
+def test_replay_past_the_pool_slot_limit(gctx):
+    """kvr_replay over more records than the pool's 32-bit slots hold (the real limit, 2^32 - 2^16
+    tuples, not lowered): 4.5 G five-byte DEL records of the empty key ([1][0 0 0 0], a valid record:
+    engine.rs:96-114 accepts an empty UTF-8 key, :141 removes it) in 15 segments of 1.5 GB, between
+    two generated segments.  kvr_replay batches the input into whole-segment pipelines; the tuples
+    (in HBM, 144 GB) are checked on the device against their exact expected values (rec_off = 5 j,
+    seg_idx, key_len = val_len = crc32 = key_tag = 0, op = 1), the generated segments tuple for
+    tuple against the oracle, and a torn last segment gives the oracle's first error.
+    (The fold caps one call at 2^31 tuples, below this limit, so the folding callers never batch at
+    the real limit; they are run batched at full cfg4 size below with the limit lowered.)"""
+    spec = K.GenSpec(seed=109, seg_bytes=1 << 20, key_space_log2=12, val_min=0, val_max=3000, del_permille=200)
+    small = [K.gen_segment_cpu(spec, s)[0] for s in range(2)]
+    n_big, rec_big = 15, 300_000_000
+    big_len = 5 * rec_big
+    n_rec = n_big * rec_big
+    assert n_rec > 0xFFFF0000
+    data = torch.zeros(n_big * big_len + 2 * (1 << 20) + 4096, dtype=torch.uint8, device="cuda")
+    data[: n_big * big_len].view(-1, 5)[:, 0] = 1
+    tail = data[n_big * big_len:]
+    o0 = 0
+    tail[o0: o0 + len(small[0])] = torch.from_numpy(np.asarray(small[0])).cuda()
+    o1 = ((len(small[0]) + 255) // 256) * 256
+    tail[o1: o1 + len(small[1])] = torch.from_numpy(np.asarray(small[1])).cuda()
+    tb = tail.data_ptr()
+    segs = ([(tb + o0, len(small[0]))] + [(data.data_ptr() + i * big_len, big_len) for i in range(n_big)] +
+            [(tb + o1, len(small[1]))])
+    rc0, ref0, _ = O.replay([small[0]])
+    rc1, ref1, _ = O.replay([small[1]])
+    assert rc0 == rc1 == 0
+    total = n_rec + len(ref0) + len(ref1)
+    out = torch.empty((total + 1024) * 32, dtype=torch.uint8, device="cuda")
+    r = gctx.replay(segs, on_device=True, out_ptr=out.data_ptr(), cap=total + 1024)
+    torch.cuda.synchronize()
+    assert r.status == 0 and r.n == total
+    t64 = out.view(torch.int64)
+    # the generated segments against the oracle
+    got0 = out[: len(ref0) * 32].cpu().numpy().view(K.TUPLE_DTYPE)
+    assert np.array_equal(got0, ref0)
+    b1 = (len(ref0) + n_rec) * 32
+    got1 = out[b1: b1 + len(ref1) * 32].cpu().numpy().view(K.TUPLE_DTYPE).copy()
+    assert (got1["seg_idx"] == n_big + 1).all()
+    got1["seg_idx"] = 0
+    assert np.array_equal(got1, ref1)
+    # the big segments: every tuple equals its expected value, checked on the device in chunks
+    step = 50_000_000
+    base = len(ref0)
+    for s in range(n_big):
+        for j0 in range(0, rec_big, step):
+            m = min(step, rec_big - j0)
+            rows = t64[4 * (base + s * rec_big + j0): 4 * (base + s * rec_big + j0 + m)].view(m, 4)
+            want_off = torch.arange(j0, j0 + m, device="cuda", dtype=torch.int64) * 5
+            assert torch.equal(rows[:, 0], want_off)
+            assert bool((rows[:, 1] == s + 1).all())          # seg_idx s + 1, key_len 0
+            assert bool((rows[:, 2] == 0).all())              # val_len 0, crc32 0
+            assert bool((rows[:, 3] == (1 << 32)).all())      # key_tag 0, op 1, flags 0
+            del rows, want_off
+    # a torn last segment: the first error is the oracle's, found in the last batch
+    torn = small[1][: len(small[1]) - 3]
+    rce, _, err = O.replay([torn])
+    assert rce == K.CORRUPTED
+    segs[-1] = (tb + o1, len(torn))
+    r = gctx.replay(segs, on_device=True, out_ptr=out.data_ptr(), cap=total + 1024)
+    assert r.status == K.CORRUPTED
+    assert (r.error.kind, r.error.seg_idx, r.error.rec_off, r.error.aux) == (err.kind, n_big + 1, err.rec_off, err.aux)
+
+
+def test_full_size_cfg4_fold_batched(gctx, monkeypatch):
+    """The folding callers batched at full size: one GPU's cfg4 shard (64 x 64 MiB, 8 M records,
+    50 % DEL) with the pool-slot limit lowered to 3 M tuples, so kvr_replay_live and kvr_compact run
+    their replay as three or more whole-segment batches, then fold all of them (the path a
+    mid-round-3 bug once broke with status 0).  The live list equals the oracle's fold and the
+    compaction output equals oracle_compact byte for byte."""
+    data, offs, sizes, man, n_rec = _generate(gctx, "cfg4")
+    segs = [(data.data_ptr() + o, ln) for (ln, _), o in zip(sizes, offs)]
+    host = data.cpu().numpy()
+    hsegs = [host[o: o + ln] for (ln, _), o in zip(sizes, offs)]
+    rc, t, _ = O.replay_parallel(hsegs, threads=16)
+    assert rc == 0 and len(t) == n_rec
+    live, nk, _ = O.fold_live(hsegs, t)
+    monkeypatch.setenv("KVR_POOL_LIMIT", "3000000")
+    r = gctx.replay_live(segs, on_device=True)
+    assert r.status == 0 and r.n == nk and np.array_equal(r.tuples, t[live])
+    total = sum(ln for ln, _ in sizes)
+    target = 64 << 20
+    out = torch.empty(total + 4096, dtype=torch.uint8, device="cuda")
+    rcmp = gctx.compact(segs, target, on_device=True, out_ptr=out.data_ptr(), out_cap=out.numel())
+    assert rcmp.status == 0
+    torch.cuda.synchronize()
+    got = out[: rcmp.out_len].cpu().numpy().tobytes()
+    del data, out
+    rco, want, ends, _ = O.compact(hsegs, seg_target=target)
+    assert rco == 0 and got == want and rcmp.seg_ends == ends

@@ -1,10 +1,12 @@
 """kvr_replay_multi (include/kvreplay.h) through the C ABI: segments dealt round-robin
-over several contexts (two or three contexts on one device stand in for GPUs), each shard replayed
-on its own host thread, merged on the host.  The result must be bit-exact with the oracle's replay
+over several contexts, each shard replayed on its own host thread, merged on the host.  Every test
+runs on repeated device 0 (contexts on one GPU stand in for GPUs) and, on a box with enough GPUs,
+on distinct devices (per-thread hipSetDevice, one stream per device).  The result must be bit-exact with the oracle's replay
 of the whole store: every tuple field in (segment, offset) order, the manifest verification flags,
 and the store's first error (the minimum (segment, offset) over the shards, engine.rs:56)."""
 import numpy as np
 import pytest
+import torch
 
 import kvreplay as K
 import oracle_py as O
@@ -15,12 +17,28 @@ SPEC = K.GenSpec(seed=0x3C7A, seg_bytes=300_000, val_min=16, val_max=5000, del_p
                  key_space_log2=10, flip_per_million=3000)
 
 
+def _n_gpus():
+    try:
+        return torch.cuda.device_count()   # (does not initialise HIP)
+    except Exception:
+        return 0
+
+
+def device_lists(n):
+    """[0] * n always; [0, 1, .., n-1] too when the box has n GPUs."""
+    out = [pytest.param([0] * n, id=f"dev0x{n}")]
+    out.append(pytest.param(list(range(n)), id=f"dev{n}",
+                            marks=pytest.mark.skipif(_n_gpus() < n, reason=f"needs {n} GPUs")))
+    return out
+
+
 def _store(n):
     parts = [K.gen_segment_cpu(SPEC, s) for s in range(n)]
     return [p[0].tobytes() for p in parts], np.concatenate([p[1] for p in parts])
 
 
-@pytest.mark.parametrize("devices,n_segs", [([0, 0], 5), ([0, 0, 0], 7), ([0, 0], 1), ([0, 0, 0], 2)])
+@pytest.mark.parametrize("n_segs", [5, 1, 7, 2])
+@pytest.mark.parametrize("devices", device_lists(2) + device_lists(3))
 def test_multi_matches_oracle(devices, n_segs):
     segs, man = _store(n_segs)
     mc = K.MultiContext(devices)
@@ -40,13 +58,14 @@ def test_multi_matches_oracle(devices, n_segs):
         mc.close()
 
 
-def test_multi_first_error_is_store_minimum():
+@pytest.mark.parametrize("devices", device_lists(2))
+def test_multi_first_error_is_store_minimum(devices):
     segs, _ = _store(6)
     bad = list(segs)
     bad[4] = bad[4][:-3]           # shard 0 (segments 0, 2, 4): torn tail
     bad[3] = bad[3][:-1]           # shard 1 (segments 1, 3, 5): torn earlier in the store
     bad[5] = b"\x07" + bad[5][1:]  # a bad opcode after both
-    mc = K.MultiContext([0, 0])
+    mc = K.MultiContext(devices)
     try:
         r = mc.replay(bad)
         rc, _, e = O.replay(bad)
@@ -57,8 +76,9 @@ def test_multi_first_error_is_store_minimum():
         mc.close()
 
 
-def test_multi_empty_and_capacity():
-    mc = K.MultiContext([0, 0])
+@pytest.mark.parametrize("devices", device_lists(2))
+def test_multi_empty_and_capacity(devices):
+    mc = K.MultiContext(devices)
     try:
         r = mc.replay([])
         assert r.status == 0 and r.n == 0
@@ -70,8 +90,8 @@ def test_multi_empty_and_capacity():
         mc.close()
 
 
-@pytest.mark.parametrize("n_ctx", [2, 3])
-def test_live_multi_matches_oracle_fold(n_ctx):
+@pytest.mark.parametrize("devices", device_lists(2) + device_lists(3))
+def test_live_multi_matches_oracle_fold(devices):
     """kvr_replay_live_multi: per-GPU reduction to every key's last record (tombstones kept: a DEL
     in one shard deletes a key SET in another), host merge by (segment, offset) -> exactly the
     oracle's live map of the whole store."""
@@ -80,7 +100,7 @@ def test_live_multi_matches_oracle_fold(n_ctx):
     ids = [2, 3, 5, 8, 13, 21, 34]
     rc, t, _ = O.replay(segs, seg_ids=ids)
     live, nk, tb = O.fold_live(segs, t)
-    m = K.MultiContext([0] * n_ctx)
+    m = K.MultiContext(devices)
     try:
         r = m.replay(segs, seg_ids=ids, live=True)
         assert r.status == 0 and r.n == nk and np.array_equal(r.tuples, t[live])
@@ -92,14 +112,14 @@ def test_live_multi_matches_oracle_fold(n_ctx):
         m.close()
 
 
-@pytest.mark.parametrize("n_ctx", [2, 3])
-def test_live_multi_device_resident_with_keys(n_ctx):
+@pytest.mark.parametrize("devices", device_lists(2) + device_lists(3))
+def test_live_multi_device_resident_with_keys(devices):
     """The sharded index of a store that lives in HBM (BASELINE cfg4/cfg5 shape: generated on the
     device, never on the host): kvr_replay_live_multi with KVR_SEGS_ON_DEVICE, segment i on
     context i mod N.  Keys repeat across segments and 35 % of records are DELs, so tombstones cross
     shards.  The live tuples equal the oracle's fold of the whole store (engine.rs:137 / :141) and
-    the exported key bytes (kvr_multi_live_keys) equal the oracle's keys of those records."""
-    torch = pytest.importorskip("torch")
+    the exported key bytes (kvr_multi_live_keys) equal the oracle's keys of those records.
+    Segment i is generated on, and stays in the HBM of, device devices[i mod N]."""
     spec = K.GenSpec(seed=108, seg_bytes=250_000, key_space_log2=9, val_min=0, val_max=300, del_permille=350)
     n = 7
     ids = [1, 4, 9, 16, 25, 36, 49]
@@ -108,18 +128,24 @@ def test_live_multi_device_resident_with_keys(n_ctx):
     live, nk, _ = O.fold_live(host, t)
     want = t[live]
     wkeys = [bytes(host[x["seg_idx"]][x["rec_off"] + 5: x["rec_off"] + 5 + x["key_len"]]) for x in want]
-    gctx = K.Context(0)
-    m = K.MultiContext([0] * n_ctx)
+    nd = len(devices)
+    gens = {d: K.Context(d) for d in sorted(set(devices))}
+    m = K.MultiContext(devices)
     try:
         sizes = [len(h) for h in host]
-        buf = torch.zeros(sum(s + 256 for s in sizes) + 256, dtype=torch.uint8, device="cuda")
-        ptrs, off = [], 16
+        bufs = {d: torch.zeros(sum(s + 256 for s in sizes) + 256, dtype=torch.uint8, device=f"cuda:{d}")
+                for d in gens}
+        offs = {d: 16 for d in gens}
+        ptrs = []
         for s, ln in enumerate(sizes):
-            got = gctx.gen_segment_device(spec, s, buf.data_ptr() + off, ln)
+            d = devices[s % nd]
+            p = bufs[d].data_ptr() + offs[d]
+            got = gens[d].gen_segment_device(spec, s, p, ln)
             assert got[0] == ln
-            ptrs.append((buf.data_ptr() + off, ln))
-            off += ln + 256 + (s % 5)            # odd device alignments
-        torch.cuda.synchronize()
+            ptrs.append((p, ln))
+            offs[d] += ln + 256 + (s % 5)          # odd device alignments
+        for d in gens:
+            torch.cuda.synchronize(d)
         r = m.replay(ptrs, seg_ids=ids, live=True, on_device=True)
         assert r.status == 0 and r.n == nk and np.array_equal(r.tuples, want)
         keys, offs = m.live_keys(r.n)
@@ -137,4 +163,5 @@ def test_live_multi_device_resident_with_keys(n_ctx):
         assert (r3.error.kind, r3.error.seg_idx, r3.error.rec_off) == (err.kind, err.seg_idx, err.rec_off)
     finally:
         m.close()
-        gctx.close()
+        for g in gens.values():
+            g.close()

@@ -1,8 +1,8 @@
 """KVStore::open bookkeeping on the host (engine.rs:24-28, :59-68), CPU only.
 
-An empty store on the host-fold path (KVS_OPEN_HOST_FOLD) never touches the replay context:
-there is nothing to replay, so these tests pass a placeholder context pointer and run without a
-GPU.  They pin the directory and active-segment behaviour of kvs_open_ex against engine.rs:
+An empty store needs no replay context: kvs_open_ex takes ctx = NULL for a host-only open
+(kvstore_host.h), which the C side checks (a store with records returns KVR_EINVAL), so these
+tests run without a GPU.  They pin the directory and active-segment behaviour of kvs_open_ex against engine.rs:
   - engine.rs:26-28  fs::create_dir_all(dir) when the directory is missing (nested parents too);
   - engine.rs:59-68  next id = max + 1 (1 for an empty store), segment-<id>.dat created for
                      appends, and a failure to create it is StoreError::Io (KVR_EIO).
@@ -14,7 +14,7 @@ import pytest
 
 import kvreplay as kv
 
-DUMMY_CTX = C.c_void_p(0x10)   # never dereferenced for an empty store on the host-fold path
+NO_CTX = None   # host-only open: no context (kvstore_host.h kvs_open_ex)
 
 
 def open_ex(path, flags=kv.OPEN_HOST_FOLD):
@@ -22,7 +22,7 @@ def open_ex(path, flags=kv.OPEN_HOST_FOLD):
     h = C.c_void_p()
     err = kv.Error()
     msg = C.create_string_buffer(4096)
-    rc = host.kvs_open_ex(str(path).encode(), DUMMY_CTX, flags, C.byref(h), C.byref(err), msg, len(msg))
+    rc = host.kvs_open_ex(str(path).encode(), NO_CTX, flags, C.byref(h), C.byref(err), msg, len(msg))
     return rc, h
 
 
@@ -81,3 +81,16 @@ def test_open_fails_when_the_directory_path_is_a_file(tmp_path):
     rc, h = open_ex(f)
     close(h)
     assert rc == kv.EIO
+
+
+def test_open_without_context_refuses_records(tmp_path):
+    d = tmp_path / "store"
+    d.mkdir()
+    (d / "segment-1.dat").write_bytes(b"")   # empty segments replay to nothing: host-only open works
+    rc, h = open_ex(d, 0)
+    close(h)
+    assert rc == kv.OK
+    (d / "segment-2.dat").write_bytes(bytes([1, 1, 0, 0, 0]) + b"k")   # a DEL record: needs the device
+    rc, h = open_ex(d, 0)
+    close(h)
+    assert rc == kv.EINVAL

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B timing of k_replay builds (tools/ablate.py cfg2: masks under lib/ablate, names under
 # lib/variants) and, optionally, their per-tile PMC counters (tools/pmc_variants.sh).
-#   usage: tools/r03_ab.sh <tag> "<timed builds>" "<pmc builds>" [cfg]
+#   usage: tools/ab.sh <tag> "<timed builds>" "<pmc builds>" [cfg]
 set -o pipefail
 T=$1; A=$2; P=$3; CFG=${4:-cfg2}
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
