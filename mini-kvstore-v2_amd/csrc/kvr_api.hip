@@ -577,7 +577,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             const uint64_t ns = g.n_tiles ? (g.n_tiles + tps - 1) / tps : 0;
             for (uint64_t j = 0; j < ns; ++j)
                 c->h_stripes.push_back(StripeDesc{(uint32_t)i, (uint32_t)(j * g.n_tiles / ns),
-                                                  (uint32_t)((j + 1) * g.n_tiles / ns), 0u});
+                                                  (uint32_t)((j + 1) * g.n_tiles / ns), j == 0 ? 1u : 0u});
             g.n_stripes = (uint32_t)ns;
         }
     }
@@ -651,7 +651,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         // the ordered gather pool -> output: one workgroup per stripe from the stripe offsets k_link
         // computes
         auto launch_compact = [&]() {
-            hipLaunchKernelGGL(k_compact_s, dim3(n_stripes), dim3(CT), 0, st, c->segs.p, c->stripes.p, c->soff.p,
+            hipLaunchKernelGGL(k_compact_s, dim3(n_stripes), dim3(CT), 0, st, c->segs.p, c->stripes.p, c->sres.p, c->soff.p,
                                c->tres.p, c->pool.p, pool_cap, d_out, out_cap, d_exp,
                                (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p, kp, kp ? c->kout : nullptr);
         };

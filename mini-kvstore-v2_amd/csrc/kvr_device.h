@@ -46,7 +46,8 @@ struct SegDesc {          // one caller segment
 };
 
 struct StripeDesc {       // tiles [t_begin, t_end) of segment seg
-    uint32_t seg, t_begin, t_end, pad;
+    uint32_t seg, t_begin, t_end;
+    uint32_t pad;         // 1: the segment's first stripe (k_link)
 };
 
 struct StripeRes {
@@ -59,6 +60,8 @@ struct StripeRes {
     uint32_t forced;      // entry was imposed by k_link (re-walk pass)
     uint32_t owned;       // k_link, before a re-walk pass: bit 0 listed for re-walk, bit 1 inconsistent
                           // (k_replay's re-walk sets 1 on the stripes it walks)
+    uint64_t pool_run;    // the stripe's tuples are pool[pool_run, + count) in order (one chunk), or NONE
+    uint64_t pad;
 };
 
 struct TileRes {          // a tile's tuples in the pool: [pool_off, + count1) then [pool_off2, + count - count1)

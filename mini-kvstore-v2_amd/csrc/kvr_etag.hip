@@ -31,19 +31,32 @@ __global__ void k_etag_map(const uint64_t *__restrict__ cpre, uint64_t n, uint32
         for (uint64_t c = cpre[v]; c < cpre[v + 1]; ++c) chunk_blob[c] = (uint32_t)v;
 }
 
-// The byte tables are k_replay's (kvr_replay_kernel.hip, Crc): slice-by-4 replicated per LDS bank
-// group with the rotation trick, so no lookup of a wave conflicts, plus a 16-replica single-byte
-// table; crc4 / crc1 are k_replay's steps.
+// The byte tables are k_replay's (kvr_replay_kernel.hip, Crc): slice-by-8 (KVR_S8) replicated per
+// LDS bank group with the rotation trick, so no lookup of a wave conflicts; crc4 / crc1 / look8 are
+// k_replay's steps.
 __device__ inline uint32_t crc_word4(const Crc &K, uint32_t c, uint32_t w) { return crc4(c, w, K); }
 
 __device__ inline uint32_t crc_byte(const Crc &K, uint32_t c, uint32_t b) { return crc1(c, b, K); }
 
-// a * K_lane by nibble tables: K[i * 16 + n] = (n << 4i) * K_lane  (8 lookups, no bit loop)
-__device__ inline uint32_t kmul_nib(const uint32_t *K, uint32_t a) {
-    uint32_t r = 0;
+struct __align__(16) EtagSmem {
+    uint32_t C2[256 * 64];   // byte tables (64 KiB, k_replay's Crc layout)
+    uint32_t KL[64 * 128];   // [16 i + n][lane]: (n << 4 i) * x^(8 (4096 - 64 (lane + 1)))
+};
+static_assert(offsetof(EtagSmem, KL) == 65536, "kmul_lane's 64-KiB bit");
+// v times this lane's constant: entry (i, n, lane) at KL + (16 i + n) 256 + 4 lane, the address one
+// v_perm_b32 (byte 0 = 4 lane, byte 1 = i << 4 | n from a nibble plane, byte 2 = the 64-KiB bit)
+__device__ __forceinline__ uint32_t kmul_lane(uint32_t v, const EtagSmem &S, uint32_t lane) {
+    const uint32_t L4k = 4u * lane | 0x10000u;
+    uint32_t pl[2] = {(v & 0x0F0F0F0Fu) | 0x60402000u, ((v >> 4) & 0x0F0F0F0Fu) | 0x70503010u};
+    asm("" : "+v"(pl[0]), "+v"(pl[1]));
+    const uint8_t *tb = reinterpret_cast<const uint8_t *>(&S);
+    uint32_t t[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) r ^= K[i * 16 + ((a >> (4 * i)) & 15u)];
-    return r;
+    for (int i = 0; i < 8; ++i)
+        t[i] = *reinterpret_cast<const uint32_t *>(
+            tb + __builtin_amdgcn_perm(pl[i & 1], L4k, 0x0C020000u | ((4u + (uint32_t)(i >> 1)) << 8)));
+    asm("" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]), "+v"(t[7]));
+    return (t[0] ^ t[1] ^ t[2]) ^ (t[3] ^ t[4] ^ t[5]) ^ (t[6] ^ t[7]);
 }
 
 // One chunk through the general path: any alignment, partial units, bounds-checked loads.
@@ -83,27 +96,17 @@ __global__ __launch_bounds__(64 * ETAG_WPB) void k_etag_chunk(const uint8_t *__r
                                                              const uint32_t *__restrict__ crc_tab,
                                                              const uint32_t *__restrict__ xt,
                                                              uint32_t *__restrict__ creg) {
-    // byte tables in k_replay's Smem::C2 layout (64 KiB, see Crc)
-    __shared__ __align__(16) uint32_t C2[256 * 64];
-    __shared__ uint32_t KL[64 * 128];     // per lane: nibble tables of x^(8 (4096 - 64 (lane + 1)))
-    for (uint32_t i = threadIdx.x; i < 256 * 64; i += blockDim.x) {
-        const uint32_t d = i & 63u, t = d < 32u ? d >> 3 : 0u;
-        C2[i] = crc_tab[t * 256 + (i >> 6)];
-    }
-    for (uint32_t i = threadIdx.x; i < 64 * 128; i += blockDim.x) KL[i] = xt[ETAG_NX + i];
+    // byte tables in k_replay's Smem::C2 layout (64 KiB, see Crc), then per lane the nibble tables
+    // of x^(8 (4096 - 64 (lane + 1))) as columns: entry (i, n, lane) at dword (16 i + n) 64 + lane,
+    // so the 32 lanes of a half-wave read 32 banks whatever their nibbles (kmul_lane)
+    __shared__ EtagSmem S;
+    for (uint32_t i = threadIdx.x; i < 256 * 64; i += blockDim.x) S.C2[i] = crc_tab[c2_table((int)(i & 63u)) * 256 + (i >> 6)];
+    for (uint32_t i = threadIdx.x; i < 64 * 128; i += blockDim.x) S.KL[i] = xt[ETAG_NX + (i & 63u) * 128 + (i >> 6)];
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t *K = KL + lane * 128;
+    const uint32_t *C2 = S.C2;
     Crc T;
-    {
-        const uint32_t g = (lane >> 3) & 3u, r = lane & 7u, r16 = lane & 15u;
-        T.t = reinterpret_cast<const uint8_t *>(C2);
-        T.L = 128u + 4u * r16;
-        T.L4 = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < 4; ++i) T.L4 |= (4u * (8u * ((g + i) & 3u) + r)) << (8 * i);
-        T.rot = (32u - 8u * g) & 31u;
-    }
+    crc_init(T, C2, lane);
     const uint64_t waves = (uint64_t)gridDim.x * ETAG_WPB;
     for (uint64_t base = (blockIdx.x * (uint64_t)ETAG_WPB + (threadIdx.x >> 6)) * ETAG_NC; base < n_chunks;
          base += waves * ETAG_NC) {
@@ -135,6 +138,30 @@ __global__ __launch_bounds__(64 * ETAG_WPB) void k_etag_chunk(const uint8_t *__r
 #pragma unroll
                 for (int i = 0; i < 4; ++i) w[k][i] = q[i];
             }
+#if KVR_S8
+            // slice-by-8: each chain carries its step input x = register ^ word; a step takes x
+            // through tables 7 .. 4 and the next word through 3 .. 0 (8 steps a chunk, not 16)
+            uint32_t x[ETAG_NC];
+#pragma unroll
+            for (int k = 0; k < ETAG_NC; ++k) x[k] = reg[k] ^ w[k][0].x;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                    for (int k = 0; k < ETAG_NC; ++k) {
+                        uint32_t px, x3, py, y3;
+                        look8(x[k], h ? w[k][i].w : w[k][i].y, T, px, x3, py, y3);
+                        if (i < 3 || h == 0) {
+                            const uint32_t nw = h ? w[k][i + (i < 3)].x : w[k][i].z;
+                            x[k] = xor3(px, x3, xor3(py, y3, nw));
+                        } else {
+                            reg[k] = xor3(px, x3, py ^ y3);
+                        }
+                    }
+                }
+            }
+#else
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -146,9 +173,10 @@ __global__ __launch_bounds__(64 * ETAG_WPB) void k_etag_chunk(const uint8_t *__r
 #pragma unroll
                 for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].w);
             }
+#endif
             if (lane != 63) {
 #pragma unroll
-                for (int k = 0; k < ETAG_NC; ++k) reg[k] = kmul_nib(K, reg[k]);
+                for (int k = 0; k < ETAG_NC; ++k) reg[k] = kmul_lane(reg[k], S, lane);
             }
         } else {
 #pragma unroll 1

@@ -30,75 +30,100 @@ __device__ __forceinline__ uint64_t stripe_lo(const StripeDesc &d, const SegDesc
     return l < 0 ? 0ull : (uint64_t)l;
 }
 
+// segments whose first-problem stripes k_link keeps in LDS (more: in the global arrays)
+constexpr uint32_t LINK_LSEG = 4096;
+
 __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, uint32_t n_segs,
                                              const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
                                              StripeRes *__restrict__ sres, RedoEnt *__restrict__ redo,
-                                             uint32_t redo_cap, LinkResult *res, uint32_t *seg_bad,
-                                             uint32_t *seg_err, uint32_t tile, uint64_t *__restrict__ soff,
+                                             uint32_t redo_cap, LinkResult *res, uint32_t *seg_bad_g,
+                                             uint32_t *seg_err_g, uint32_t tile, uint64_t *__restrict__ soff,
                                              Counters *ctr) {
     __shared__ int32_t wm[LT / 64];
+    __shared__ uint64_t wx[LT / 64];
     __shared__ unsigned long long wsum[LT / 64];
     __shared__ uint32_t first_problem, nredo;
+    __shared__ uint32_t l_bad[LINK_LSEG], l_err[LINK_LSEG];
+    // per segment: its first inconsistent stripe and its first error stripe (LDS for the usual
+    // segment counts; flat pointers, so the atomics below serve both)
+    uint32_t *const seg_bad = n_segs <= LINK_LSEG ? l_bad : seg_bad_g;
+    uint32_t *const seg_err = n_segs <= LINK_LSEG ? l_err : seg_err_g;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (uint32_t g = tid; g < n_segs; g += LT) { seg_bad[g] = ~0u; seg_err[g] = ~0u; }
     if (tid == 0) { first_problem = ~0u; nredo = 0; }
     const uint32_t per = (n_stripes + LT - 1) / LT;
     const uint32_t b = tid * per, e = min(b + per, n_stripes);
-    // this thread's chunk: its last stripe with a record start, and its stripes' records (the
-    // output offsets k_compact_s writes from); exclusive scans over the chunks, a max and a sum,
-    // by wave shuffles and then the 16 wave totals
+    // this thread's chunk: its last stripe with a record start (and that stripe's exit), and its
+    // stripes' records (the output offsets k_compact_s writes from); exclusive scans over the
+    // chunks, a "latest" and a sum, by wave shuffles and then the 16 wave totals, so no stripe
+    // result is read twice and none after the scan
     // (up to KL stripes per thread, the common case: their results and descriptors are loaded
     // once, all together, and kept in registers for the passes below)
     constexpr int KL = 4;
     const bool cached = per <= (uint32_t)KL;
     uint64_t c_entry[KL], c_exit[KL];
-    uint32_t c_kind[KL], c_count[KL], c_seg[KL], c_tb[KL], c_te[KL];
+    uint32_t c_kind[KL], c_count[KL], c_seg[KL], c_tb[KL], c_te[KL], c_first[KL];
     if (cached) {
 #pragma unroll
         for (int i = 0; i < KL; ++i) {
             const uint32_t s = b + i;
             c_entry[i] = NONE; c_exit[i] = NONE; c_kind[i] = 0; c_count[i] = 0; c_seg[i] = 0; c_tb[i] = 0; c_te[i] = 0;
+            c_first[i] = 0;
             if (s < e) {
                 c_entry[i] = sres[s].entry; c_exit[i] = sres[s].exit; c_kind[i] = sres[s].err_kind;
                 c_count[i] = sres[s].count;
                 const StripeDesc d = stripes[s];
-                c_seg[i] = d.seg; c_tb[i] = d.t_begin; c_te[i] = d.t_end;
+                c_seg[i] = d.seg; c_tb[i] = d.t_begin; c_te[i] = d.t_end; c_first[i] = d.pad;
             }
         }
     }
     int32_t m = -1;
+    uint64_t mx = NONE;   // the exit of stripe m
     unsigned long long mine = 0;
     if (cached) {
 #pragma unroll
         for (int i = 0; i < KL; ++i) {
-            if (b + i < e && c_entry[i] != NONE) m = (int32_t)(b + i);
+            if (b + i < e && c_entry[i] != NONE) { m = (int32_t)(b + i); mx = c_exit[i]; }
             mine += c_count[i];
         }
     } else {
         for (uint32_t s = b; s < e; ++s) {
-            if (sres[s].entry != NONE) m = (int32_t)s;
-            mine += sres[s].count;
+            const StripeRes r = sres[s];
+            if (r.entry != NONE) { m = (int32_t)s; mx = r.exit; }
+            mine += r.count;
         }
     }
     int32_t im = m;
+    uint64_t ix = mx;
     unsigned long long is = mine;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const int32_t om = __shfl_up(im, d, 64);
+        const uint64_t ox = __shfl_up(ix, d, 64);
         const unsigned long long os = __shfl_up(is, d, 64);
-        if (lane >= d) { im = om > im ? om : im; is += os; }
+        if (lane >= d) {
+            if (om > im) { im = om; ix = ox; }
+            is += os;
+        }
     }
-    if (lane == 63) { wm[wv] = im; wsum[wv] = is; }
+    if (lane == 63) { wm[wv] = im; wx[wv] = ix; wsum[wv] = is; }
     __syncthreads();
     int32_t pm = -1;
+    uint64_t px = NONE;
     unsigned long long ps = 0, all_recs = 0;
     for (int i = 0; i < LT / 64; ++i) {
-        if (i < wv) { pm = wm[i] > pm ? wm[i] : pm; ps += wsum[i]; }
+        if (i < wv) {
+            if (wm[i] > pm) { pm = wm[i]; px = wx[i]; }
+            ps += wsum[i];
+        }
         all_recs += wsum[i];
     }
     const int32_t xm = __shfl_up(im, 1, 64);
+    const uint64_t xx = __shfl_up(ix, 1, 64);
     const unsigned long long xs = __shfl_up(is, 1, 64);
-    const int32_t run0 = lane ? (xm > pm ? xm : pm) : pm;   // the last stripe with records before the chunk
+    int32_t run0 = pm;                       // the last stripe with records before the chunk ...
+    uint64_t xrun0 = px;                     // ... and its exit
+    if (lane && xm > pm) { run0 = xm; xrun0 = xx; }
     if (soff) {
         unsigned long long at = (lane ? xs : 0ull) + ps;
         if (cached) {
@@ -112,23 +137,19 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
     // pass 1: consistency of every stripe with its predecessor's exit
     int32_t run = run0;
     if (cached) {
-        SegDesc gc[KL];
-#pragma unroll
-        for (int i = 0; i < KL; ++i) if (b + i < e) gc[i] = segs[c_seg[i]];
-        uint64_t xrun = run0 >= 0 ? sres[run0].exit : NONE;   // the exit of stripe `run`
+        uint64_t xrun = run0 >= 0 ? xrun0 : NONE;   // the exit of stripe `run`
 #pragma unroll
         for (int i = 0; i < KL; ++i) {
             const uint32_t s = b + i;
             if (s >= e) break;
             StripeDesc d;
             d.seg = c_seg[i]; d.t_begin = c_tb[i]; d.t_end = c_te[i]; d.pad = 0;
-            const SegDesc &g = gc[i];
-            const bool first = (s == g.stripe0);
+            const bool first = c_first[i] != 0u;    // (the host marks a segment's first stripe)
             bool bad = false, after_err = false;
             if (!first) {
                 const uint64_t xp = run >= 0 ? xrun : NONE;
                 if (xp == ERRP) after_err = true;
-                else if (c_entry[i] == NONE) bad = xp < stripe_hi(d, g, tile);
+                else if (c_entry[i] == NONE) bad = xp < stripe_hi(d, segs[d.seg], tile);   // (a pass-through stripe)
                 else bad = (c_entry[i] != xp);
             }
             if (bad && !after_err) atomicMin(&seg_bad[d.seg], s);
@@ -252,6 +273,7 @@ constexpr int CB = CT;            // tiles per chunk of k_compact_s
 // its thread also does the expected-CRC check, and moves the key prefix when the call keeps one
 // (kpool -> kout, the fold's keys).
 __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ segs, const StripeDesc *__restrict__ stripes,
+                                                  const StripeRes *__restrict__ sres,
                                                   const uint64_t *__restrict__ soff, const TileRes *__restrict__ tres,
                                                   const kvr_tuple *__restrict__ pool, uint64_t pool_cap,
                                                   kvr_tuple *__restrict__ out, uint64_t out_cap,
@@ -261,11 +283,33 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
     if (link->status != 0 || ctr->overflow) return;
     __shared__ uint64_t off[CB + 1];
     __shared__ uint64_t part[CT];
+    uint32_t fails = 0;
+    // the tuple of output slot o from pool slot src: half k2 & 1 per thread, the manifest check
+    // on the second half (a SET: op in byte 0 of w), the key prefix beside it
+    auto move = [&](uint64_t src, uint64_t o, uint32_t half) {
+        if (src >= pool_cap) return;
+        uint4 v = reinterpret_cast<const uint4 *>(pool + src)[half];
+        if (half && expected && o < n_expected && (v.w & 255u) == 0u) {
+            v.w |= KVR_TF_VERIFIED << 8;
+            if (expected[o] != v.y) { v.w |= KVR_TF_CRC_FAIL << 8; ++fails; }
+        }
+        if (o < out_cap) {
+            reinterpret_cast<uint4 *>(out + o)[half] = v;
+            if (half && kout) kout[o] = kpool[src];
+        }
+    };
+    const uint64_t run = sres[blockIdx.x].pool_run;
+    if (run != NONE) {   // the stripe's tuples are one run of the pool: a straight copy
+        const uint64_t n = sres[blockIdx.x].count, o0 = soff[blockIdx.x];
+        for (uint64_t k2 = threadIdx.x; k2 < 2 * n; k2 += CT) move(run + (k2 >> 1), o0 + (k2 >> 1), (uint32_t)k2 & 1u);
+        for (int d = 32; d >= 1; d >>= 1) fails += __shfl_xor(fails, d, 64);
+        if ((threadIdx.x & 63) == 0 && fails) atomicAdd(&ctr->crc_fail, (unsigned long long)fails);
+        return;
+    }
     const StripeDesc sd = stripes[blockIdx.x];
     const uint32_t tile0 = segs[sd.seg].tile0;
     const uint32_t t_end = tile0 + sd.t_end;
     uint64_t carry = soff[blockIdx.x];
-    uint32_t fails = 0;
     for (uint32_t tb = tile0 + sd.t_begin; tb < t_end; tb += CB) {
         const uint32_t nt = min((uint32_t)CB, t_end - tb);
         const uint32_t t = tb + threadIdx.x;
@@ -294,16 +338,7 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
             const TileRes &tr = tres[tb + lo_i];
             const uint64_t r = o - off[lo_i];
             const uint64_t src = r < tr.count1 ? tr.pool_off + r : tr.pool_off2 + (r - tr.count1);
-            if (src >= pool_cap) continue;
-            uint4 v = reinterpret_cast<const uint4 *>(pool + src)[half];
-            if (half && expected && o < n_expected && (v.w & 255u) == 0u) {   // a SET: op in byte 0 of w
-                v.w |= KVR_TF_VERIFIED << 8;
-                if (expected[o] != v.y) { v.w |= KVR_TF_CRC_FAIL << 8; ++fails; }
-            }
-            if (o < out_cap) {
-                reinterpret_cast<uint4 *>(out + o)[half] = v;
-                if (half && kout) kout[o] = kpool[src];
-            }
+            move(src, o, half);
         }
         carry += ctotal;
         __syncthreads();   // (off and part are rewritten by the next chunk)

@@ -92,6 +92,15 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #ifndef KVR_LANEFRAME   // 1: lane-parallel framing (0: the exact scalar hop loop for every record)
 #define KVR_LANEFRAME 1
 #endif
+#ifndef KVR_S8   // 1: slice-by-8 unit loop (8 table lookups per 8 bytes, half the dependent LDS steps)
+#define KVR_S8 1
+#endif
+#ifndef KVR_PSEL   // 1: per-lane v_perm selectors pick each lane group's byte (no rotation of x per step)
+#define KVR_PSEL 1
+#endif
+#ifndef KVR_CANDFRAME   // 1: candidate-chain rounds for what the stride round leaves (records of varying lengths)
+#define KVR_CANDFRAME 1
+#endif
 #ifndef KVR_TOPWAIT   // 1: wait for the tile's load at the top of the loop (0: where its registers are
 #define KVR_TOPWAIT 0   // first read, so the framing round's window loads go out under the tile's load;
 #endif                  // cfg2 1.326-1.332 vs 1.334-1.342 ms, cfg4 1.805-1.819 vs 1.813-1.857, medians)
@@ -154,23 +163,109 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {   // (every lane gets
     return rl32(v, 63);
 }
 
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {   // inclusive prefix sum over the lanes
+    v += dpp<0x111>(v);
+    v += dpp<0x112>(v);
+    v += dpp<0x114>(v);
+    v += dpp<0x118>(v);
+    v += dpp<0x142, 0xA, false>(v);
+    v += dpp<0x143, 0xC, false>(v);
+    return v;
+}
+
+// Record-start candidates of a lane's unit w (SWAR over its 32 registers): byte b of word i is one
+// when it is an opcode byte (0x00 / 0x01) and the byte 4 on -- the top byte of the key length that
+// would follow -- does not exceed the top byte of rem (the segment bytes left from the tile start;
+// a necessary condition for a valid record, engine.rs:96-107).  cm[g] bit 8 b + j: byte b of word
+// 8 g + j, i.e. unit offset 32 g + 4 j + b.  (The unit's last word is not bounded by its next.)
+__device__ __forceinline__ void cand_masks(const uint32_t (&w)[UW], int64_t rem, uint32_t (&cm)[4]) {
+    const int32_t rc = rem > 0x7FFFFFFFll ? 0x7FFFFFFF : (int32_t)rem;
+    const uint32_t addT = (0x7Fu - ((uint32_t)rc >> 24)) * 0x01010101u;
+    cm[0] = cm[1] = cm[2] = cm[3] = 0u;
+#pragma unroll
+    for (int i = 0; i < UW; ++i) {
+        // bit 7 of a byte: the byte is 0x00 / 0x01 (no carry leaves a byte: (b & 0x7E) + 0x7F <= 0xFD)
+        uint32_t z = ~(((w[i] & 0x7E7E7E7Eu) + 0x7F7F7F7Fu) | w[i] | 0x7F7F7F7Fu);
+        if (i + 1 < UW) {                              // bytes above the bound set their 0x80 bit
+            const uint32_t x = w[i + 1];
+            z &= ~((((x & 0x7F7F7F7Fu) + addT) | x));
+        }
+        cm[i >> 3] |= z >> (7 - (i & 7));
+    }
+}
+// keep only the candidates at unit offsets below lim (any lim; <= 0 clears all)
+__device__ __forceinline__ void mask_from(uint32_t (&cm)[4], int32_t lim) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        uint32_t mk = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {   // offsets 32 g + 4 j + b < lim  <=>  j < ceil((lim - 32 g - b) / 4)
+            int32_t nj = (lim - 32 * g - b + 3) >> 2;
+            nj = nj < 0 ? 0 : (nj > 8 ? 8 : nj);
+            mk |= ((1u << nj) - 1u) << (8 * b);
+        }
+        cm[g] &= mk;
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // CRC primitives
 // ---------------------------------------------------------------------------------------
 // Row b of Smem::C2 (64 dwords):
 //   [0, 32):  dword 8 t + r = table t (t = 0: one byte, t = k: a byte then k zero bytes) for byte
-//             b, replica r < 8 -- the slice-by-4 set of the unit loop
-//   [32, 48): table 0, replica lane & 15 (single-byte steps)
+//             b, replica r < 8 -- the slice-by-4 set
+//   [32, 64): KVR_S8: tables 4 .. 7 the same way (the slice-by-8 set of the unit loop: a step
+//             takes the register-folded word through tables 7 .. 4 and the next word through
+//             3 .. 0); otherwise [32, 48) is table 0, replica lane & 15 (single-byte steps)
 // A slice-by-4 step x = c ^ w needs T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3].  Lane group
 // g = (lane >> 3) & 3 takes table (g + i) & 3 in its i-th lookup and replica lane & 7, so the 32
 // lanes of a half-wave hit 32 distinct banks in every lookup; the group's byte order is absorbed
 // by rotating x left by 8 g first (one v_alignbit), which keeps the four selectors uniform.
 struct Crc {
     const uint8_t *t;   // Smem::C2
-    uint32_t L;         // byte 0: T0 copy (128 + 4 (lane & 15))
+    uint32_t L;         // byte 0: T0 copy (KVR_S8: 4 (lane & 7); else 128 + 4 (lane & 15))
     uint32_t L4;        // byte i: 4 (8 ((g + i) & 3) + (lane & 7)), this lane's i-th slice-by-4 lookup
+    uint32_t L4x;       // L4 + 128 per byte: the same lookups in tables 4 .. 7 (KVR_S8)
+#if KVR_PSEL
+    uint32_t sel[4];    // lookup i's v_perm selector: byte 0 = L4's byte i, byte 1 = x's byte 3 - ((g + i) & 3)
+#else
     uint32_t rot;       // (32 - 8 g) & 31: x rotated right by this = x rotated left by 8 g
+#endif
 };
+// the C2 entry (dword) of LDS row b, column d: which table it holds (the staging loops)
+__host__ __device__ constexpr int c2_table(int d) { return KVR_S8 ? (d >> 3) : (d < 32 ? (d >> 3) : 0); }
+__device__ __forceinline__ void crc_init(Crc &K, const uint32_t *C2, uint32_t lane) {
+    const uint32_t g = (lane >> 3) & 3u, r = lane & 7u, r16 = lane & 15u;
+    K.t = reinterpret_cast<const uint8_t *>(C2);
+    K.L = KVR_S8 ? 4u * r : 128u + 4u * r16;
+    K.L4 = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) K.L4 |= (4u * (8u * ((g + i) & 3u) + r)) << (8 * i);
+    K.L4x = K.L4 + 0x80808080u;
+#if KVR_PSEL
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) K.sel[i] = 0x0C0C0000u | ((7u - ((g + i) & 3u)) << 8) | i;
+#else
+    K.rot = (32u - 8u * g) & 31u;
+#endif
+}
+// the byte order a lookup selector expects: x itself (KVR_PSEL) or x rotated left by 8 g
+__device__ __forceinline__ uint32_t crc_rot(uint32_t x, const Crc &k) {
+#if KVR_PSEL
+    (void)k;
+    return x;
+#else
+    return __builtin_amdgcn_alignbit(x, x, k.rot);
+#endif
+}
+__device__ __forceinline__ uint32_t crc_sel(const Crc &k, uint32_t i) {
+#if KVR_PSEL
+    return k.sel[i];
+#else
+    (void)k;
+    return 0x0C0C0000u | ((7u - i) << 8) | i;
+#endif
+}
 // v_perm_b32 builds the LDS address: byte 1 = a byte of x, byte 0 = this lane's table copy
 constexpr uint32_t SEL_T0_B0 = 0x0C0C0400u;
 __device__ __forceinline__ uint32_t tget(const Crc &k, uint32_t x, uint32_t sel) {
@@ -184,13 +279,12 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {  
 // lookup i of a slice-by-4 step on xr = x rotated left by 8 g: byte 1 = xr byte 3 - i, which
 // is x byte 3 - ((g + i) & 3), the byte table (g + i) & 3 takes
 __device__ __forceinline__ uint32_t s4get(const Crc &k, uint32_t xr, uint32_t i) {
-    return *reinterpret_cast<const uint32_t *>(
-        k.t + __builtin_amdgcn_perm(xr, k.L4, 0x0C0C0000u | ((7u - i) << 8) | i));
+    return *reinterpret_cast<const uint32_t *>(k.t + __builtin_amdgcn_perm(xr, k.L4, crc_sel(k, i)));
 }
 // (the four lookups are issued before any is used: the empty asm keeps the scheduler from
 // serialising them; it is not volatile, so independent chains still interleave around it)
 __device__ __forceinline__ uint32_t crc4(uint32_t c, uint32_t w, const Crc &k) {
-    const uint32_t x = c ^ w, xr = __builtin_amdgcn_alignbit(x, x, k.rot);
+    const uint32_t x = c ^ w, xr = crc_rot(x, k);
     uint32_t a0 = s4get(k, xr, 0), a1 = s4get(k, xr, 1), a2 = s4get(k, xr, 2), a3 = s4get(k, xr, 3);
     asm("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
     return xor3(a0, a1, a2) ^ a3;
@@ -202,7 +296,7 @@ __device__ __forceinline__ uint32_t bitop3_xandn(uint32_t a, uint32_t b, uint32_
 // step's result is ta ^ a3 (tb ^ b3), and the next step's input that ^ the next word, one v_bitop3
 __device__ __forceinline__ void look4x2(uint32_t xa, uint32_t xb, const Crc &k, uint32_t &ta, uint32_t &a3, uint32_t &tb,
                                         uint32_t &b3) {
-    const uint32_t ra = __builtin_amdgcn_alignbit(xa, xa, k.rot), rb = __builtin_amdgcn_alignbit(xb, xb, k.rot);
+    const uint32_t ra = crc_rot(xa, k), rb = crc_rot(xb, k);
     uint32_t a0 = s4get(k, ra, 0), a1 = s4get(k, ra, 1), a2 = s4get(k, ra, 2), a3_ = s4get(k, ra, 3);
     uint32_t b0 = s4get(k, rb, 0), b1 = s4get(k, rb, 1), b2 = s4get(k, rb, 2), b3_ = s4get(k, rb, 3);
     asm("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3_), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3_));
@@ -210,6 +304,25 @@ __device__ __forceinline__ void look4x2(uint32_t xa, uint32_t xb, const Crc &k, 
     a3 = a3_;
     tb = xor3(b0, b1, b2);
     b3 = b3_;
+}
+// slice-by-8: the lookups of one step for two chains, x (register folded into the word) through
+// tables 7 .. 4 and y (the next word, no register) through tables 3 .. 0.  The step's result is
+// xor3(px, x3, xor3(py, y3, next word)): the y half does not wait for the chain, so the compiler
+// may issue it early.
+__device__ __forceinline__ uint32_t s8get(const Crc &k, uint32_t xr, uint32_t i) {
+    return *reinterpret_cast<const uint32_t *>(k.t + __builtin_amdgcn_perm(xr, k.L4x, crc_sel(k, i)));
+}
+__device__ __forceinline__ void look8(uint32_t x, uint32_t y, const Crc &k, uint32_t &px, uint32_t &x3, uint32_t &py,
+                                      uint32_t &y3) {
+    const uint32_t xr = crc_rot(x, k), yr = crc_rot(y, k);
+    uint32_t b0 = s4get(k, yr, 0), b1 = s4get(k, yr, 1), b2 = s4get(k, yr, 2), b3 = s4get(k, yr, 3);
+    uint32_t a0 = s8get(k, xr, 0), a1 = s8get(k, xr, 1), a2 = s8get(k, xr, 2), a3 = s8get(k, xr, 3);
+    asm("" : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
+    asm("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
+    px = xor3(a0, a1, a2);
+    x3 = a3;
+    py = xor3(b0, b1, b2);
+    y3 = b3;
 }
 __device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
     const uint32_t x = c ^ b;
@@ -660,10 +773,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
     constexpr bool redo_mode = REDO;
     __shared__ Smem S;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    for (int i = tid; i < 256 * 64; i += RT) {
-        const int d = i & 63, t = d < 32 ? d >> 3 : 0;
-        S.C2[i] = tb.crc8[t * 256 + (i >> 6)];
-    }
+    for (int i = tid; i < 256 * 64; i += RT) S.C2[i] = tb.crc8[c2_table(i & 63) * 256 + (i >> 6)];
     for (int i = tid; i < 8 * 16 * 64; i += RT)
         S.KR[i] = tb.kmul[((KSET_R + (i & 63)) * 8 + (i >> 10)) * 16 + ((i >> 6) & 15)];
     for (int i = tid; i < 8 * 16 * 64; i += RT) {
@@ -676,15 +786,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
     uint32_t *const MK = S.MK[wv];   // this wave's long-value marks
 
     Crc K;
-    {
-        const uint32_t g = (uint32_t)(lane >> 3) & 3u, r = (uint32_t)lane & 7u, r16 = (uint32_t)lane & 15u;
-        K.t = reinterpret_cast<const uint8_t *>(S.C2);
-        K.L = 128u + 4u * r16;
-        K.L4 = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < 4; ++i) K.L4 |= (4u * (8u * ((g + i) & 3u) + r)) << (8 * i);
-        K.rot = (32u - 8u * g) & 31u;
-    }
+    crc_init(K, S.C2, (uint32_t)lane);
     // the stripe index is wave-uniform: say so, so that the whole stripe state lives in SGPRs
     const uint32_t gw = blockIdx.x * WPB + (uint32_t)__builtin_amdgcn_readfirstlane(wv);
     uint32_t si;
@@ -730,6 +832,8 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
     uint32_t err_kind = 0, total = 0;
     uint32_t stride = 0, fast_skip = 0;           // lane-parallel framing: the last record length, tiles
                                                   // left to the scalar hop loop
+    uint32_t run_first = N32;                     // the stripe's first pool slot, while its tuples are one run
+    bool run_contig = true;                       // (no second chunk claimed after its first tuple)
     uint32_t carry = 0, c_state = 0;              // 1: a long value crosses the tile start (c_state: its register);
     uint64_t c_vb = 0, c_ve = 0;                  // 2: pending (its value starts in a later tile)
     uint32_t c_slot = 0;
@@ -784,19 +888,8 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             // byte of the segment bytes left: a necessary condition, word-wide (SWAR).  plausible()
             // (memory reads, the exact tests) runs on the survivors alone.  cm[g] bit 8 b + j:
             // byte 4 (8 g + j) + b of the lane's unit.
-            const int32_t rc = rem > 0x7FFFFFFFll ? 0x7FFFFFFF : (int32_t)rem;
-            const uint32_t addT = (0x7Fu - ((uint32_t)rc >> 24)) * 0x01010101u;
-            uint32_t cm[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-            for (int i = 0; i < UW; ++i) {
-                const uint32_t y = w[i] & 0xFEFEFEFEu;            // bytes 0x00 / 0x01 become 0
-                uint32_t z = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
-                if (i + 1 < UW) {                              // bytes above the bound set their 0x80 bit
-                    const uint32_t x = w[i + 1];
-                    z &= ~((((x & 0x7F7F7F7Fu) + addT) | x));
-                }
-                cm[i >> 3] |= z >> (7 - (i & 7));
-            }
+            uint32_t cm[4];
+            cand_masks(w, rem, cm);
             // each round every lane tests one survivor, so the lanes' plausible() calls (dependent
             // loads) run side by side; a lane keeps its lowest plausible start, and lanes above the
             // lowest lane holding one stop (unit positions grow with the lane)
@@ -874,19 +967,21 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 chunk_base = uni32((uint32_t)bb);
                 chunk_left = cm;
                 if (nrec) { b2 = chunk_base; c1 = nrec; }   // the tile's second run
+                if (run_first != N32) run_contig = false;
             }
+            if (run_first == N32 && nb) run_first = chunk_base;
             if (nrec == 0) b1 = chunk_base;
             const uint32_t s0 = chunk_base;
             chunk_base += nb;
             chunk_left -= nb;
             return s0;
         };
-        // a batch's long values crossing a unit boundary: each marks its first unit with its lane
-        // + 1 (lmark); one DPP prefix max over the units finds, for every unit, the last one
-        // starting at or before it (and, shifted by one lane, before it); two ds_bpermute fetch
-        // that record's value span from its lane.  Long values are disjoint and in order (lane
-        // order = position order), so these are the only candidates.  rank: the record's index
-        // within the tile's records so far, per lane.
+        // a batch's long values crossing a unit boundary: each marks its first unit with
+        // (rank + 1) << 6 | its lane (lmark; rank order = position order); one DPP prefix max over
+        // the units finds, for every unit, the last one starting at or before it (and, shifted by
+        // one lane, before it); two ds_bpermute fetch that record's value span from its lane.  Long
+        // values are disjoint and in order, so these are the only candidates.  rank: the record's
+        // index within the tile's records so far, per lane.
         auto fold_views = [&](uint32_t lmark, int32_t rvb, int32_t re2, uint32_t rank) {
             uint32_t pm = lmark;
             pm = __builtin_elementwise_max(pm, dpp<0x111>(pm));
@@ -896,7 +991,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             pm = __builtin_elementwise_max(pm, dpp<0x142, 0xA, false>(pm));
             pm = __builtin_elementwise_max(pm, dpp<0x143, 0xC, false>(pm));
             const uint32_t pp = dpp<0x138>(pm);   // wave_shr:1: the marks before this unit
-            const int ic = 4 * (int)(pm ? pm - 1u : 0u), ip = 4 * (int)(pp ? pp - 1u : 0u);
+            const int ic = 4 * (int)(pm & 63u), ip = 4 * (int)(pp & 63u);   // (the marks' lanes)
             const int32_t vbc = __builtin_amdgcn_ds_bpermute(ic, rvb), e2c = __builtin_amdgcn_ds_bpermute(ic, re2);
             const int32_t e2p = __builtin_amdgcn_ds_bpermute(ip, re2);
             const uint32_t rkp = (uint32_t)__builtin_amdgcn_ds_bpermute(ip, (int)rank);
@@ -958,167 +1053,205 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             if (KVR_ABLATE & 4) p = vhi_r;
             if (KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
 #if KVR_LANEFRAME
+            // ---- lane-parallel framing ---------------------------------------------------------------
+            // decode(c): the record that would start at tile offset c (per lane; act: the lane takes
+            // part), from a window of the segment bytes: opcode, key length, value length, every
+            // engine.rs framing check, and where its successor starts.  The value-length field is read
+            // out of the window for the key length of lane kl (one length for every key is the usual
+            // case); a lane with another key length reads it from memory (vmem) or leaves its
+            // successor unknown (nx = UNK, resolved when the chain reaches it).
+            struct Dec {
+                uint32_t win[WINW];
+                uint32_t s, op, klen, vlen, vb, nx;
+                bool ok;
+            };
+            constexpr uint32_t UNK = 0xFFFFFFFEu;
+            const int32_t vhiT = (int32_t)vhi_r, remT = (int32_t)rem;   // (used only when !huge)
+            auto decode = [&](int32_t c, bool act, int kl, bool vmem) -> Dec {
+                Dec d;
+                const int32_t a = c & ~3;
+                d.s = (uint32_t)c & 3u;
+#pragma unroll
+                for (int i = 0; i < WINW; ++i) d.win[i] = act ? ts.w32a(a + 4 * i) : 0u;
+                const uint32_t x0 = __builtin_amdgcn_alignbyte(d.win[1], d.win[0], d.s);
+                const uint32_t x1 = __builtin_amdgcn_alignbyte(d.win[2], d.win[1], d.s);
+                d.op = x0 & 255u;
+                d.klen = (x0 >> 8) | (x1 << 24);
+                // engine.rs framing checks, tile-relative in 32 bits (rem < 2^31)
+                const uint32_t room = (uint32_t)(remT - c);
+                bool ok = act && d.op <= 1u && c < vhiT && room >= 5u && d.klen <= room - 5u;
+                const uint32_t e = (uint32_t)c + 5u + (ok ? d.klen : 0u);   // < 2^31
+                const bool need_v = ok && d.op == 0u;
+                ok = ok && (!need_v || (uint32_t)remT - e >= 4u);
+                const uint32_t ku = rl32(d.klen, kl);
+                d.vlen = 0;
+                bool vdone = false;
+                {
+                    const uint32_t dd = 5u + ku, B0 = dd >> 2;
+                    if (B0 >= 1u && B0 <= (uint32_t)(WINW - 3)) {
+                        uint32_t wa = 0, wb = 0, wc = 0;
+#pragma unroll
+                        for (int bb = 1; bb <= WINW - 3; ++bb)
+                            if (B0 == (uint32_t)bb) { wa = d.win[bb]; wb = d.win[bb + 1]; wc = d.win[bb + 2]; }
+                        const uint32_t oo = d.s + (dd & 3u);
+                        const bool cy = oo >= 4u;
+                        d.vlen = __builtin_amdgcn_alignbyte(cy ? wc : wb, cy ? wb : wa, oo & 3u);
+                        vdone = d.klen == ku;
+                    }
+                }
+                bool unk = false;
+                if (need_v && ok && !vdone) {
+                    if (vmem) d.vlen = ts.u32((int64_t)e);
+                    else unk = true;
+                }
+                d.vb = e + 4u;
+                ok = ok && (!need_v || unk || d.vlen <= (uint32_t)remT - d.vb);
+                d.ok = ok;
+                d.nx = unk ? UNK : (d.op == 1u ? e : d.vb + d.vlen);
+                return d;
+            };
+            // emit: the records of a framing round.  Lane j with `on` emits record nrec + rk (rk: its
+            // rank on the chain, rank order = position order); lead / lastl: the lanes of the round's
+            // first and last records.  strided: record j starts at cur0 + j L (the stride round), so the
+            // long values of a round of equal SETs fold into the units by arithmetic.
+            // (it calls no other lambda: the caller claims the pool slots and runs the long-value
+            // fold it asks for, so no closure object has to live in memory)
+            struct Fold { uint32_t lmark; int kind; };   // kind 0: none, 1: fold_uniform, 2: fold_views
+            auto emit = [&](const Dec &d, int32_t c, bool on, uint32_t rk, uint32_t n_on, int lead, int lastl,
+                            bool strided, uint32_t slot0) -> Fold {
+                if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
+                const uint32_t klen = d.klen, op = d.op, vlen = d.vlen, vb = d.vb, s = d.s;
+                Fold fo{0u, 0};
+                // one key length for the batch (the first record's, ku): no per-lane byte masks
+                const uint32_t ku = rl32(klen, lead);
+                const bool kuni = __ballot(on && klen != ku) == 0ull && ku <= 4u * KEYW;
+                const uint32_t kmx = kuni ? ku : wave_max(on ? klen : 0u);
+                uint32_t rerr = N32, rkind = 0;
+                uint64_t raux = 0;
+                if (on && !(KVR_ABLATE & 1)) {
+                    const uint32_t kc = kmx > 4u * KEYW ? 4u * KEYW : kmx;
+                    const uint32_t nw = (kc + 3u) >> 2;   // key words of the longest key
+                    uint32_t kr[KEYW + 1];
+#pragma unroll
+                    for (int i = 0; i <= KEYW; ++i) kr[i] = s == 3u ? d.win[i + 2] : d.win[i + 1];
+                    const int kb = c + 5;
+                    uint32_t cc = ~0u, bad = 0x80u;
+                    if (kuni) cc = crc_words_u<KEYW>(kr, K, (s + 1u) & 3u, ku, &bad);
+                    else if (klen <= 4u * KEYW) cc = crc_words<KEYW>(kr, K, (s + 1u) & 3u, klen, nw, &bad);
+                    if (bad != 0u) {              // non-ASCII or long key: the full UTF-8 check
+                        uint64_t vu = 0;
+                        uint32_t el = 0;
+                        if (!utf8_check(ts, kb, klen, &vu, &el)) {   // engine.rs:114
+                            rerr = nrec + rk; rkind = KVR_E_UTF8; raux = vu | ((uint64_t)el << 32);
+                        } else {
+                            cc = crc_long(ts, ~0u, kb, klen, K);
+                        }
+                    }
+                    if (rerr == N32) {
+                        kvr_tuple t;
+                        t.rec_off = (uint64_t)(lo + c);
+                        t.seg_idx = sd.seg;
+                        t.key_len = klen;
+                        t.val_len = op == 0u ? vlen : 0u;
+                        t.crc32 = op == 0u ? short_value_crc(ts, K, (int)vb, vlen) : 0u;
+                        t.key_tag = ~cc;
+                        t.op = (uint8_t)op;
+                        t.flags = 0;
+                        t.reserved = 0;
+                        pool[slot0 + rk] = t;
+                        // the key prefix for the fold (only calls that fold ask for it)
+                        if (kpool) kpool[slot0 + rk] = key_prefix_words(kr, (s + 1u) & 3u, klen);
+                    }
+                }
+                // long values crossing a unit boundary: marked at their first unit (a scatter through
+                // this wave's LDS row; the mark carries the rank, so the prefix max finds the latest,
+                // and the lane), then folded into every unit's view
+                const bool lv = on && op == 0u && vlen > (uint32_t)SMALL && ((vb ^ (vb + vlen - 1u)) >> SC_LOG) != 0u;
+                const uint64_t lvm = __ballot(lv);
+                // a round of SETs of one key and one value length (longer than a unit)
+                const uint32_t vu = rl32(vlen, lead);
+                const bool vuni = KVR_UNIFOLD && strided && vu > (uint32_t)SC &&
+                                  __ballot(on && (op != 0u || vlen != vu || klen != ku)) == 0ull;
+                if (lvm && !(KVR_ABLATE & 32)) {
+                    uint32_t lmark = 0;
+                    if (!vuni) {
+                        MK[lane] = 0u;
+                        __builtin_amdgcn_wave_barrier();
+                        if (lv && vb < (uint32_t)TILE) MK[vb >> SC_LOG] = ((rk + 1u) << 6) | (uint32_t)lane;
+                        __builtin_amdgcn_wave_barrier();
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        lmark = MK[lane];
+                    }
+                    // a long value starting past the tile end (only the last record's): carried
+                    if ((lvm >> lastl) & 1ull) {
+                        const uint32_t vbl = rl32(vb, lastl);
+                        if (vbl >= (uint32_t)TILE) {
+                            n_carry = 2; n_vb = (uint64_t)(lo + (int64_t)vbl);
+                            n_ve = (uint64_t)(lo + (int64_t)vbl + rl32(vlen, lastl));
+                            n_ref = nrec + n_on - 1u;
+                            n_abs = false;
+                        }
+                    }
+                    fo.lmark = lmark;
+                    fo.kind = vuni ? 1 : 2;
+                } else if (lvm) {
+                    any_long = true;
+                }
+                // the first error of the batch (lowest record index)
+                if (__ballot(rerr != N32)) {
+                    const uint32_t mn = ~wave_max(~rerr);
+                    const int el = (int)__builtin_ctzll(__ballot(rerr == mn));
+                    err_rec = mn;
+                    err_kind = rl32(rkind, el);
+                    err_aux = rl64(raux, el);
+                    err_pos = (uint64_t)(lo + (int64_t)(int32_t)rl32((uint32_t)c, el));
+                }
+                if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
+                return fo;
+            };
+            bool round_broke = false;        // a lane-parallel round ended on a broken record
             if (!huge && p < vhi_r && fast_skip == 0u) {
-                // ---- lane-parallel framing: stride prediction, verified --------------------------
+                // ---- stride prediction, verified ---------------------------------------------------
                 // Lane j decodes the record that would start at cur + j L (L = the last record's
-                // length) from a window of the segment bytes: opcode, key length, value length, every
-                // engine.rs framing check, and where its successor starts.  Lane 0's position is
-                // exact; lane j's is exact if records 0 .. j-1 were valid and L long.  The first lane
-                // whose record is broken or whose successor is not the next prediction ends the
-                // round (record f): the records up to f are the exact chain, and f's own successor
-                // is exact.  A store of equal-sized records takes every record of the tile in one
-                // round.  One round a tile (a loop here made the compiler spill and reload much of
-                // the stripe state every tile): a broken record, or a round that found fewer than
-                // three records, leaves the rest of the tile to the exact scalar hop loop below.
-                const int32_t vhiT = (int32_t)vhi_r, remT = (int32_t)rem;
+                // length).  Lane 0's position is exact; lane j's is exact if records 0 .. j-1 were
+                // valid and L long.  The first lane whose record is broken or whose successor is not
+                // the next prediction ends the round (record f): the records up to f are the exact
+                // chain, and f's own successor is exact.  A store of equal-sized records takes every
+                // record of the tile in one round.  One round a tile (a loop here made the compiler
+                // spill and reload much of the stripe state every tile): a round that found fewer than
+                // three records hands the next tiles to the candidate round.
                 int32_t cur = (int32_t)p;
                 uint32_t L = stride;
                 do {
                     const bool one = L == 0u || L >= (uint32_t)TILE;   // no usable stride: lane 0 only
                     const int32_t c = cur + (one ? 0 : lane * (int32_t)L);
                     const bool act = lane == 0 || (!one && c < vhiT);
-                    const int32_t a = c & ~3;
-                    const uint32_t s = (uint32_t)c & 3u;
-                    uint32_t win[WINW];
-#pragma unroll
-                    for (int i = 0; i < WINW; ++i) win[i] = act ? ts.w32a(a + 4 * i) : 0u;
-                    const uint32_t x0 = __builtin_amdgcn_alignbyte(win[1], win[0], s);
-                    const uint32_t x1 = __builtin_amdgcn_alignbyte(win[2], win[1], s);
-                    const uint32_t op = x0 & 255u, klen = (x0 >> 8) | (x1 << 24);
-                    // engine.rs framing checks, tile-relative in 32 bits (rem < 2^31)
-                    const uint32_t room = (uint32_t)(remT - c);
-                    bool ok = act && op <= 1u && c < vhiT && room >= 5u && klen <= room - 5u;
-                    const uint32_t e = (uint32_t)c + 5u + (ok ? klen : 0u);   // < 2^31
-                    const bool need_v = ok && op == 0u;
-                    ok = ok && (!need_v || (uint32_t)remT - e >= 4u);
-                    // the value length: from the window when the key length is lane 0's (one length
-                    // for every key is the usual case) and the field lies in it, else from memory
-                    const uint32_t ku = rl32(klen, 0);
-                    uint32_t vlen = 0;
-                    bool vdone = false;
-                    {
-                        const uint32_t dd = 5u + ku, B0 = dd >> 2;
-                        if (B0 >= 1u && B0 <= (uint32_t)(WINW - 3)) {
-                            uint32_t wa = 0, wb = 0, wc = 0;
-#pragma unroll
-                            for (int bb = 1; bb <= WINW - 3; ++bb)
-                                if (B0 == (uint32_t)bb) { wa = win[bb]; wb = win[bb + 1]; wc = win[bb + 2]; }
-                            const uint32_t oo = s + (dd & 3u);
-                            const bool cy = oo >= 4u;
-                            vlen = __builtin_amdgcn_alignbyte(cy ? wc : wb, cy ? wb : wa, oo & 3u);
-                            vdone = klen == ku;
-                        }
-                    }
-                    if (need_v && ok && !vdone) vlen = ts.u32((int64_t)e);
-                    const uint32_t vb = e + 4u;
-                    ok = ok && (!need_v || vlen <= (uint32_t)remT - vb);
-                    const uint32_t nx = op == 1u ? e : vb + vlen;
+                    const Dec d = decode(c, act, 0, true);
                     // the first lane whose record is broken or whose successor is not the next
                     // prediction (the last active lane's successor is unconstrained)
                     const int n = (int)__builtin_popcountll(__ballot(act));
-                    const bool mis = act && (!ok || (lane < n - 1 && nx != (uint32_t)(c + (int32_t)L)));
+                    const bool mis = act && (!d.ok || (lane < n - 1 && d.nx != (uint32_t)(c + (int32_t)L)));
                     const uint64_t mm = __ballot(mis);
                     const int f = mm ? (int)__builtin_ctzll(mm) : n - 1;   // the round's last chain record
-                    const bool okf = rl32(ok ? 1u : 0u, f) != 0u;
+                    const bool okf = rl32(d.ok ? 1u : 0u, f) != 0u;
                     const uint32_t n_on = okf ? (uint32_t)f + 1u : (uint32_t)f;   // records on the chain
                     const uint32_t cf = rl32((uint32_t)c, f);
                     if (n_on) {
-                        // the walked records: lane j < n_on emits record nrec + j (lane order is
-                        // position order)
-                        if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
-                        const bool on = (uint32_t)lane < n_on;
-                        const uint32_t rk = (uint32_t)lane;
                         const uint32_t slot0 = claim(n_on);
-                        // one key length for the batch (lane 0's, ku): no per-lane byte masks
-                        const bool kuni = __ballot(on && klen != ku) == 0ull && ku <= 4u * KEYW;
-                        const uint32_t kmx = kuni ? ku : wave_max(on ? klen : 0u);
-                        uint32_t rerr = N32, rkind = 0;
-                        uint64_t raux = 0;
-                        if (on && !(KVR_ABLATE & 1)) {
-                            const uint32_t kc = kmx > 4u * KEYW ? 4u * KEYW : kmx;
-                            const uint32_t nw = (kc + 3u) >> 2;   // key words of the longest key
-                            uint32_t kr[KEYW + 1];
-#pragma unroll
-                            for (int i = 0; i <= KEYW; ++i) kr[i] = s == 3u ? win[i + 2] : win[i + 1];
-                            const int kb = c + 5;
-                            uint32_t cc = ~0u, bad = 0x80u;
-                            if (kuni) cc = crc_words_u<KEYW>(kr, K, (s + 1u) & 3u, ku, &bad);
-                            else if (klen <= 4u * KEYW) cc = crc_words<KEYW>(kr, K, (s + 1u) & 3u, klen, nw, &bad);
-                            if (bad != 0u) {              // non-ASCII or long key: the full UTF-8 check
-                                uint64_t vu = 0;
-                                uint32_t el = 0;
-                                if (!utf8_check(ts, kb, klen, &vu, &el)) {   // engine.rs:114
-                                    rerr = nrec + rk; rkind = KVR_E_UTF8; raux = vu | ((uint64_t)el << 32);
-                                } else {
-                                    cc = crc_long(ts, ~0u, kb, klen, K);
-                                }
-                            }
-                            if (rerr == N32) {
-                                kvr_tuple t;
-                                t.rec_off = (uint64_t)(lo + c);
-                                t.seg_idx = sd.seg;
-                                t.key_len = klen;
-                                t.val_len = op == 0u ? vlen : 0u;
-                                t.crc32 = op == 0u ? short_value_crc(ts, K, (int)vb, vlen) : 0u;
-                                t.key_tag = ~cc;
-                                t.op = (uint8_t)op;
-                                t.flags = 0;
-                                t.reserved = 0;
-                                pool[slot0 + rk] = t;
-                                // the key prefix for the fold (only calls that fold ask for it)
-                                if (kpool) kpool[slot0 + rk] = key_prefix_words(kr, (s + 1u) & 3u, klen);
-                            }
-                        }
-                        // long values crossing a unit boundary: marked at their first unit (a scatter
-                        // through this wave's LDS row), then folded into every unit's view
-                        const bool lv = on && op == 0u && vlen > (uint32_t)SMALL &&
-                                        ((vb ^ (vb + vlen - 1u)) >> SC_LOG) != 0u;
-                        const uint64_t lvm = __ballot(lv);
-                        // a round of SETs of one key and one value length (longer than a unit)
-                        const uint32_t vu = rl32(vlen, 0);
-                        const bool vuni = KVR_UNIFOLD && !one && vu > (uint32_t)SC &&
-                                          __ballot(on && (op != 0u || vlen != vu || klen != ku)) == 0ull;
-                        if (lvm && !(KVR_ABLATE & 32)) {
-                            uint32_t lmark = 0;
-                            if (!vuni) {
-                                MK[lane] = 0u;
-                                __builtin_amdgcn_wave_barrier();
-                                if (lv && vb < (uint32_t)TILE) MK[vb >> SC_LOG] = (uint32_t)lane + 1u;
-                                __builtin_amdgcn_wave_barrier();
-                                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                                lmark = MK[lane];
-                            }
-                            // a long value starting past the tile end (only the last record): carried
-                            const int jl = 63 - (int)__builtin_clzll(lvm);
-                            const uint32_t vbl = rl32(vb, jl);
-                            if (vbl >= (uint32_t)TILE) {
-                                n_carry = 2; n_vb = (uint64_t)(lo + (int64_t)vbl);
-                                n_ve = (uint64_t)(lo + (int64_t)vbl + rl32(vlen, jl));
-                                n_ref = nrec + (uint32_t)jl;
-                                n_abs = false;
-                            }
-                            if (vuni) fold_uniform(cur + 9 + (int32_t)ku, (int32_t)L, n_on, (int32_t)vu, nrec);
-                            else fold_views(lmark, (int32_t)vb, (int32_t)(vb + vlen), nrec + rk);
-                        } else if (lvm) {
-                            any_long = true;
-                        }
-                        // the first error of the batch (lowest record index)
-                        if (__ballot(rerr != N32)) {
-                            const int el = (int)__builtin_ctzll(__ballot(rerr != N32));
-                            err_rec = rl32(rerr, el);
-                            err_kind = rl32(rkind, el);
-                            err_aux = rl64(raux, el);
-                            err_pos = (uint64_t)(lo + (int64_t)(int32_t)rl32((uint32_t)c, el));
+                        const Fold fo = emit(d, c, (uint32_t)lane < n_on, (uint32_t)lane, n_on, 0, (int)n_on - 1, !one, slot0);
+                        if (fo.kind == 1) {
+                            fold_uniform(cur + 9 + (int32_t)rl32(d.klen, 0), (int32_t)L, n_on, (int32_t)rl32(d.vlen, 0), nrec);
+                        } else if (fo.kind == 2) {
+                            fold_views(fo.lmark, (int32_t)d.vb, (int32_t)(d.vb + d.vlen), nrec + (uint32_t)lane);
                         }
                         nrec = err_rec != N32 ? err_rec : nrec + n_on;
-                        if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
                     }
-                    if (!okf) { cur = (int32_t)cf; break; }    // a broken record at cf: the exact loop reports it
-                    const uint32_t nf = rl32(nx, f);
+                    if (!okf) { cur = (int32_t)cf; round_broke = true; break; }   // the exact loop reports it
+                    const uint32_t nf = rl32(d.nx, f);
                     L = nf - cf;                               // record f's length predicts the next tile
                     cur = (int32_t)nf;
                     if (err_rec != N32) break;
-                    if (!one && n_on < 3u && cur < vhiT) {      // lengths vary: the scalar loop is cheaper
+                    if (!one && n_on < 3u && cur < vhiT) {      // lengths vary: candidate rounds for a while
                         fast_skip = KVR_FAST_BACKOFF;
                         break;
                     }
@@ -1128,6 +1261,84 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             } else if (fast_skip) {
                 --fast_skip;
             }
+#if KVR_CANDFRAME
+            if (!huge && p < vhi_r && err_rec == N32 && !round_broke) {
+                // ---- candidate chain: records of varying lengths, lane-parallel ----------------------
+                // Every byte of [p, vhi) that can start a record (an opcode byte 0x00 / 0x01 whose key
+                // length does not reach past the segment end in its top byte: SWAR over the registers)
+                // is a candidate; up to 64 of them go to one lane each (a scatter through this wave's
+                // LDS row) and are decoded there with their successor.  The chain from p then follows
+                // the candidates by lane matches (a ballot per record), which ranks the records: rank
+                // order is position order.  A position that is not a candidate is a broken record (the
+                // filter is a necessary condition), left with the rest of the tile to the exact loop.
+                const int32_t p0 = (int32_t)p;
+                uint32_t cm[4];
+                cand_masks(w, rem, cm);
+                if (ue <= p0) { cm[0] = 0u; cm[1] = 0u; cm[2] = 0u; cm[3] = 0u; }
+                if (vhiT < TILE) mask_from(cm, vhiT - us);   // the segment's last tile: nothing past its end
+                const uint32_t cnt = (uint32_t)(__builtin_popcount(cm[0]) + __builtin_popcount(cm[1]) +
+                                                __builtin_popcount(cm[2]) + __builtin_popcount(cm[3]));
+                const uint32_t inc = wave_incl_add(cnt);
+                const uint32_t tot = rl32(inc, 63);
+                if (tot - 1u < 64u) {
+                    // lane l's candidates to slots [ex, ex + cnt) of the row (any order within a unit)
+                    uint32_t ex = inc - cnt;
+                    uint32_t m0 = cm[0], m1 = cm[1], m2 = cm[2], m3 = cm[3];
+#pragma unroll 1
+                    while (__ballot((m0 | m1 | m2 | m3) != 0u)) {
+                        if ((m0 | m1 | m2 | m3) != 0u) {
+                            const int q = m0 ? 0 : m1 ? 1 : m2 ? 2 : 3;
+                            const uint32_t mb = q == 0 ? m0 : q == 1 ? m1 : q == 2 ? m2 : m3;
+                            const uint32_t nb2 = mb & (mb - 1u);
+                            m0 = q == 0 ? nb2 : m0; m1 = q == 1 ? nb2 : m1; m2 = q == 2 ? nb2 : m2; m3 = q == 3 ? nb2 : m3;
+                            const int t = __builtin_ctz(mb);
+                            MK[ex] = (uint32_t)(us + 32 * q + 4 * (t & 7) + (t >> 3));
+                            ++ex;
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    const int32_t c = lane < (int)tot ? (int32_t)MK[lane] : -1;
+                    const bool act = c >= p0 && c < vhiT;
+                    const uint64_t at0 = __ballot(act && c == p0);
+                    Dec d = decode(act ? c : p0, act, at0 ? (int)__builtin_ctzll(at0) : 0, false);
+                    const uint32_t nxp = act && d.ok ? d.nx : N32;
+                    // the chain from p through the candidates
+                    uint32_t rk = N32, vl = d.vlen;
+                    int32_t cur = p0;
+                    uint32_t nb = 0;
+                    int lead = 0, lastl = 0;
+#pragma unroll 1
+                    while (cur < vhiT) {
+                        const uint64_t mm = __ballot(c == cur);
+                        if (mm == 0ull) break;                 // not a candidate: a broken record
+                        const int j = (int)__builtin_ctzll(mm);
+                        uint32_t nxj = rl32(nxp, j);
+                        if (nxj == UNK) {                      // another key length: its value length
+                            const int32_t e = cur + 5 + (int32_t)rl32(d.klen, j);
+                            const uint32_t vj = e + 8 <= TILE ? (uint32_t)tu64(e) : uni32(ts.u32(e));
+                            nxj = vj <= (uint32_t)(remT - e - 4) ? (uint32_t)(e + 4) + vj : N32;
+                            vl = wl32(vl, vj, (uint32_t)j);
+                        }
+                        if (nxj == N32) break;                 // a broken record: the exact loop reports it
+                        rk = wl32(rk, nb, (uint32_t)j);
+                        lead = nb == 0u ? j : lead;
+                        lastl = j;
+                        ++nb;
+                        cur = (int32_t)nxj;
+                    }
+                    d.vlen = vl;
+                    if (nb) {
+                        const uint32_t slot0 = claim(nb);
+                        const Fold fo = emit(d, c, rk != N32, rk, nb, lead, lastl, false, slot0);
+                        if (fo.kind) fold_views(fo.lmark, (int32_t)d.vb, (int32_t)(d.vb + d.vlen), nrec + rk);
+                        nrec = err_rec != N32 ? err_rec : nrec + nb;
+                        if (cur >= vhiT) stride = (uint32_t)(cur - (int32_t)rl32((uint32_t)c, lastl));
+                    }
+                    p = cur;
+                }
+            }
+#endif
 #endif
             // ---- the exact scalar hop loop: anything the lane-parallel framing left -----------
             // (entered only when the lane-parallel round left part of the tile: the loop's spill and
@@ -1182,7 +1393,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                                 // (a 64-bit walk: the value may end more than 2^31 bytes on, so it
                                 // is folded on the spot with its 64-bit end, not batched in 32 bits)
                                 if constexpr (sizeof(T) == 8) consider((int32_t)vb, (uint64_t)(lo + e2), idx, false, false);
-                                else { lmark = wl32(lmark, nb, (uint32_t)vb >> SC_LOG); bl = 1; }
+                                else { lmark = wl32(lmark, (nb << 6) | (nb - 1u), (uint32_t)vb >> SC_LOG); bl = 1; }
                             }
                             else { n_carry = 2; n_vb = (uint64_t)(lo + vb); n_ve = (uint64_t)(lo + e2); n_ref = idx; n_abs = false; }
                         }
@@ -1306,6 +1517,53 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             uint32_t ca = 0, cb = 0, sn = 0;
             if (KVR_ABLATE & 8) {
                 ca = w[0]; cb = w[1];
+            } else if (KVR_S8) {
+                // slice-by-8: step s takes words 2 s (x, the register folded in) and 2 s + 1 (y) of
+                // each half.  A restart at an even word replaces x by the masked word; at an odd one
+                // x becomes 0 (T[0] = 0: the register and the word before drop out) and y the masked
+                // word.  The snapshot takes x at step qh >> 1: for an even qh the register is x ^ wm,
+                // for an odd one it is one slice-by-4 step of x (after the loop).
+                constexpr int H2 = H / 2;
+                const int sh = qh >> 1, sah = qah >= 0 ? (qah >> 1) : -1;
+                const bool odd_a = (qah & 1) != 0;
+                const bool gen = __ballot(m != 0 || qa >= 0) != 0ull;
+                uint32_t xa = w[0], xb = w[H], snx = 0;
+                if (gen) {
+                    const bool r0 = sah == 0;
+                    const uint32_t ma = r0 && !ab ? (odd_a ? 0u : (w[0] & amask)) : w[0];
+                    const uint32_t mbv = r0 && ab ? (odd_a ? 0u : (w[H] & amask)) : w[H];
+                    xa = ma; xb = mbv;
+                }
+#pragma unroll
+                for (int st = 0; st < H2; ++st) {
+                    uint32_t ya = w[2 * st + 1], yb = w[H + 2 * st + 1];
+                    if (gen) {
+                        snx = st == sh ? (mb ? xb : xa) : snx;
+                        const bool ro = st == sah && odd_a;   // restart at this step's odd word
+                        ya = ro && !ab ? (ya & amask) : ya;
+                        yb = ro && ab ? (yb & amask) : yb;
+                    }
+                    uint32_t pxa, xa3, pya, ya3, pxb, xb3, pyb, yb3;
+                    look8(xa, ya, K, pxa, xa3, pya, ya3);
+                    look8(xb, yb, K, pxb, xb3, pyb, yb3);
+                    if (st + 1 < H2) {
+                        const uint32_t na = w[2 * st + 2], nb_ = w[H + 2 * st + 2];
+                        xa = xor3(pxa, xa3, xor3(pya, ya3, na));
+                        xb = xor3(pxb, xb3, xor3(pyb, yb3, nb_));
+                        if (gen) {
+                            const bool r = st + 1 == sah;         // restart at the next step
+                            xa = r && !ab ? (odd_a ? 0u : (na & amask)) : xa;
+                            xb = r && ab ? (odd_a ? 0u : (nb_ & amask)) : xb;
+                        }
+                    } else {
+                        ca = xor3(pxa, xa3, pya ^ ya3);
+                        cb = xor3(pxb, xb3, pyb ^ yb3);
+                    }
+                }
+                if (gen) {
+                    const uint32_t s4 = crc4(0u, snx, K);   // (odd qh: one slice-by-4 step of x)
+                    sn = qm == UW ? cb : ((qh & 1) ? s4 : (snx ^ wm));
+                }
             } else if (!__ballot(m != 0 || qa >= 0)) {
                 uint32_t xa = w[0], xb = w[H];
 #pragma unroll
@@ -1368,7 +1626,9 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             if (!(KVR_ABLATE & 16)) {
                 const int32_t ce = vx > TILE ? 63 : ((vx - 1) >> SC_LOG) - 1;   // (vx = 0: v = 0)
                 const int32_t dd = ce - lane;
-                const uint32_t t_ = kmul_col<KR_OFF>(v, S, dd > 0 ? 4u * (uint32_t)(dd - 1) : 0u);
+                // (a lane with no push reads the broadcast entry of a zero register: its lookups add no
+                // distinct address to column 0's bank)
+                const uint32_t t_ = kmul_col<KR_OFF>(dd > 0 ? v : 0u, S, dd > 0 ? 4u * (uint32_t)(dd - 1) : 0u);
                 v = dd > 0 ? t_ : v;
                 // (a lane without a source reads 0 from the DPP move -- row_shr past the row start,
                 // the rows a broadcast skips -- which adds nothing and starts no segment, so no lane
@@ -1451,6 +1711,8 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
         r.count = total;
         r.forced = redo_mode ? 1u : 0u;
         r.owned = redo_mode ? 1u : 0u;
+        r.pool_run = run_contig && run_first != N32 ? (uint64_t)run_first : NONE;
+        r.pad = 0;
         sres[si] = r;
     }
     // ---- redo pass: walk on into the next stripe of the segment --------------------------------

@@ -193,8 +193,9 @@ def test_replay_past_the_pool_slot_limit(gctx):
 
 def test_full_size_cfg4_fold_batched(gctx, monkeypatch):
     """The folding callers batched at full size: one GPU's cfg4 shard (64 x 64 MiB, 8 M records,
-    50 % DEL) with the pool-slot limit lowered to 3 M tuples, so kvr_replay_live and kvr_compact run
-    their replay as three or more whole-segment batches, then fold all of them (the path a
+    50 % DEL) with the pool-slot limit lowered to 16 M tuples (above the 8.4 M slots of claim slack
+    the 4096 stripes reserve), so kvr_replay_live and kvr_compact run their replay as four
+    whole-segment batches, then fold all of them (the path a
     mid-round-3 bug once broke with status 0).  The live list equals the oracle's fold and the
     compaction output equals oracle_compact byte for byte."""
     data, offs, sizes, man, n_rec = _generate(gctx, "cfg4")
@@ -204,7 +205,7 @@ def test_full_size_cfg4_fold_batched(gctx, monkeypatch):
     rc, t, _ = O.replay_parallel(hsegs, threads=16)
     assert rc == 0 and len(t) == n_rec
     live, nk, _ = O.fold_live(hsegs, t)
-    monkeypatch.setenv("KVR_POOL_LIMIT", "3000000")
+    monkeypatch.setenv("KVR_POOL_LIMIT", "16000000")
     r = gctx.replay_live(segs, on_device=True)
     assert r.status == 0 and r.n == nk and np.array_equal(r.tuples, t[live])
     total = sum(ln for ln, _ in sizes)

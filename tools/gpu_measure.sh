@@ -44,6 +44,10 @@ for s in $STEPS; do
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
         python "$R/bench.py" --no-cpu --no-stream --no-open > "$OUT/prof.log" 2>&1) || { echo "rocprof failed"; tail -20 "$OUT/prof.log"; exit 1; }
       find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \; ;;
+    trace)    # kernel + memory-copy timeline of the headline step (tools/trace_gaps.py): the gaps around k_replay
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$OUT/trace" -o run -- \
+        python "$R/bench.py" --no-cpu --no-stream --no-open --steps 20 > "$OUT/trace.log" 2>&1) || { echo "trace failed"; tail -20 "$OUT/trace.log"; exit 1; }
+      python "$R/tools/trace_gaps.py" "$OUT/trace" > "$OUT/trace_gaps.txt" 2>&1; cat "$OUT/trace_gaps.txt" ;;
     profc)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profc" -o run -- \
         python "$R/bench.py" --mode compact --steps 5 --warmup 2 > "$OUT/profc.log" 2>&1) || { echo "rocprof compact failed"; tail -20 "$OUT/profc.log"; exit 1; }
