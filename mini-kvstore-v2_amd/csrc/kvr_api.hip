@@ -168,7 +168,7 @@ struct kvr_ctx {
     kvr_stream_stats sstats{};
     // batch ETag (kvr_etag_batch)
     DevBuf<uint32_t> e_x, e_cb, e_creg, e_out, e_exp;
-    DevBuf<uint64_t> e_cpre, e_offs, e_lens, e_fail;
+    DevBuf<uint64_t> e_cpre, e_offs, e_lens, e_fail, e_cdesc;
     DevBuf<uint8_t> e_data;
     kvr_etag_stats estats{};
     uint32_t e_wg_per_cu = 0;
@@ -352,6 +352,7 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->r_best.release(); c->r_hk.release();
     c->e_x.release(); c->e_cb.release(); c->e_creg.release(); c->e_out.release(); c->e_exp.release();
     c->e_cpre.release(); c->e_offs.release(); c->e_lens.release(); c->e_fail.release(); c->e_data.release();
+    c->e_cdesc.release();
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     for (int i = 0; i < 2; ++i) {
         c->slot[i].release();
@@ -1496,7 +1497,7 @@ int kvr_etag_batch(kvr_ctx *c, const uint8_t *data, uint64_t data_len, const uin
         bytes += lens[i];
     }
     cpre[n] = nch;
-    if (nch >= 0xFFFFFFFFull) return KVR_EINVAL;
+    if (nch >= 0xFFFFFFFFull || data_len >= (1ull << 48)) return KVR_EINVAL;   // (k_etag_map's packed descriptors)
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
     if (!c->e_x.p) {   // XT[t] = x^(8t) for t <= CH, XC[l] = x^(8 l CH) for l < 64, x^(8 * 64 CH)
@@ -1522,7 +1523,7 @@ int kvr_etag_batch(kvr_ctx *c, const uint8_t *data, uint64_t data_len, const uin
         if (data_len) HIPCHK(hipMemcpyAsync(c->e_data.p, data, data_len, hipMemcpyHostToDevice, st));
         d_data = c->e_data.p;
     }
-    if (c->e_cpre.ensure(n + 1) || c->e_offs.ensure(n) || c->e_lens.ensure(n) || c->e_cb.ensure(nch) ||
+    if (c->e_cpre.ensure(n + 1) || c->e_offs.ensure(n) || c->e_lens.ensure(n) || c->e_cdesc.ensure(nch + 1) ||
         c->e_creg.ensure(nch) || c->e_fail.ensure(1))
         return KVR_ENOMEM;
     HIPCHK(hipMemcpyAsync(c->e_cpre.p, cpre.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
@@ -1540,11 +1541,13 @@ int kvr_etag_batch(kvr_ctx *c, const uint8_t *data, uint64_t data_len, const uin
         HIPCHK(hipMemcpyAsync(c->e_exp.p, expected, n * 4, hipMemcpyHostToDevice, st));
         d_exp = c->e_exp.p;
     }
-    const uint32_t mgrid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 65536);
-    hipLaunchKernelGGL(k_etag_map, dim3(mgrid), dim3(256), 0, st, c->e_cpre.p, (uint64_t)n, c->e_cb.p);
+    const uint32_t mgrid = (uint32_t)std::min<uint64_t>((nch + 255) / 256, 65536);
+    if (nch)
+        hipLaunchKernelGGL(k_etag_map, dim3(mgrid), dim3(256), 0, st, c->e_cpre.p, (uint64_t)n, c->e_offs.p, c->e_lens.p,
+                           nch, c->e_cdesc.p);
     HIPCHK(hipEventRecord(c->ev[0], st));
     if (nch) {
-        const uint64_t per = (uint64_t)ETAG_WPB * ETAG_NC;
+        const uint64_t per = (uint64_t)ETAG_WPB * (KVR_ETAG_DB ? ETAG_NC_DB : ETAG_NC);
         if (!c->e_wg_per_cu) {   // persistent grid: exactly the resident workgroups
             int occ = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_etag_chunk, 64 * ETAG_WPB, 0) != hipSuccess || occ < 1)
@@ -1552,8 +1555,8 @@ int kvr_etag_batch(kvr_ctx *c, const uint8_t *data, uint64_t data_len, const uin
             c->e_wg_per_cu = (uint32_t)occ;
         }
         const uint64_t g = std::min<uint64_t>((nch + per - 1) / per, (uint64_t)c->n_cu * c->e_wg_per_cu);
-        hipLaunchKernelGGL(k_etag_chunk, dim3((uint32_t)g), dim3(64 * ETAG_WPB), 0, st, d_data, data_len, c->e_offs.p,
-                           c->e_lens.p, c->e_cpre.p, c->e_cb.p, nch, c->crc.p, c->e_x.p, c->e_creg.p);
+        hipLaunchKernelGGL(k_etag_chunk, dim3((uint32_t)g), dim3(64 * ETAG_WPB), 0, st, d_data, data_len, c->e_cdesc.p,
+                           nch, c->crc.p, c->e_x.p, c->e_creg.p);
     }
     HIPCHK(hipEventRecord(c->ev[1], st));
     hipLaunchKernelGGL(k_etag_join, dim3((uint32_t)((n + ETAG_WPB - 1) / ETAG_WPB)), dim3(64 * ETAG_WPB), 0, st,

@@ -25,10 +25,31 @@ constexpr uint32_t ETAG_NC = 4;              // chunks per wave and round (inter
 constexpr uint32_t ETAG_NX = ETAG_CH + 1 + 64 + 1;   // XT[0..CH], XC[0..63], X(64 CH); then KL
 constexpr uint32_t ETAG_NKL = 64 * 128;             // KL[lane][i][n]: nibble tables of XT[CH - 64 (lane+1)]
 
-// chunk -> blob map: blob v owns chunks [cpre[v], cpre[v+1])
-__global__ void k_etag_map(const uint64_t *__restrict__ cpre, uint64_t n, uint32_t *__restrict__ chunk_blob) {
-    for (uint64_t v = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
-        for (uint64_t c = cpre[v]; c < cpre[v + 1]; ++c) chunk_blob[c] = (uint32_t)v;
+#ifndef KVR_ETAG_DB
+#define KVR_ETAG_DB 0   // 1: double-buffered rounds of ETAG_NC_DB chunks (the next round's loads in flight)
+#endif
+constexpr int ETAG_NC_DB = 2;
+
+// chunk descriptors: blob v owns chunks [cpre[v], cpre[v+1]); chunk c = the j-th of its blob is
+// data[start, start + clen) with start = offs[v] + j CH, packed as start | (clen - 1) << 48 |
+// (j == 0) << 63 (one load per chunk in k_etag_chunk).  One thread per chunk, v by binary search.
+__global__ void k_etag_map(const uint64_t *__restrict__ cpre, uint64_t n, const uint64_t *__restrict__ offs,
+                           const uint64_t *__restrict__ lens, uint64_t nch, uint64_t *__restrict__ cdesc) {
+    for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nch; c += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t lo = 0, hi = n - 1;   // the last blob with cpre[v] <= c (empty blobs own no chunk)
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi + 1) >> 1;
+            if (cpre[mid] <= c) lo = mid; else hi = mid - 1;
+        }
+        const uint64_t j = c - cpre[lo];
+        const uint64_t clen = min<uint64_t>(ETAG_CH, lens[lo] - j * ETAG_CH);
+        cdesc[c] = (offs[lo] + j * ETAG_CH) | ((clen - 1) << 48) | ((j == 0 ? 1ull : 0ull) << 63);
+    }
+}
+__device__ __forceinline__ void etag_desc(uint64_t d, uint64_t &start, uint32_t &clen, bool &first) {
+    start = d & ((1ull << 48) - 1);
+    clen = (uint32_t)((d >> 48) & 0x7FFFu) + 1u;
+    first = (d >> 63) != 0;
 }
 
 // The byte tables are k_replay's (kvr_replay_kernel.hip, Crc): slice-by-8 (KVR_S8) replicated per
@@ -88,11 +109,53 @@ __device__ inline uint32_t etag_unit_general(const Crc &T, const uint8_t *data, 
 
 // Persistent: as many workgroups as are resident (occupancy query); each wave takes ETAG_NC chunks per round and runs
 // their CRC chains interleaved (independent LDS lookup chains hide each other's latency).
+// slice-by-8 over NC full aligned chunks whose 16-B words are w[k][0..3] (per lane), chains
+// interleaved; reg[k] in: the chain's start register, out: the lane's register pushed to the chunk end
+template <int NC>
+__device__ __forceinline__ void etag_fast(const Crc &T, const EtagSmem &S, uint32_t lane, const uint4 (&w)[NC][4],
+                                          uint32_t (&reg)[NC]) {
+#if KVR_S8
+    uint32_t x[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) x[k] = reg[k] ^ w[k][0].x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                uint32_t px, x3, py, y3;
+                look8(x[k], h ? w[k][i].w : w[k][i].y, T, px, x3, py, y3);
+                if (i < 3 || h == 0) {
+                    const uint32_t nw = h ? w[k][i + (i < 3)].x : w[k][i].z;
+                    x[k] = xor3(px, x3, xor3(py, y3, nw));
+                } else {
+                    reg[k] = xor3(px, x3, py ^ y3);
+                }
+            }
+        }
+    }
+#else
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int k = 0; k < NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].x);
+#pragma unroll
+        for (int k = 0; k < NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].y);
+#pragma unroll
+        for (int k = 0; k < NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].z);
+#pragma unroll
+        for (int k = 0; k < NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].w);
+    }
+#endif
+    if (lane != 63) {
+#pragma unroll
+        for (int k = 0; k < NC; ++k) reg[k] = kmul_lane(reg[k], S, lane);
+    }
+}
+
 __global__ __launch_bounds__(64 * ETAG_WPB) void k_etag_chunk(const uint8_t *__restrict__ data, uint64_t data_len,
-                                                             const uint64_t *__restrict__ offs,
-                                                             const uint64_t *__restrict__ lens,
-                                                             const uint64_t *__restrict__ cpre,
-                                                             const uint32_t *__restrict__ chunk_blob, uint64_t n_chunks,
+                                                             const uint64_t *__restrict__ cdesc, uint64_t n_chunks,
                                                              const uint32_t *__restrict__ crc_tab,
                                                              const uint32_t *__restrict__ xt,
                                                              uint32_t *__restrict__ creg) {
@@ -108,28 +171,83 @@ __global__ __launch_bounds__(64 * ETAG_WPB) void k_etag_chunk(const uint8_t *__r
     Crc T;
     crc_init(T, C2, lane);
     const uint64_t waves = (uint64_t)gridDim.x * ETAG_WPB;
-    for (uint64_t base = (blockIdx.x * (uint64_t)ETAG_WPB + (threadIdx.x >> 6)) * ETAG_NC; base < n_chunks;
-         base += waves * ETAG_NC) {
-        uint64_t start[ETAG_NC];
-        uint32_t clen[ETAG_NC], reg[ETAG_NC];
+    const uint64_t wave = blockIdx.x * (uint64_t)ETAG_WPB + (threadIdx.x >> 6);
+    // a round's chunks: start, length, start register (0xFFFFFFFF for lane 0 of a blob's first
+    // chunk), and whether all of them are full and 16-B aligned (the fast path)
+    auto round_desc = [&](uint64_t base, auto &start, auto &clen, auto &reg) -> bool {
+        constexpr int NC = sizeof(clen) / sizeof(clen[0]);
         bool fast = true;
 #pragma unroll
-        for (int k = 0; k < ETAG_NC; ++k) {
+        for (int k = 0; k < NC; ++k) {
             const uint64_t c = base + k;
+            start[k] = 0; clen[k] = 0; reg[k] = 0;
             if (c < n_chunks) {
-                const uint32_t v = chunk_blob[c];
-                const uint64_t j = c - cpre[v];
-                start[k] = offs[v] + j * ETAG_CH;
-                clen[k] = (uint32_t)min<uint64_t>(ETAG_CH, lens[v] - j * ETAG_CH);
-                reg[k] = (j == 0 && lane == 0) ? 0xFFFFFFFFu : 0u;
-                fast = fast && clen[k] == ETAG_CH && ((reinterpret_cast<uintptr_t>(data) + start[k]) & 15u) == 0;
-            } else {
-                start[k] = 0;
-                clen[k] = 0;
-                reg[k] = 0;
-                fast = false;
+                bool first;
+                etag_desc(cdesc[c], start[k], clen[k], first);
+                reg[k] = (first && lane == 0) ? 0xFFFFFFFFu : 0u;
             }
+            fast = fast && clen[k] == ETAG_CH && ((reinterpret_cast<uintptr_t>(data) + start[k]) & 15u) == 0;
         }
+        return fast;
+    };
+    auto finish = [&](uint64_t base, auto &reg) {
+        constexpr int NC = sizeof(reg) / sizeof(reg[0]);
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            uint32_t r = reg[k];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) r ^= __shfl_xor(r, o, 64);
+            if (lane == 0 && base + k < n_chunks) creg[base + k] = r;
+        }
+    };
+#if KVR_ETAG_DB
+    // double-buffered: the next round's descriptors and 16-B words are loaded before this round's
+    // chains run, so every wave keeps a round of loads in flight while it computes
+    constexpr int NC = ETAG_NC_DB;
+    uint64_t base = wave * NC;
+    uint64_t st[NC];
+    uint32_t cl[NC], rg[NC];
+    bool fast = base < n_chunks && round_desc(base, st, cl, rg);
+    uint4 wa[NC][4];
+    if (fast) {
+#pragma unroll
+        for (int k = 0; k < NC; ++k)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) wa[k][i] = reinterpret_cast<const uint4 *>(data + st[k] + lane * 64u)[i];
+    }
+    for (; base < n_chunks; base += waves * NC) {
+        const uint64_t nbase = base + waves * NC;
+        uint64_t nst[NC];
+        uint32_t ncl[NC], nrg[NC];
+        const bool nfast = nbase < n_chunks && round_desc(nbase, nst, ncl, nrg);
+        uint4 wb[NC][4];
+        if (nfast) {
+#pragma unroll
+            for (int k = 0; k < NC; ++k)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) wb[k][i] = reinterpret_cast<const uint4 *>(data + nst[k] + lane * 64u)[i];
+        }
+        if (fast) {
+            etag_fast<NC>(T, S, lane, wa, rg);
+        } else {
+#pragma unroll 1
+            for (int k = 0; k < NC; ++k)
+                if (cl[k]) rg[k] = etag_unit_general(T, data, data_len, st[k], cl[k], lane, rg[k], xt);
+        }
+        finish(base, rg);
+        fast = nfast;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            st[k] = nst[k]; cl[k] = ncl[k]; rg[k] = nrg[k];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) wa[k][i] = wb[k][i];
+        }
+    }
+#else
+    for (uint64_t base = wave * ETAG_NC; base < n_chunks; base += waves * ETAG_NC) {
+        uint64_t start[ETAG_NC];
+        uint32_t clen[ETAG_NC], reg[ETAG_NC];
+        const bool fast = round_desc(base, start, clen, reg);
         if (fast) {   // ETAG_NC full aligned chunks: 4 x 16-B loads per lane and chunk, chains interleaved
             uint4 w[ETAG_NC][4];
 #pragma unroll
@@ -138,59 +256,15 @@ __global__ __launch_bounds__(64 * ETAG_WPB) void k_etag_chunk(const uint8_t *__r
 #pragma unroll
                 for (int i = 0; i < 4; ++i) w[k][i] = q[i];
             }
-#if KVR_S8
-            // slice-by-8: each chain carries its step input x = register ^ word; a step takes x
-            // through tables 7 .. 4 and the next word through 3 .. 0 (8 steps a chunk, not 16)
-            uint32_t x[ETAG_NC];
-#pragma unroll
-            for (int k = 0; k < ETAG_NC; ++k) x[k] = reg[k] ^ w[k][0].x;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-#pragma unroll
-                    for (int k = 0; k < ETAG_NC; ++k) {
-                        uint32_t px, x3, py, y3;
-                        look8(x[k], h ? w[k][i].w : w[k][i].y, T, px, x3, py, y3);
-                        if (i < 3 || h == 0) {
-                            const uint32_t nw = h ? w[k][i + (i < 3)].x : w[k][i].z;
-                            x[k] = xor3(px, x3, xor3(py, y3, nw));
-                        } else {
-                            reg[k] = xor3(px, x3, py ^ y3);
-                        }
-                    }
-                }
-            }
-#else
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-#pragma unroll
-                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].x);
-#pragma unroll
-                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].y);
-#pragma unroll
-                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].z);
-#pragma unroll
-                for (int k = 0; k < ETAG_NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].w);
-            }
-#endif
-            if (lane != 63) {
-#pragma unroll
-                for (int k = 0; k < ETAG_NC; ++k) reg[k] = kmul_lane(reg[k], S, lane);
-            }
+            etag_fast<ETAG_NC>(T, S, lane, w, reg);
         } else {
 #pragma unroll 1
             for (int k = 0; k < ETAG_NC; ++k)
                 if (clen[k]) reg[k] = etag_unit_general(T, data, data_len, start[k], clen[k], lane, reg[k], xt);
         }
-#pragma unroll
-        for (int k = 0; k < ETAG_NC; ++k) {
-            uint32_t r = reg[k];
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) r ^= __shfl_xor(r, o, 64);
-            if (lane == 0 && base + k < n_chunks) creg[base + k] = r;
-        }
+        finish(base, reg);
     }
+#endif
 }
 
 // one wave per blob: join the chunk registers, finish the CRC, verify against expected
