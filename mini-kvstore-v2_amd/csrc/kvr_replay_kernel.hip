@@ -1266,24 +1266,37 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 // ---- candidate chain: records of varying lengths, lane-parallel ----------------------
                 // Every byte of [p, vhi) that can start a record (an opcode byte 0x00 / 0x01 whose key
                 // length does not reach past the segment end in its top byte: SWAR over the registers)
-                // is a candidate; up to 64 of them go to one lane each (a scatter through this wave's
-                // LDS row) and are decoded there with their successor.  The chain from p then follows
-                // the candidates by lane matches (a ballot per record), which ranks the records: rank
-                // order is position order.  A position that is not a candidate is a broken record (the
-                // filter is a necessary condition), left with the rest of the tile to the exact loop.
-                const int32_t p0 = (int32_t)p;
+                // is a candidate.  A window takes the candidates of the units from p's on, as many
+                // whole units as fit 64: they go to one lane each (a scatter through this wave's LDS
+                // row) and are decoded there with their successor.  The chain from p then follows the
+                // candidates by lane matches (a ballot per record), which ranks the records: rank
+                // order is position order.  A window ends where its units end (the next one starts at
+                // the chain's position); a position that is not a candidate is a broken record (the
+                // filter is a necessary condition), left with the rest of the tile to the exact loop,
+                // and so is a unit holding more than 64 candidates.
                 uint32_t cm[4];
                 cand_masks(w, rem, cm);
-                if (ue <= p0) { cm[0] = 0u; cm[1] = 0u; cm[2] = 0u; cm[3] = 0u; }
                 if (vhiT < TILE) mask_from(cm, vhiT - us);   // the segment's last tile: nothing past its end
-                const uint32_t cnt = (uint32_t)(__builtin_popcount(cm[0]) + __builtin_popcount(cm[1]) +
-                                                __builtin_popcount(cm[2]) + __builtin_popcount(cm[3]));
-                const uint32_t inc = wave_incl_add(cnt);
-                const uint32_t tot = rl32(inc, 63);
-                if (tot - 1u < 64u) {
-                    // lane l's candidates to slots [ex, ex + cnt) of the row (any order within a unit)
+                const uint32_t cnt_u = (uint32_t)(__builtin_popcount(cm[0]) + __builtin_popcount(cm[1]) +
+                                                  __builtin_popcount(cm[2]) + __builtin_popcount(cm[3]));
+                bool go = true;
+#pragma unroll 1
+                while (go && p < vhi_r && err_rec == N32) {
+                    const int32_t p0 = (int32_t)p;
+                    const uint32_t cnt = ue <= p0 ? 0u : cnt_u;       // units wholly before p hold none
+                    const uint32_t inc = wave_incl_add(cnt);
+                    const bool fits = inc <= 64u;                     // (inc grows with the lane)
+                    const uint64_t fm = __ballot(!fits);
+                    const int fl = fm ? (int)__builtin_ctzll(fm) : 64;   // the first lane whose unit does not fit
+                    if (fl <= (p0 >> SC_LOG)) break;                  // p's unit alone holds more than 64
+                    const uint32_t tot = rl32(inc, fl - 1);
+                    const int32_t cover = fl * SC;                    // the window's units end here
+                    if (tot == 0u) break;                             // p is no candidate: a broken record
+                    // lane l's candidates (when its units fit) to slots [ex, ex + cnt) of the row (any
+                    // order within a unit)
                     uint32_t ex = inc - cnt;
                     uint32_t m0 = cm[0], m1 = cm[1], m2 = cm[2], m3 = cm[3];
+                    if (!fits || ue <= p0) { m0 = 0u; m1 = 0u; m2 = 0u; m3 = 0u; }
 #pragma unroll 1
                     while (__ballot((m0 | m1 | m2 | m3) != 0u)) {
                         if ((m0 | m1 | m2 | m3) != 0u) {
@@ -1303,15 +1316,16 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const uint64_t at0 = __ballot(act && c == p0);
                     Dec d = decode(act ? c : p0, act, at0 ? (int)__builtin_ctzll(at0) : 0, false);
                     const uint32_t nxp = act && d.ok ? d.nx : N32;
-                    // the chain from p through the candidates
+                    // the chain from p through the window's candidates
                     uint32_t rk = N32, vl = d.vlen;
                     int32_t cur = p0;
                     uint32_t nb = 0;
                     int lead = 0, lastl = 0;
+                    const int32_t wend = cover < vhiT ? cover : vhiT;
 #pragma unroll 1
-                    while (cur < vhiT) {
+                    while (cur < wend) {
                         const uint64_t mm = __ballot(c == cur);
-                        if (mm == 0ull) break;                 // not a candidate: a broken record
+                        if (mm == 0ull) { go = false; break; }   // not a candidate: a broken record
                         const int j = (int)__builtin_ctzll(mm);
                         uint32_t nxj = rl32(nxp, j);
                         if (nxj == UNK) {                      // another key length: its value length
@@ -1320,7 +1334,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                             nxj = vj <= (uint32_t)(remT - e - 4) ? (uint32_t)(e + 4) + vj : N32;
                             vl = wl32(vl, vj, (uint32_t)j);
                         }
-                        if (nxj == N32) break;                 // a broken record: the exact loop reports it
+                        if (nxj == N32) { go = false; break; }   // a broken record: the exact loop reports it
                         rk = wl32(rk, nb, (uint32_t)j);
                         lead = nb == 0u ? j : lead;
                         lastl = j;
@@ -1333,9 +1347,10 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                         const Fold fo = emit(d, c, rk != N32, rk, nb, lead, lastl, false, slot0);
                         if (fo.kind) fold_views(fo.lmark, (int32_t)d.vb, (int32_t)(d.vb + d.vlen), nrec + rk);
                         nrec = err_rec != N32 ? err_rec : nrec + nb;
-                        if (cur >= vhiT) stride = (uint32_t)(cur - (int32_t)rl32((uint32_t)c, lastl));
+                        if (go) stride = (uint32_t)(cur - (int32_t)rl32((uint32_t)c, lastl));
                     }
                     p = cur;
+                    if (nb == 0u) go = false;
                 }
             }
 #endif

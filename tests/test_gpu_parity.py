@@ -368,3 +368,63 @@ def test_repeated_calls_reuse_and_refresh_descriptors(gctx):
     bad = a[:2] + [a[2][: len(a[2]) // 2 + 7]]
     for segs in (a, a, b, a, bad, bad, a, b, b):
         check_parity(gctx, segs)
+
+
+def _varied_store(seed, n_bytes, del_frac, klen_rng, vlen_rng, zero_values=False, key_alphabet=None):
+    """Records of varying lengths (the candidate rounds' case): keys of random length from
+    key_alphabet (ASCII letters by default), values random or all zero."""
+    rnd = random.Random(seed)
+    alpha = key_alphabet or [bytes([c]) for c in range(0x41, 0x5B)] + [bytes([c]) for c in range(0x61, 0x7B)]
+    out = bytearray()
+    while len(out) < n_bytes:
+        k = b"".join(rnd.choice(alpha) for _ in range(rnd.randint(*klen_rng)))
+        if rnd.random() < del_frac:
+            out += rec_del(k)
+        else:
+            n = rnd.randint(*vlen_rng)
+            v = bytes(n) if zero_values else rnd.randbytes(n)
+            out += rec_set(k, v)
+    return bytes(out)
+
+
+CAND_STORES = {
+    # keys of 1 .. 40 bytes (lengths other than the first record's take the successor from memory;
+    # keys past 24 bytes the long-key CRC), values up to 300 B, 30 % DEL
+    "mixed_keys": dict(del_frac=0.3, klen_rng=(1, 40), vlen_rng=(0, 300)),
+    # 95 % DEL of short records: a few hundred records a tile, windows of 64 candidates
+    "del_heavy": dict(del_frac=0.95, klen_rng=(8, 16), vlen_rng=(0, 40)),
+    # zero-valued SETs: every value byte is a candidate, so units past 64 go to the exact loop
+    "zero_values": dict(del_frac=0.2, klen_rng=(4, 20), vlen_rng=(50, 3000), zero_values=True),
+    # keys of control and multi-byte characters: candidates inside keys, the UTF-8 check per record
+    "odd_keys": dict(del_frac=0.3, klen_rng=(1, 12), vlen_rng=(0, 200),
+                     key_alphabet=[b"\x00", b"\x01", b"a", b"\xc3\xa9", b"\xe2\x82\xac", b"\xf0\x9f\x98\x80"]),
+}
+
+
+@pytest.mark.parametrize("tps", [0, 2])
+@pytest.mark.parametrize("name", list(CAND_STORES))
+def test_candidate_rounds(gctx, name, tps):
+    """Stores whose record lengths vary tile to tile (the candidate-chain framing and its windows,
+    k_replay), bit-exact against the oracle; the same with a broken record planted mid-segment
+    (the chain breaks there and the exact loop reports engine.rs's error) and with an invalid UTF-8
+    key in the middle (the first error of a candidate round by rank)."""
+    kw = CAND_STORES[name]
+    segs = [_varied_store(1000 * i + len(name), 250_000, **kw) for i in range(3)]
+    gctx.set_tiles_per_stripe(tps)
+    try:
+        check_parity(gctx, segs)
+        # a record start overwritten with an opcode of 7 about two thirds into segment 1
+        ro = O.replay([segs[1]])
+        offs = ro[1]["rec_off"]
+        at = int(offs[2 * len(offs) // 3])
+        bad = bytearray(segs[1])
+        bad[at] = 7
+        check_parity(gctx, [segs[0], bytes(bad), segs[2]])
+        # an invalid UTF-8 key: the first key byte of a later record set to 0xFF (a 1-byte key
+        # stays a valid record framing)
+        at2 = int(offs[len(offs) // 2])
+        bad2 = bytearray(segs[1])
+        bad2[at2 + 5] = 0xFF if int.from_bytes(bad2[at2 + 1:at2 + 5], "little") else bad2[at2 + 5]
+        check_parity(gctx, [segs[0], bytes(bad2), segs[2]])
+    finally:
+        gctx.set_tiles_per_stripe(0)
