@@ -654,7 +654,8 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         auto launch_compact = [&]() {
             hipLaunchKernelGGL(k_compact_s, dim3(n_stripes), dim3(CT), 0, st, c->segs.p, c->stripes.p, c->sres.p, c->soff.p,
                                c->tres.p, c->pool.p, pool_cap, d_out, out_cap, d_exp,
-                               (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p, kp, kp ? c->kout : nullptr);
+                               (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p, kp, kp ? c->kout : nullptr,
+                               c->h_ctr);
         };
         // counters and link result start at zero (the last successful call cleared them behind its
         // results, so this memset usually runs only on a context's first call or after an error)
@@ -667,7 +668,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         HIPCHK(hipEventRecord(c->ev[1], st));
         hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
                            c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p, (uint32_t)KR_TILE,
-                           c->soff.p, c->ctr.p);
+                           c->soff.p, c->ctr.p, c->h_link, c->h_ctr);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[2], st));
         // compaction is launched right away: it does nothing unless linking succeeded (status 0),
@@ -675,8 +676,14 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         launch_compact();
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[3], st));
-        HIPCHK(hipMemcpyAsync(c->h_lc, c->lcbuf.p, LC_BYTES, hipMemcpyDeviceToHost, st));   // link result + counters
+        // link result + counters: k_link and the compaction's last workgroup write them into the
+        // pinned mirror h_lc; when the call did not end cleanly they are copied as they are
         HIPCHK(wait_stream(st, c->ev[5]));
+        const bool clean = c->h_link->status == 0 && !c->h_ctr->overflow;
+        if (!clean) {
+            HIPCHK(hipMemcpyAsync(c->h_lc, c->lcbuf.p, LC_BYTES, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+        }
         c->stats.ms_replay = ev_ms(c->ev[0], c->ev[1]);
         c->stats.ms_link = ev_ms(c->ev[1], c->ev[2]);
         c->stats.ms_compact = ev_ms(c->ev[2], c->ev[3]);
@@ -713,7 +720,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
                                tb, c->redo.p, c->link.p, pool_chunk, kp);
             hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes,
                                c->sres.p, c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p, (uint32_t)KR_TILE,
-                               c->soff.p, c->ctr.p);
+                               c->soff.p, c->ctr.p, nullptr, nullptr);
             HIPCHK(hipGetLastError());
             HIPCHK(hipMemcpyAsync(c->h_link, c->link.p, sizeof(LinkResult), hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, st));
@@ -747,11 +754,12 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             fprintf(stderr, "kvr: stripe linking did not converge after %u rounds\n", guard);
             return KVR_EHIP;
         }
+        bool cleared = clean;   // the compaction's last workgroup cleared the block
         if (recompact && c->h_link->status == 0 && !c->h_ctr->overflow) {
-            launch_compact();
+            launch_compact();   // (its last workgroup writes the CRC failures to h_ctr, clears the block)
             HIPCHK(hipGetLastError());
-            HIPCHK(hipMemcpyAsync(c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
+            cleared = true;
         }
         c->stats.n_link_passes = c->h_link->passes;
         if (c->h_ctr->overflow & 2u) {   // stitch did not converge (bug trap)
@@ -775,8 +783,9 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         c->stats.n_records = total;
         c->stats.n_crc_fail = c->h_ctr->crc_fail;
         *n_out = total;
-        // clear the counters for the next call now, behind this call's work on the stream
-        if (hipMemsetAsync(c->lcbuf.p, 0, LC_BYTES, st) == hipSuccess) c->lc_zero = true;
+        // the block is clear for the next call (else clear it now, behind this call's work)
+        if (cleared) c->lc_zero = true;
+        else if (hipMemsetAsync(c->lcbuf.p, 0, LC_BYTES, st) == hipSuccess) c->lc_zero = true;
         if (!(flags & KVR_OUT_ON_DEVICE) && cap) {
             const uint64_t m = std::min<uint64_t>(total, cap);
             if (m) {

@@ -38,7 +38,7 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
                                              StripeRes *__restrict__ sres, RedoEnt *__restrict__ redo,
                                              uint32_t redo_cap, LinkResult *res, uint32_t *seg_bad_g,
                                              uint32_t *seg_err_g, uint32_t tile, uint64_t *__restrict__ soff,
-                                             Counters *ctr) {
+                                             Counters *ctr, LinkResult *hres, Counters *hctr) {
     __shared__ int32_t wm[LT / 64];
     __shared__ uint64_t wx[LT / 64];
     __shared__ unsigned long long wsum[LT / 64];
@@ -257,6 +257,14 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
             L.err_aux = r.err_aux;
         }
         *res = L;
+        if (hres) {   // the host's pinned mirror, written straight (no copy on the stream)
+            *hres = L;
+            hctr->pool_cursor = ctr->pool_cursor;
+            hctr->overflow = ctr->overflow;
+            hctr->total_tuples = (L.status == 0 && soff) ? all_recs : ctr->total_tuples;
+            hctr->crc_fail = 0;
+            __threadfence_system();
+        }
     }
 }
 
@@ -278,8 +286,9 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
                                                   const kvr_tuple *__restrict__ pool, uint64_t pool_cap,
                                                   kvr_tuple *__restrict__ out, uint64_t out_cap,
                                                   const uint32_t *__restrict__ expected, uint64_t n_expected,
-                                                  Counters *ctr, const LinkResult *__restrict__ link,
-                                                  const uint4 *__restrict__ kpool, uint4 *__restrict__ kout) {
+                                                  Counters *ctr, LinkResult *link,
+                                                  const uint4 *__restrict__ kpool, uint4 *__restrict__ kout,
+                                                  Counters *hctr) {
     if (link->status != 0 || ctr->overflow) return;
     __shared__ uint64_t off[CB + 1];
     __shared__ uint64_t part[CT];
@@ -298,12 +307,29 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
             if (half && kout) kout[o] = kpool[src];
         }
     };
+    // the last workgroup to finish hands the CRC failure count to the host's pinned mirror and
+    // clears the link + counters block for the next call (no copy or fill on the stream)
+    auto finish = [&]() {
+        for (int d = 32; d >= 1; d >>= 1) fails += __shfl_xor(fails, d, 64);
+        if ((threadIdx.x & 63) == 0 && fails) atomicAdd(&ctr->crc_fail, (unsigned long long)fails);
+        if (!hctr) return;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            if (atomicAdd(&ctr->pad, 1u) == gridDim.x - 1) {
+                __threadfence();
+                hctr->crc_fail = __hip_atomic_load(&ctr->crc_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                *link = LinkResult{};
+                *ctr = Counters{};
+                __threadfence_system();
+            }
+        }
+    };
     const uint64_t run = sres[blockIdx.x].pool_run;
     if (run != NONE) {   // the stripe's tuples are one run of the pool: a straight copy
         const uint64_t n = sres[blockIdx.x].count, o0 = soff[blockIdx.x];
         for (uint64_t k2 = threadIdx.x; k2 < 2 * n; k2 += CT) move(run + (k2 >> 1), o0 + (k2 >> 1), (uint32_t)k2 & 1u);
-        for (int d = 32; d >= 1; d >>= 1) fails += __shfl_xor(fails, d, 64);
-        if ((threadIdx.x & 63) == 0 && fails) atomicAdd(&ctr->crc_fail, (unsigned long long)fails);
+        finish();
         return;
     }
     const StripeDesc sd = stripes[blockIdx.x];
@@ -343,8 +369,7 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
         carry += ctotal;
         __syncthreads();   // (off and part are rewritten by the next chunk)
     }
-    for (int d = 32; d >= 1; d >>= 1) fails += __shfl_xor(fails, d, 64);
-    if ((threadIdx.x & 63) == 0 && fails) atomicAdd(&ctr->crc_fail, (unsigned long long)fails);
+    finish();
 }
 
 // ---------------------------------------------------------------------------------------

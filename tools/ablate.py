@@ -21,7 +21,7 @@ ABL = os.path.join(ROOT, "mini-kvstore-v2_amd", "lib", "ablate")
 nseg, seg_bytes, kw, desc = CONFIGS["cfg3" if cfg == "etag" else cfg]
 if nseg_o:
     nseg = nseg_o
-spec = K.GenSpec(seed=0x6B767265706C6179 + int(cfg[3:]), seg_bytes=seg_bytes, **kw)
+spec = None if cfg == "etag" else K.GenSpec(seed=0x6B767265706C6179 + int(cfg[3:]), seg_bytes=seg_bytes, **kw)
 P, U32, U64, SZ = C.c_void_p, C.c_uint32, C.c_uint64, C.c_size_t
 VAR = os.path.join(ROOT, "mini-kvstore-v2_amd", "lib", "variants")
 AB = os.path.join(ROOT, "mini-kvstore-v2_amd", "lib", "ab")

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Per-tile PMC counters of k_replay's first pass for ablation variants (tools/ablate.py cfg2):
-# three rocprofv3 --pmc passes per variant (counter groups within the gfx950 per-pass limits).
-#   usage: tools/pmc_variants.sh <outdir> [masks...]
+# Per-tile PMC counters of k_replay's first pass for ablation variants / A/B builds (tools/ablate.py
+# $PCFG, default cfg2): three rocprofv3 --pmc passes per variant (counter groups within the gfx950
+# per-pass limits).
+#   usage: [PCFG=cfg4] tools/pmc_variants.sh <outdir> [masks or build names...]
 set -o pipefail
 OUT=$(mkdir -p "$1" && cd "$1" && pwd); shift
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -13,7 +14,7 @@ for m in ${*:-0 3 64}; do
   g=0
   for grp in "$G1" "$G2" "$G3"; do
     g=$((g+1))
-    timeout -k 10 120 rocprofv3 --pmc $grp --output-format csv -d "$OUT/a$m/g$g" -o pmc -- python "$R/tools/ablate.py" cfg2 0 $m \
+    timeout -k 10 120 rocprofv3 --pmc $grp --output-format csv -d "$OUT/a$m/g$g" -o pmc -- python "$R/tools/ablate.py" ${PCFG:-cfg2} 0 $m \
       > "$OUT/a$m.g$g.log" 2>&1 || { echo "variant $m group $g failed"; tail -5 "$OUT/a$m.g$g.log"; exit 1; }
   done
 done
