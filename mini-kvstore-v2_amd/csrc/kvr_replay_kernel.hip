@@ -95,6 +95,9 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #ifndef KVR_S8   // 1: slice-by-8 unit loop (8 table lookups per 8 bytes, half the dependent LDS steps)
 #define KVR_S8 1
 #endif
+#ifndef KVR_SPLITLOAD   // 1: the unit's halves CRC'd one after the other, each half's next-tile load issued
+#define KVR_SPLITLOAD 0    // as soon as its chain is done (0: both chains interleaved, one load after both)
+#endif
 #ifndef KVR_PSEL   // 1: per-lane v_perm selectors pick each lane group's byte (no rotation of x per step)
 #define KVR_PSEL 1
 #endif
@@ -718,6 +721,8 @@ __device__ __forceinline__ uint32_t short_value_crc(const TileSeg &ts, const Crc
 // this lane's 128-B unit of tile k: eight 16-B raw buffer loads through a per-tile resource whose
 // range is the 16-B words touching the segment, so words outside it read as 0 in hardware
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// (quads [Q0, Q1) of the unit: the whole unit, or one half while the other is still in use)
+template <int Q0 = 0, int Q1 = UW / 4>
 __device__ __forceinline__ void load_unit(const uint8_t *abase, int64_t d0, uint64_t len, uint32_t k, int lane,
                                           uint32_t *r) {
     const int64_t t0 = (int64_t)k * TILE;
@@ -732,10 +737,42 @@ __device__ __forceinline__ void load_unit(const uint8_t *abase, int64_t d0, uint
         (void *)(((uint64_t)bhi << 32) | blo), (short)0, nr, 0x00020000);
     const int vo = lane * SC - (int)skip;   // negative -> out of range -> 0
 #pragma unroll
-    for (int i = 0; i < UW / 4; ++i) {
+    for (int i = Q0; i < Q1; ++i) {
         const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16 * i, 0, 0);
         r[4 * i] = a.x; r[4 * i + 1] = a.y; r[4 * i + 2] = a.z; r[4 * i + 3] = a.w;
     }
+}
+
+// one half of a unit (words H0 .. H0 + 15) as one slice-by-8 chain: step st takes words H0 + 2 st
+// (x, the register folded in) and H0 + 2 st + 1 (y).  gen: some lane has a value boundary in the
+// unit; in this half (mine_m) the snapshot takes x at step sh, and (mine_a) a value starting at word
+// 2 sah (+1 when odd_a) restarts the chain: x = the masked word (even), or x = 0 and y masked (odd:
+// T[0] = 0, the register and the word before drop out).  Returns the half's register.
+template <int H0>
+__device__ __forceinline__ uint32_t s8_half(const uint32_t (&w)[UW], const Crc &K, bool gen, bool mine_m, bool mine_a,
+                                            int sh, int sah, bool odd_a, uint32_t amask, uint32_t &snx) {
+    constexpr int H2 = UW / 4;
+    uint32_t x = w[H0];
+    if (gen && mine_a && sah == 0) x = odd_a ? 0u : (w[H0] & amask);
+    uint32_t out = 0;
+#pragma unroll
+    for (int st = 0; st < H2; ++st) {
+        uint32_t y = w[H0 + 2 * st + 1];
+        if (gen) {
+            snx = mine_m && st == sh ? x : snx;
+            y = mine_a && st == sah && odd_a ? (y & amask) : y;   // restart at this step's odd word
+        }
+        uint32_t px, x3, py, y3;
+        look8(x, y, K, px, x3, py, y3);
+        if (st + 1 < H2) {
+            const uint32_t nw = w[H0 + 2 * st + 2];
+            x = xor3(px, x3, xor3(py, y3, nw));
+            if (gen) x = mine_a && st + 1 == sah ? (odd_a ? 0u : (nw & amask)) : x;   // restart at the next step
+        } else {
+            out = xor3(px, x3, py ^ y3);
+        }
+    }
+    return out;
 }
 
 // the reads of tile k relative to its first byte (see TileSeg)
@@ -1533,47 +1570,18 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             if (KVR_ABLATE & 8) {
                 ca = w[0]; cb = w[1];
             } else if (KVR_S8) {
-                // slice-by-8: step s takes words 2 s (x, the register folded in) and 2 s + 1 (y) of
-                // each half.  A restart at an even word replaces x by the masked word; at an odd one
-                // x becomes 0 (T[0] = 0: the register and the word before drop out) and y the masked
-                // word.  The snapshot takes x at step qh >> 1: for an even qh the register is x ^ wm,
-                // for an odd one it is one slice-by-4 step of x (after the loop).
-                constexpr int H2 = H / 2;
+                // slice-by-8, each half its own chain (s8_half); for an even qh the snapshot's
+                // register is x ^ wm, for an odd one it is one slice-by-4 step of x
                 const int sh = qh >> 1, sah = qah >= 0 ? (qah >> 1) : -1;
                 const bool odd_a = (qah & 1) != 0;
                 const bool gen = __ballot(m != 0 || qa >= 0) != 0ull;
-                uint32_t xa = w[0], xb = w[H], snx = 0;
-                if (gen) {
-                    const bool r0 = sah == 0;
-                    const uint32_t ma = r0 && !ab ? (odd_a ? 0u : (w[0] & amask)) : w[0];
-                    const uint32_t mbv = r0 && ab ? (odd_a ? 0u : (w[H] & amask)) : w[H];
-                    xa = ma; xb = mbv;
-                }
-#pragma unroll
-                for (int st = 0; st < H2; ++st) {
-                    uint32_t ya = w[2 * st + 1], yb = w[H + 2 * st + 1];
-                    if (gen) {
-                        snx = st == sh ? (mb ? xb : xa) : snx;
-                        const bool ro = st == sah && odd_a;   // restart at this step's odd word
-                        ya = ro && !ab ? (ya & amask) : ya;
-                        yb = ro && ab ? (yb & amask) : yb;
-                    }
-                    uint32_t pxa, xa3, pya, ya3, pxb, xb3, pyb, yb3;
-                    look8(xa, ya, K, pxa, xa3, pya, ya3);
-                    look8(xb, yb, K, pxb, xb3, pyb, yb3);
-                    if (st + 1 < H2) {
-                        const uint32_t na = w[2 * st + 2], nb_ = w[H + 2 * st + 2];
-                        xa = xor3(pxa, xa3, xor3(pya, ya3, na));
-                        xb = xor3(pxb, xb3, xor3(pyb, yb3, nb_));
-                        if (gen) {
-                            const bool r = st + 1 == sah;         // restart at the next step
-                            xa = r && !ab ? (odd_a ? 0u : (na & amask)) : xa;
-                            xb = r && ab ? (odd_a ? 0u : (nb_ & amask)) : xb;
-                        }
-                    } else {
-                        ca = xor3(pxa, xa3, pya ^ ya3);
-                        cb = xor3(pxb, xb3, pyb ^ yb3);
-                    }
+                uint32_t snx = 0;
+                ca = s8_half<0>(w, K, gen, !mb, !ab, sh, sah, odd_a, amask, snx);
+                if (KVR_SPLITLOAD && need_next) load_unit<0, UW / 8>(abase, d0, len, k + 1, lane, w);
+                cb = s8_half<H>(w, K, gen, mb, ab, sh, sah, odd_a, amask, snx);
+                if (KVR_SPLITLOAD && need_next) {
+                    load_unit<UW / 8, UW / 4>(abase, d0, len, k + 1, lane, w);
+                    loaded = true;
                 }
                 if (gen) {
                     const uint32_t s4 = crc4(0u, snx, K);   // (odd qh: one slice-by-4 step of x)
@@ -1617,7 +1625,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             }
             // the unit loop was the tile registers' last reader: the next tile's load is issued
             // here and its latency runs under the scan and the finalize
-            if (need_next) {
+            if (need_next && !loaded) {
                 load_unit(abase, d0, len, k + 1, lane, w);
                 loaded = true;
             }
