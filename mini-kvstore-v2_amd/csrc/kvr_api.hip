@@ -306,7 +306,11 @@ int kvr_ctx_create(int device, kvr_ctx **out) {
     if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return KVR_EHIP; }
     c->stream = c->own;
     for (auto &e : c->ev) if (hipEventCreate(&e) != hipSuccess) { delete c; return KVR_EHIP; }
-    if (hipHostMalloc(reinterpret_cast<void **>(&c->h_lc), LC_BYTES) != hipSuccess) { delete c; return KVR_ENOMEM; }
+    // (fine-grained: k_link writes it and k_compact_s adds to it from the device, see replay_one)
+    if (hipHostMalloc(reinterpret_cast<void **>(&c->h_lc), LC_BYTES, hipHostMallocCoherent) != hipSuccess) {
+        delete c;
+        return KVR_ENOMEM;
+    }
     c->h_link = reinterpret_cast<LinkResult *>(c->h_lc);
     c->h_ctr = reinterpret_cast<Counters *>(c->h_lc + LC_CTR);
     std::vector<uint32_t> crc, kmul, initx;
@@ -676,8 +680,9 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         launch_compact();
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[3], st));
-        // link result + counters: k_link and the compaction's last workgroup write them into the
-        // pinned mirror h_lc; when the call did not end cleanly they are copied as they are
+        // link result + counters: k_link writes them into the pinned mirror h_lc (and clears the
+        // device block after a clean pass), k_compact_s adds its CRC failures there; when the call
+        // did not end cleanly the device block is copied as it is
         HIPCHK(wait_stream(st, c->ev[5]));
         const bool clean = c->h_link->status == 0 && !c->h_ctr->overflow;
         if (!clean) {
@@ -754,12 +759,12 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             fprintf(stderr, "kvr: stripe linking did not converge after %u rounds\n", guard);
             return KVR_EHIP;
         }
-        bool cleared = clean;   // the compaction's last workgroup cleared the block
+        const bool cleared = clean;   // k_link cleared the block after a clean first pass
         if (recompact && c->h_link->status == 0 && !c->h_ctr->overflow) {
-            launch_compact();   // (its last workgroup writes the CRC failures to h_ctr, clears the block)
+            c->h_ctr->crc_fail = 0;
+            launch_compact();   // (its CRC failures go to h_ctr)
             HIPCHK(hipGetLastError());
             HIPCHK(hipStreamSynchronize(st));
-            cleared = true;
         }
         c->stats.n_link_passes = c->h_link->passes;
         if (c->h_ctr->overflow & 2u) {   // stitch did not converge (bug trap)

@@ -89,7 +89,7 @@ struct Counters {         // device scratch, reset per call
     unsigned long long total_tuples;
     unsigned long long crc_fail;
     uint32_t overflow;
-    uint32_t pad;         // k_compact_s: workgroups done (its last one clears the block)
+    uint32_t pad;
 };
 
 struct Tables {           // read-only tables in global memory (copied to LDS per workgroup)

@@ -257,13 +257,18 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
             L.err_aux = r.err_aux;
         }
         *res = L;
-        if (hres) {   // the host's pinned mirror, written straight (no copy on the stream)
+        if (hres) {   // the host's pinned mirror (fine-grained), written straight: no copy on the stream
             *hres = L;
+            const uint32_t ov = ctr->overflow;
             hctr->pool_cursor = ctr->pool_cursor;
-            hctr->overflow = ctr->overflow;
+            hctr->overflow = ov;
             hctr->total_tuples = (L.status == 0 && soff) ? all_recs : ctr->total_tuples;
-            hctr->crc_fail = 0;
-            __threadfence_system();
+            hctr->crc_fail = 0;   // (k_compact_s adds its failures here)
+            if (L.status == 0 && ov == 0u) {   // a clean pass: the block is cleared for the next call
+                res->passes = 0;
+                ctr->pool_cursor = 0;
+                ctr->total_tuples = 0;
+            }
         }
     }
 }
@@ -286,7 +291,7 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
                                                   const kvr_tuple *__restrict__ pool, uint64_t pool_cap,
                                                   kvr_tuple *__restrict__ out, uint64_t out_cap,
                                                   const uint32_t *__restrict__ expected, uint64_t n_expected,
-                                                  Counters *ctr, LinkResult *link,
+                                                  Counters *ctr, const LinkResult *__restrict__ link,
                                                   const uint4 *__restrict__ kpool, uint4 *__restrict__ kout,
                                                   Counters *hctr) {
     if (link->status != 0 || ctr->overflow) return;
@@ -307,22 +312,13 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
             if (half && kout) kout[o] = kpool[src];
         }
     };
-    // the last workgroup to finish hands the CRC failure count to the host's pinned mirror and
-    // clears the link + counters block for the next call (no copy or fill on the stream)
+    // the CRC failures go to the host's pinned mirror (a system-scope atomic, only for a wave
+    // that found any), or to the device counters
     auto finish = [&]() {
         for (int d = 32; d >= 1; d >>= 1) fails += __shfl_xor(fails, d, 64);
-        if ((threadIdx.x & 63) == 0 && fails) atomicAdd(&ctr->crc_fail, (unsigned long long)fails);
-        if (!hctr) return;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();
-            if (atomicAdd(&ctr->pad, 1u) == gridDim.x - 1) {
-                __threadfence();
-                hctr->crc_fail = __hip_atomic_load(&ctr->crc_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                *link = LinkResult{};
-                *ctr = Counters{};
-                __threadfence_system();
-            }
+        if ((threadIdx.x & 63) == 0 && fails) {
+            if (hctr) atomicAdd_system(&hctr->crc_fail, (unsigned long long)fails);
+            else atomicAdd(&ctr->crc_fail, (unsigned long long)fails);
         }
     };
     const uint64_t run = sres[blockIdx.x].pool_run;

@@ -93,7 +93,7 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #define KVR_LANEFRAME 1
 #endif
 #ifndef KVR_S8   // 1: slice-by-8 unit loop (8 table lookups per 8 bytes, half the dependent LDS steps)
-#define KVR_S8 1
+#define KVR_S8 0
 #endif
 #ifndef KVR_SPLITLOAD   // 1: the unit's halves CRC'd one after the other, each half's next-tile load issued
 #define KVR_SPLITLOAD 0    // as soon as its chain is done (0: both chains interleaved, one load after both)
@@ -1264,6 +1264,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const int32_t c = cur + (one ? 0 : lane * (int32_t)L);
                     const bool act = lane == 0 || (!one && c < vhiT);
                     const Dec d = decode(c, act, 0, true);
+                    KVR_STAMP(1);
                     // the first lane whose record is broken or whose successor is not the next
                     // prediction (the last active lane's successor is unconstrained)
                     const int n = (int)__builtin_popcountll(__ballot(act));
@@ -1283,6 +1284,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                         }
                         nrec = err_rec != N32 ? err_rec : nrec + n_on;
                     }
+                    KVR_STAMP(6);
                     if (!okf) { cur = (int32_t)cf; round_broke = true; break; }   // the exact loop reports it
                     const uint32_t nf = rl32(d.nx, f);
                     L = nf - cf;                               // record f's length predicts the next tile
@@ -1316,6 +1318,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 if (vhiT < TILE) mask_from(cm, vhiT - us);   // the segment's last tile: nothing past its end
                 const uint32_t cnt_u = (uint32_t)(__builtin_popcount(cm[0]) + __builtin_popcount(cm[1]) +
                                                   __builtin_popcount(cm[2]) + __builtin_popcount(cm[3]));
+                KVR_STAMP(7);
                 bool go = true;
 #pragma unroll 1
                 while (go && p < vhi_r && err_rec == N32) {
@@ -1353,6 +1356,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const uint64_t at0 = __ballot(act && c == p0);
                     Dec d = decode(act ? c : p0, act, at0 ? (int)__builtin_ctzll(at0) : 0, false);
                     const uint32_t nxp = act && d.ok ? d.nx : N32;
+                    KVR_STAMP(11);
                     // the chain from p through the window's candidates
                     uint32_t rk = N32, vl = d.vlen;
                     int32_t cur = p0;
@@ -1379,6 +1383,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                         cur = (int32_t)nxj;
                     }
                     d.vlen = vl;
+                    KVR_STAMP(12);
                     if (nb) {
                         const uint32_t slot0 = claim(nb);
                         const Fold fo = emit(d, c, rk != N32, rk, nb, lead, lastl, false, slot0);
@@ -1388,6 +1393,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     }
                     p = cur;
                     if (nb == 0u) go = false;
+                    KVR_STAMP(13);
                 }
             }
 #endif

@@ -57,8 +57,8 @@ for it in range(3):
     lib.kvr_last_stats(ctx, C.byref(st))
     lib.kvr_prof_read(prof, 0)
 # KVR_STAMP slots of kvr_replay_kernel.hip (unused slots print 0)
-names = ["setup(load)", "-", "framing+records", "finalize", "bookkeep", "wait(vmcnt)", "-", "-",
-         "crc-entry", "unit-loop+kmul", "scan", "-", "-", "-", "-", "-"]
+names = ["setup(load)", "stride-decode", "hop-loop+rest", "finalize", "bookkeep", "wait(vmcnt)", "stride-emit",
+         "cand-swar", "crc-entry", "unit-loop+kmul", "scan", "cand-decode", "cand-walk", "cand-emit", "-", "-"]
 tiles = st.n_tiles
 tot_c = sum(prof[i] for i in range(16))
 print(f"{cfg}: rc={rc} n={n.value}/{nrec} bytes={tot} tiles={tiles} stripes={st.n_stripes} ms_replay={st.ms_replay:.3f}"
