@@ -196,6 +196,24 @@ __device__ __forceinline__ void cand_masks(const uint32_t (&w)[UW], int64_t rem,
         cm[i >> 3] |= z >> (7 - (i & 7));
     }
 }
+// The candidate rounds' filter (cheaper, not a necessary condition): the opcode byte and the byte 4
+// on (the key length's top byte) are both 0x00 / 0x01, i.e. (w | x) & 0xFE is a zero byte: four
+// VALU a word, the accumulation two words at a time.  A record whose key is 32 MiB or longer is not
+// a candidate, so the chain stops there and the exact loop walks it.  Same layout as cand_masks.
+__device__ __forceinline__ void cand_masks_fast(const uint32_t (&w)[UW], uint32_t (&cm)[4]) {
+    cm[0] = cm[1] = cm[2] = cm[3] = 0u;
+    uint32_t z[UW];
+#pragma unroll
+    for (int i = 0; i < UW; ++i) {
+        const uint32_t x = i + 1 < UW ? w[i + 1] : 0u;   // (the unit's last word: its opcode bytes only)
+        const uint32_t v = (w[i] | x) & 0xFEFEFEFEu;                   // (one v_bitop3 each)
+        const uint32_t t = ((w[i] | x) & 0x7E7E7E7Eu) + 0x7F7F7F7Fu;
+        z[i] = ~(t | v | 0x7F7F7F7Fu);   // bit 7 of a byte: (w | x) & 0xFE is zero there
+    }
+#pragma unroll
+    for (int i = 0; i < UW; i += 2)
+        cm[i >> 3] |= (z[i] >> (7 - (i & 7))) | (z[i + 1] >> (7 - ((i + 1) & 7)));
+}
 // keep only the candidates at unit offsets below lim (any lim; <= 0 clears all)
 __device__ __forceinline__ void mask_from(uint32_t (&cm)[4], int32_t lim) {
 #pragma unroll
@@ -1303,18 +1321,18 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
 #if KVR_CANDFRAME
             if (!huge && p < vhi_r && err_rec == N32 && !round_broke) {
                 // ---- candidate chain: records of varying lengths, lane-parallel ----------------------
-                // Every byte of [p, vhi) that can start a record (an opcode byte 0x00 / 0x01 whose key
-                // length does not reach past the segment end in its top byte: SWAR over the registers)
-                // is a candidate.  A window takes the candidates of the units from p's on, as many
+                // Every byte of [p, vhi) that can start a record of a key shorter than 32 MiB (an opcode
+                // byte 0x00 / 0x01 with a key length whose top byte is 0x00 / 0x01: SWAR over the
+                // registers, cand_masks_fast) is a candidate.  A window takes the candidates of the units from p's on, as many
                 // whole units as fit 64: they go to one lane each (a scatter through this wave's LDS
                 // row) and are decoded there with their successor.  The chain from p then follows the
                 // candidates by lane matches (a ballot per record), which ranks the records: rank
                 // order is position order.  A window ends where its units end (the next one starts at
-                // the chain's position); a position that is not a candidate is a broken record (the
-                // filter is a necessary condition), left with the rest of the tile to the exact loop,
-                // and so is a unit holding more than 64 candidates.
+                // the chain's position); a position that is not a candidate (a broken record, or a key
+                // of 32 MiB or more) is left with the rest of the tile to the exact loop, and so is a
+                // unit holding more than 64 candidates.
                 uint32_t cm[4];
-                cand_masks(w, rem, cm);
+                cand_masks_fast(w, cm);
                 if (vhiT < TILE) mask_from(cm, vhiT - us);   // the segment's last tile: nothing past its end
                 const uint32_t cnt_u = (uint32_t)(__builtin_popcount(cm[0]) + __builtin_popcount(cm[1]) +
                                                   __builtin_popcount(cm[2]) + __builtin_popcount(cm[3]));
