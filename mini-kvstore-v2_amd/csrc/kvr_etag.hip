@@ -52,9 +52,8 @@ __device__ __forceinline__ void etag_desc(uint64_t d, uint64_t &start, uint32_t 
     first = (d >> 63) != 0;
 }
 
-// The byte tables are k_replay's (kvr_replay_kernel.hip, Crc): slice-by-8 (KVR_S8) replicated per
-// LDS bank group with the rotation trick, so no lookup of a wave conflicts; crc4 / crc1 / look8 are
-// k_replay's steps.
+// The byte tables are k_replay's (kvr_replay_kernel.hip, Crc): slice-by-4 replicated per LDS bank
+// group with the rotation trick, so no lookup of a wave conflicts; crc4 / crc1 are k_replay's steps.
 __device__ inline uint32_t crc_word4(const Crc &K, uint32_t c, uint32_t w) { return crc4(c, w, K); }
 
 __device__ inline uint32_t crc_byte(const Crc &K, uint32_t c, uint32_t b) { return crc1(c, b, K); }
@@ -109,33 +108,11 @@ __device__ inline uint32_t etag_unit_general(const Crc &T, const uint8_t *data, 
 
 // Persistent: as many workgroups as are resident (occupancy query); each wave takes ETAG_NC chunks per round and runs
 // their CRC chains interleaved (independent LDS lookup chains hide each other's latency).
-// slice-by-8 over NC full aligned chunks whose 16-B words are w[k][0..3] (per lane), chains
+// slice-by-4 over NC full aligned chunks whose 16-B words are w[k][0..3] (per lane), chains
 // interleaved; reg[k] in: the chain's start register, out: the lane's register pushed to the chunk end
 template <int NC>
 __device__ __forceinline__ void etag_fast(const Crc &T, const EtagSmem &S, uint32_t lane, const uint4 (&w)[NC][4],
                                           uint32_t (&reg)[NC]) {
-#if KVR_S8
-    uint32_t x[NC];
-#pragma unroll
-    for (int k = 0; k < NC; ++k) x[k] = reg[k] ^ w[k][0].x;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-#pragma unroll
-            for (int k = 0; k < NC; ++k) {
-                uint32_t px, x3, py, y3;
-                look8(x[k], h ? w[k][i].w : w[k][i].y, T, px, x3, py, y3);
-                if (i < 3 || h == 0) {
-                    const uint32_t nw = h ? w[k][i + (i < 3)].x : w[k][i].z;
-                    x[k] = xor3(px, x3, xor3(py, y3, nw));
-                } else {
-                    reg[k] = xor3(px, x3, py ^ y3);
-                }
-            }
-        }
-    }
-#else
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -147,7 +124,6 @@ __device__ __forceinline__ void etag_fast(const Crc &T, const EtagSmem &S, uint3
 #pragma unroll
         for (int k = 0; k < NC; ++k) reg[k] = crc_word4(T, reg[k], w[k][i].w);
     }
-#endif
     if (lane != 63) {
 #pragma unroll
         for (int k = 0; k < NC; ++k) reg[k] = kmul_lane(reg[k], S, lane);

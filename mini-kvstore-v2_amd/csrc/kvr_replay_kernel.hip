@@ -65,13 +65,19 @@ constexpr int WINW = KEYW + 3;            // decode window: dwords from the cand
 // Every table starts below 64 KiB, or is reached through a perm-built address that carries the
 // 64-KiB bit: a lookup is then one address VGPR plus a constant the ds_read instruction carries as
 // its 16-bit immediate offset, with no add (the byte tables C2 are the hot ones: 4 lookups a word).
+constexpr int KR_PITCH = 66;              // KR's row pitch in dwords (see kmul_col)
+#ifndef KVR_KQLPAD   // 1: KQL's rows padded like KR's (0: 64 dwords, one v_perm a lookup)
+#define KVR_KQLPAD 1
+#endif
+constexpr int KQL_PITCH = KVR_KQLPAD ? KR_PITCH : 64;
 struct __align__(16) Smem {
-    uint32_t KQ[NQ * 8 * 16];             // [q][i][n]: (n << 4i) * x^(8*4q), q <= SC/4 (a lane-uniform q)
+    uint32_t KQ2[2 * 8 * 16];             // [h][i][n]: (n << 4i) * x^(8*4q), q = SC/8 (h 0), SC/4 (h 1): the two
+                                          // lane-uniform pushes of the finalize
     uint32_t IX[NIX + 3];                 // 0xFFFFFFFF * x^(8j): initial register pushed through j bytes
     uint32_t MK[NWAVE][64];               // per wave: long-value marks by unit (framing)
     uint32_t C2[256 * 64];                // byte tables, row b = 256 B (64 KiB), see Crc
-    uint32_t KR[8 * 16 * 64];             // [i][n][k]: (n << 4i) * x^(8*SC*(k+1)), k < 64  (above 64 KiB,
-    uint32_t KQL[8 * 16 * 64];            // [i][n][q]: as KQ, q per lane (columns > SC/4: 0)  see kmul_col)
+    uint32_t KR[8 * 16 * KR_PITCH];       // [i][n][k]: (n << 4i) * x^(8*SC*(k+1)), k < 64  (above 64 KiB,
+    uint32_t KQL[8 * 16 * KQL_PITCH];     // [i][n][q]: (n << 4i) * x^(8*4q), q per lane (columns > SC/4: 0)  see kmul_col)
 };
 constexpr uint32_t KR_OFF = (uint32_t)offsetof(Smem, KR), KQL_OFF = (uint32_t)offsetof(Smem, KQL);
 static_assert(offsetof(Smem, C2) < 65536, "the byte tables' base fits a ds_read immediate");
@@ -92,17 +98,14 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #ifndef KVR_LANEFRAME   // 1: lane-parallel framing (0: the exact scalar hop loop for every record)
 #define KVR_LANEFRAME 1
 #endif
-#ifndef KVR_S8   // 1: slice-by-8 unit loop (8 table lookups per 8 bytes, half the dependent LDS steps)
-#define KVR_S8 0
-#endif
-#ifndef KVR_SPLITLOAD   // 1: the unit's halves CRC'd one after the other, each half's next-tile load issued
-#define KVR_SPLITLOAD 0    // as soon as its chain is done (0: both chains interleaved, one load after both)
-#endif
 #ifndef KVR_PSEL   // 1: per-lane v_perm selectors pick each lane group's byte (no rotation of x per step)
 #define KVR_PSEL 1
 #endif
 #ifndef KVR_CANDFRAME   // 1: candidate-chain rounds for what the stride round leaves (records of varying lengths)
 #define KVR_CANDFRAME 1
+#endif
+#ifndef KVR_SUCC   // 1: the candidate chain follows precomputed successor slots (0: a ballot per record)
+#define KVR_SUCC 1
 #endif
 #ifndef KVR_TOPWAIT   // 1: wait for the tile's load at the top of the loop (0: where its registers are
 #define KVR_TOPWAIT 0   // first read, so the framing round's window loads go out under the tile's load;
@@ -235,18 +238,15 @@ __device__ __forceinline__ void mask_from(uint32_t (&cm)[4], int32_t lim) {
 // Row b of Smem::C2 (64 dwords):
 //   [0, 32):  dword 8 t + r = table t (t = 0: one byte, t = k: a byte then k zero bytes) for byte
 //             b, replica r < 8 -- the slice-by-4 set
-//   [32, 64): KVR_S8: tables 4 .. 7 the same way (the slice-by-8 set of the unit loop: a step
-//             takes the register-folded word through tables 7 .. 4 and the next word through
-//             3 .. 0); otherwise [32, 48) is table 0, replica lane & 15 (single-byte steps)
+//   [32, 64): table 0, replica lane & 31 (single-byte steps: a half-wave's 32 lanes in 32 banks)
 // A slice-by-4 step x = c ^ w needs T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3].  Lane group
 // g = (lane >> 3) & 3 takes table (g + i) & 3 in its i-th lookup and replica lane & 7, so the 32
 // lanes of a half-wave hit 32 distinct banks in every lookup; the group's byte order is absorbed
 // by rotating x left by 8 g first (one v_alignbit), which keeps the four selectors uniform.
 struct Crc {
     const uint8_t *t;   // Smem::C2
-    uint32_t L;         // byte 0: T0 copy (KVR_S8: 4 (lane & 7); else 128 + 4 (lane & 15))
+    uint32_t L;         // byte 0: T0 copy, 128 + 4 (lane & 31)
     uint32_t L4;        // byte i: 4 (8 ((g + i) & 3) + (lane & 7)), this lane's i-th slice-by-4 lookup
-    uint32_t L4x;       // L4 + 128 per byte: the same lookups in tables 4 .. 7 (KVR_S8)
 #if KVR_PSEL
     uint32_t sel[4];    // lookup i's v_perm selector: byte 0 = L4's byte i, byte 1 = x's byte 3 - ((g + i) & 3)
 #else
@@ -254,15 +254,14 @@ struct Crc {
 #endif
 };
 // the C2 entry (dword) of LDS row b, column d: which table it holds (the staging loops)
-__host__ __device__ constexpr int c2_table(int d) { return KVR_S8 ? (d >> 3) : (d < 32 ? (d >> 3) : 0); }
+__host__ __device__ constexpr int c2_table(int d) { return d < 32 ? (d >> 3) : 0; }
 __device__ __forceinline__ void crc_init(Crc &K, const uint32_t *C2, uint32_t lane) {
-    const uint32_t g = (lane >> 3) & 3u, r = lane & 7u, r16 = lane & 15u;
+    const uint32_t g = (lane >> 3) & 3u, r = lane & 7u, r32 = lane & 31u;
     K.t = reinterpret_cast<const uint8_t *>(C2);
-    K.L = KVR_S8 ? 4u * r : 128u + 4u * r16;
+    K.L = 128u + 4u * r32;
     K.L4 = 0;
 #pragma unroll
     for (uint32_t i = 0; i < 4; ++i) K.L4 |= (4u * (8u * ((g + i) & 3u) + r)) << (8 * i);
-    K.L4x = K.L4 + 0x80808080u;
 #if KVR_PSEL
 #pragma unroll
     for (uint32_t i = 0; i < 4; ++i) K.sel[i] = 0x0C0C0000u | ((7u - ((g + i) & 3u)) << 8) | i;
@@ -326,25 +325,6 @@ __device__ __forceinline__ void look4x2(uint32_t xa, uint32_t xb, const Crc &k, 
     tb = xor3(b0, b1, b2);
     b3 = b3_;
 }
-// slice-by-8: the lookups of one step for two chains, x (register folded into the word) through
-// tables 7 .. 4 and y (the next word, no register) through tables 3 .. 0.  The step's result is
-// xor3(px, x3, xor3(py, y3, next word)): the y half does not wait for the chain, so the compiler
-// may issue it early.
-__device__ __forceinline__ uint32_t s8get(const Crc &k, uint32_t xr, uint32_t i) {
-    return *reinterpret_cast<const uint32_t *>(k.t + __builtin_amdgcn_perm(xr, k.L4x, crc_sel(k, i)));
-}
-__device__ __forceinline__ void look8(uint32_t x, uint32_t y, const Crc &k, uint32_t &px, uint32_t &x3, uint32_t &py,
-                                      uint32_t &y3) {
-    const uint32_t xr = crc_rot(x, k), yr = crc_rot(y, k);
-    uint32_t b0 = s4get(k, yr, 0), b1 = s4get(k, yr, 1), b2 = s4get(k, yr, 2), b3 = s4get(k, yr, 3);
-    uint32_t a0 = s8get(k, xr, 0), a1 = s8get(k, xr, 1), a2 = s8get(k, xr, 2), a3 = s8get(k, xr, 3);
-    asm("" : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
-    asm("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
-    px = xor3(a0, a1, a2);
-    x3 = a3;
-    py = xor3(b0, b1, b2);
-    y3 = b3;
-}
 __device__ __forceinline__ uint32_t crc1(uint32_t c, uint32_t b, const Crc &k) {
     const uint32_t x = c ^ b;
     return (x >> 8) ^ tget(k, x, SEL_T0_B0);
@@ -368,11 +348,14 @@ __device__ __forceinline__ uint32_t kmul(uint32_t v, const uint32_t *K) {
     return xor8(t);
 }
 // v times the constant in column k (per lane) of a [i][n][k] table of 64 columns (KR, KQL) at
-// byte OFF >= 64 KiB of Smem: entry (i, n, k) sits at OFF + i 4096 + n 256 + 4 k.  Its address is
-// one v_perm_b32: byte 0 = 4 k and byte 2 = 1 (the 64-KiB bit) from L4k, byte 1 = i << 4 | n from
-// a plane (each plane byte carries its lookup's i above the nibble), and the ds_read immediate is
-// OFF - 64 KiB
-template <uint32_t OFF>
+// byte OFF >= 64 KiB of Smem, rows of PITCH dwords: entry (i, n, k) sits at OFF + (16 i + n) 4 PITCH
+// + 4 k.  PITCH 64: the address is one v_perm_b32 (byte 0 = 4 k and byte 2 = 1, the 64-KiB bit,
+// from L4k; byte 1 = i << 4 | n from a plane, each plane byte carrying its lookup's i above the
+// nibble), and the ds_read immediate is OFF - 64 KiB.  A lookup's bank is then k mod 32 whatever
+// the nibble, so lanes that share a column (the pieces of different values pushed the same
+// distance, KR) conflict; PITCH 66 puts entry (n, k) in bank 2 n + k: one v_perm (the row byte)
+// and one v_mad_u32_u24 a lookup.
+template <uint32_t OFF, int PITCH = 64>
 __device__ __forceinline__ uint32_t kmul_col(uint32_t v, const Smem &S, uint32_t k4) {
     const uint32_t L4k = k4 | 0x10000u;
     // plane 0: nibbles i = 0, 2, 4, 6 (byte j: i = 2j), plane 1: i = 1, 3, 5, 7
@@ -381,9 +364,16 @@ __device__ __forceinline__ uint32_t kmul_col(uint32_t v, const Smem &S, uint32_t
     const uint8_t *tb = reinterpret_cast<const uint8_t *>(&S);
     uint32_t t[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-        t[i] = *reinterpret_cast<const uint32_t *>(
-            tb + (OFF - 65536u) + __builtin_amdgcn_perm(pl[i & 1], L4k, 0x0C020000u | ((4u + (uint32_t)(i >> 1)) << 8)));
+    for (int i = 0; i < 8; ++i) {
+        uint32_t a;
+        if constexpr (PITCH == 64) {
+            a = __builtin_amdgcn_perm(pl[i & 1], L4k, 0x0C020000u | ((4u + (uint32_t)(i >> 1)) << 8));
+        } else {
+            const uint32_t row = __builtin_amdgcn_perm(0u, pl[i & 1], 0x0C0C0C00u | (uint32_t)(i >> 1));
+            a = __umul24(row, 4u * (uint32_t)PITCH) + L4k;
+        }
+        t[i] = *reinterpret_cast<const uint32_t *>(tb + (OFF - 65536u) + a);
+    }
     return xor8(t);
 }
 
@@ -761,38 +751,6 @@ __device__ __forceinline__ void load_unit(const uint8_t *abase, int64_t d0, uint
     }
 }
 
-// one half of a unit (words H0 .. H0 + 15) as one slice-by-8 chain: step st takes words H0 + 2 st
-// (x, the register folded in) and H0 + 2 st + 1 (y).  gen: some lane has a value boundary in the
-// unit; in this half (mine_m) the snapshot takes x at step sh, and (mine_a) a value starting at word
-// 2 sah (+1 when odd_a) restarts the chain: x = the masked word (even), or x = 0 and y masked (odd:
-// T[0] = 0, the register and the word before drop out).  Returns the half's register.
-template <int H0>
-__device__ __forceinline__ uint32_t s8_half(const uint32_t (&w)[UW], const Crc &K, bool gen, bool mine_m, bool mine_a,
-                                            int sh, int sah, bool odd_a, uint32_t amask, uint32_t &snx) {
-    constexpr int H2 = UW / 4;
-    uint32_t x = w[H0];
-    if (gen && mine_a && sah == 0) x = odd_a ? 0u : (w[H0] & amask);
-    uint32_t out = 0;
-#pragma unroll
-    for (int st = 0; st < H2; ++st) {
-        uint32_t y = w[H0 + 2 * st + 1];
-        if (gen) {
-            snx = mine_m && st == sh ? x : snx;
-            y = mine_a && st == sah && odd_a ? (y & amask) : y;   // restart at this step's odd word
-        }
-        uint32_t px, x3, py, y3;
-        look8(x, y, K, px, x3, py, y3);
-        if (st + 1 < H2) {
-            const uint32_t nw = w[H0 + 2 * st + 2];
-            x = xor3(px, x3, xor3(py, y3, nw));
-            if (gen) x = mine_a && st + 1 == sah ? (odd_a ? 0u : (nw & amask)) : x;   // restart at the next step
-        } else {
-            out = xor3(px, x3, py ^ y3);
-        }
-    }
-    return out;
-}
-
 // the reads of tile k relative to its first byte (see TileSeg)
 __device__ __forceinline__ TileSeg tile_seg(const uint8_t *abase, const uint8_t *seg, int64_t d0, uint64_t len,
                                             uint32_t k) {
@@ -829,13 +787,15 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
     __shared__ Smem S;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (int i = tid; i < 256 * 64; i += RT) S.C2[i] = tb.crc8[c2_table(i & 63) * 256 + (i >> 6)];
-    for (int i = tid; i < 8 * 16 * 64; i += RT)
-        S.KR[i] = tb.kmul[((KSET_R + (i & 63)) * 8 + (i >> 10)) * 16 + ((i >> 6) & 15)];
-    for (int i = tid; i < 8 * 16 * 64; i += RT) {
-        const int q = i & 63;
-        S.KQL[i] = q < NQ ? tb.kmul[((KSET_Q + q) * 8 + (i >> 10)) * 16 + ((i >> 6) & 15)] : 0u;
+    for (int i = tid; i < 8 * 16 * KR_PITCH; i += RT) {
+        const int row = i / KR_PITCH, kk = i - row * KR_PITCH;   // row = 16 i + n
+        S.KR[i] = kk < 64 ? tb.kmul[((KSET_R + kk) * 8 + (row >> 4)) * 16 + (row & 15)] : 0u;
     }
-    for (int i = tid; i < NQ * 8 * 16; i += RT) S.KQ[i] = tb.kmul[KSET_Q * 8 * 16 + i];
+    for (int i = tid; i < 8 * 16 * KQL_PITCH; i += RT) {
+        const int row = i / KQL_PITCH, q = i - row * KQL_PITCH;   // row = 16 i + n
+        S.KQL[i] = q < NQ ? tb.kmul[((KSET_Q + q) * 8 + (row >> 4)) * 16 + (row & 15)] : 0u;
+    }
+    for (int i = tid; i < 2 * 8 * 16; i += RT) S.KQ2[i] = tb.kmul[(KSET_Q + (i < 128 ? SC / 8 : SC / 4)) * 8 * 16 + (i & 127)];
     if (tid < NIX) S.IX[tid] = tb.initx[tid];
     __syncthreads();   // the only workgroup barrier: from here on every wave is on its own
     uint32_t *const MK = S.MK[wv];   // this wave's long-value marks
@@ -1126,8 +1086,11 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 Dec d;
                 const int32_t a = c & ~3;
                 d.s = (uint32_t)c & 3u;
+                // (a lane that takes no part reads past the resource, which yields 0 with no memory
+                // access: the loads need no exec mask, so no branch around each of them)
+                const int32_t ao = act ? a : (int32_t)0x7FFFFF00;
 #pragma unroll
-                for (int i = 0; i < WINW; ++i) d.win[i] = act ? ts.w32a(a + 4 * i) : 0u;
+                for (int i = 0; i < WINW; ++i) d.win[i] = ts.w32a(ao + 4 * i);
                 const uint32_t x0 = __builtin_amdgcn_alignbyte(d.win[1], d.win[0], d.s);
                 const uint32_t x1 = __builtin_amdgcn_alignbyte(d.win[2], d.win[1], d.s);
                 d.op = x0 & 255u;
@@ -1374,24 +1337,47 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const uint64_t at0 = __ballot(act && c == p0);
                     Dec d = decode(act ? c : p0, act, at0 ? (int)__builtin_ctzll(at0) : 0, false);
                     const uint32_t nxp = act && d.ok ? d.nx : N32;
+                    const int32_t wend = cover < vhiT ? cover : vhiT;
+                    // each candidate's successor slot (KVR_SUCC): the row slots of the successor's unit
+                    // come from that unit's lane by one ds_bpermute (start | count << 8), and the few
+                    // slots are compared in parallel; -1 when none holds it (or the successor lies past
+                    // the window, or is unknown)
+                    int32_t sl = -1;
+                    if (KVR_SUCC) {
+                        const uint32_t rng = (fits && cnt) ? ((inc - cnt) | (cnt << 8)) : 0u;
+                        const bool want = nxp < (uint32_t)wend;   // (UNK and N32 are past any window)
+                        const uint32_t r2 =
+                            (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (want ? nxp >> SC_LOG : 0u)), (int)rng);
+                        const uint32_t s0 = r2 & 255u, sc = want ? (r2 >> 8) : 0u;
+                        const uint32_t mx = wave_max(sc);
+#pragma unroll 1
+                        for (uint32_t t = 0; t < mx; ++t) {
+                            const uint32_t pos = t < sc ? MK[(s0 + t) & 63u] : N32;
+                            sl = (sl < 0 && pos == nxp) ? (int32_t)(s0 + t) : sl;
+                        }
+                    }
                     KVR_STAMP(11);
                     // the chain from p through the window's candidates
                     uint32_t rk = N32, vl = d.vlen;
                     int32_t cur = p0;
                     uint32_t nb = 0;
                     int lead = 0, lastl = 0;
-                    const int32_t wend = cover < vhiT ? cover : vhiT;
+                    int j = at0 ? (int)__builtin_ctzll(at0) : -1;   // the lane holding cur (-1: look it up)
 #pragma unroll 1
                     while (cur < wend) {
-                        const uint64_t mm = __ballot(c == cur);
-                        if (mm == 0ull) { go = false; break; }   // not a candidate: a broken record
-                        const int j = (int)__builtin_ctzll(mm);
+                        if (j < 0) {
+                            const uint64_t mm = __ballot(c == cur);
+                            if (mm == 0ull) { go = false; break; }   // not a candidate: a broken record
+                            j = (int)__builtin_ctzll(mm);
+                        }
                         uint32_t nxj = rl32(nxp, j);
+                        int jn = (int)rl32((uint32_t)sl, j);
                         if (nxj == UNK) {                      // another key length: its value length
                             const int32_t e = cur + 5 + (int32_t)rl32(d.klen, j);
                             const uint32_t vj = e + 8 <= TILE ? (uint32_t)tu64(e) : uni32(ts.u32(e));
                             nxj = vj <= (uint32_t)(remT - e - 4) ? (uint32_t)(e + 4) + vj : N32;
                             vl = wl32(vl, vj, (uint32_t)j);
+                            jn = -1;
                         }
                         if (nxj == N32) { go = false; break; }   // a broken record: the exact loop reports it
                         rk = wl32(rk, nb, (uint32_t)j);
@@ -1399,6 +1385,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                         lastl = j;
                         ++nb;
                         cur = (int32_t)nxj;
+                        j = jn;
                     }
                     d.vlen = vl;
                     KVR_STAMP(12);
@@ -1593,24 +1580,6 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             uint32_t ca = 0, cb = 0, sn = 0;
             if (KVR_ABLATE & 8) {
                 ca = w[0]; cb = w[1];
-            } else if (KVR_S8) {
-                // slice-by-8, each half its own chain (s8_half); for an even qh the snapshot's
-                // register is x ^ wm, for an odd one it is one slice-by-4 step of x
-                const int sh = qh >> 1, sah = qah >= 0 ? (qah >> 1) : -1;
-                const bool odd_a = (qah & 1) != 0;
-                const bool gen = __ballot(m != 0 || qa >= 0) != 0ull;
-                uint32_t snx = 0;
-                ca = s8_half<0>(w, K, gen, !mb, !ab, sh, sah, odd_a, amask, snx);
-                if (KVR_SPLITLOAD && need_next) load_unit<0, UW / 8>(abase, d0, len, k + 1, lane, w);
-                cb = s8_half<H>(w, K, gen, mb, ab, sh, sah, odd_a, amask, snx);
-                if (KVR_SPLITLOAD && need_next) {
-                    load_unit<UW / 8, UW / 4>(abase, d0, len, k + 1, lane, w);
-                    loaded = true;
-                }
-                if (gen) {
-                    const uint32_t s4 = crc4(0u, snx, K);   // (odd qh: one slice-by-4 step of x)
-                    sn = qm == UW ? cb : ((qh & 1) ? s4 : (snx ^ wm));
-                }
             } else if (!__ballot(m != 0 || qa >= 0)) {
                 uint32_t xa = w[0], xb = w[H];
 #pragma unroll
@@ -1657,13 +1626,13 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             // (A does not count when that value starts in B's half); the raw CRC of the first
             // 4 qm bytes: A's snapshot, or all of A pushed through 4 (qm - H) bytes, then B's
             if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(KVR_FIN_PRIO);
-            const uint32_t pa = kmul(ca, S.KQ + 128 * H);
+            const uint32_t pa = kmul(ca, S.KQ2);
             const uint32_t c = qa >= H ? cb : (pa ^ cb);
             KVR_STAMP(9);
             uint32_t v = 0, fm = N32;            // segment start fm (all ones): no inflow from the previous unit
             if (vx) {
                 if (a_off >= 0) v = c ^ S.IX[SC - a_off];
-                else if (lane == 0 && vx_carry) v = c ^ kmul(c_state, S.KQ + 128 * (NQ - 1));   // carried register across unit 0
+                else if (lane == 0 && vx_carry) v = c ^ kmul(c_state, S.KQ2 + 128);   // carried register across unit 0
                 else { v = c; fm = 0u; }
             }
             // every piece pushed straight to where it is consumed (the unit before the one the
@@ -1675,7 +1644,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 const int32_t dd = ce - lane;
                 // (a lane with no push reads the broadcast entry of a zero register: its lookups add no
                 // distinct address to column 0's bank)
-                const uint32_t t_ = kmul_col<KR_OFF>(dd > 0 ? v : 0u, S, dd > 0 ? 4u * (uint32_t)(dd - 1) : 0u);
+                const uint32_t t_ = kmul_col<KR_OFF, KR_PITCH>(dd > 0 ? v : 0u, S, dd > 0 ? 4u * (uint32_t)(dd - 1) : 0u);
                 v = dd > 0 ? t_ : v;
                 // (a lane without a source reads 0 from the DPP move -- row_shr past the row start,
                 // the rows a broadcast skips -- which adds nothing and starts no segment, so no lane
@@ -1703,8 +1672,8 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             // (one per-lane multiply); then the r = m & 3 bytes past 4 qm, by linearity one chain
             if (!(KVR_ABLATE & 16) && m != 0) {
                 const int r = m & 3;
-                const uint32_t base = mb ? (kmul(sin, S.KQ + 128 * H) ^ ca) : sin;
-                uint32_t t = kmul_col<KQL_OFF>(base, S, 4u * (uint32_t)(mb ? qm - H : qm)) ^ sn;
+                const uint32_t base = mb ? (kmul(sin, S.KQ2) ^ ca) : sin;
+                uint32_t t = kmul_col<KQL_OFF, KQL_PITCH>(base, S, 4u * (uint32_t)(mb ? qm - H : qm)) ^ sn;
                 for (int b = 0; b < r; ++b) t = crc1(t, (wm >> (8 * b)) & 255u, K);
                 pool[slot_of(m_ref, m_abs)].crc32 = ~t;
             }
