@@ -103,6 +103,8 @@ struct kvr_ctx {
     // key prefixes for the fold: k_replay writes them per pool slot when kout is set, k_compact_s
     // moves them into kout (parallel to the output tuples); compact_front points kout at ckeys
     DevBuf<uint4> kpool, ckeys;
+    DevBuf<uint2> ctk;                     // the tuples' (key tag, key length) beside ckeys (k_compact_s):
+                                           // k_hll and k_fold_part read these instead of the tuples
     uint4 *kout = nullptr;
     bool ckeys_ok = false;                 // ckeys holds the prefixes of ctup[0, c_nt)
     DevBuf<RedoEnt> redo;
@@ -122,6 +124,10 @@ struct kvr_ctx {
     DevBuf<uint32_t> fsz;                  // the fold table's size on the device (k_hll_size)
     bool fold_pending = false;             // deferred rounds launched, not yet checked (fold_settle)
     DevBuf<uint32_t> cslot, cflag, cpos;
+    DevBuf<uint8_t> cfl8;                  // kvr_compact: a byte per tuple, live (k_live_ent -> k_dl_*)
+    DevBuf<uint32_t> dl_cnt;               // ... per block of DL_CH tuples: live count, then its prefix
+    DevBuf<uint64_t> dl_bytes;             // ... and live bytes, then their prefix
+    DevBuf<uint64_t> dl_tot;               // fold_derive's totals: live bytes (unused), live records
     DevBuf<uint64_t> csize, coff, l_src, l_off, ctot, ccuts;
     DevBuf<uint8_t> cout, ctmp;
     kvr_compact_stats cstats{};
@@ -344,10 +350,10 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->lcbuf.release();
     c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->soff.release();
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
-    c->kpool.release(); c->ckeys.release();
+    c->kpool.release(); c->ckeys.release(); c->ctk.release();
     c->ctup.release(); c->lout.release(); c->fent.release(); c->flist.release(); c->fcnt.release(); c->fsz.release();
     c->frec.release(); c->fwoff.release(); c->fhot.release();
-    c->cslot.release(); c->cflag.release(); c->islots.release(); c->ing.release(); c->hpart.release(); c->hreg.release();
+    c->cslot.release(); c->cflag.release(); c->cfl8.release(); c->dl_cnt.release(); c->dl_bytes.release(); c->dl_tot.release(); c->islots.release(); c->ing.release(); c->hpart.release(); c->hreg.release();
     c->koff.release(); c->klen.release(); c->kbuf.release();
     c->cpos.release(); c->csize.release(); c->coff.release(); c->l_src.release();
     c->l_off.release(); c->ctot.release(); c->ccuts.release(); c->cout.release(); c->ctmp.release();
@@ -643,6 +649,10 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             if (c->kpool.ensure(pool_cap + POOL_SLACK)) return KVR_ENOMEM;
             kp = c->kpool.p;
         }
+        // (key tag, key length) beside the prefixes (ctk parallels ckeys, where compact_front points kout)
+        uint2 *ktk = nullptr;
+        if (kp && c->kout >= c->ckeys.p && c->kout < c->ckeys.p + c->ckeys.n && c->ctk.n >= c->ckeys.n)
+            ktk = c->ctk.p + (c->kout - c->ckeys.p);
         kvr_tuple *d_out;
         uint64_t out_cap;
         if (flags & KVR_OUT_ON_DEVICE) {
@@ -659,7 +669,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             hipLaunchKernelGGL(k_compact_s, dim3(n_stripes), dim3(CT), 0, st, c->segs.p, c->stripes.p, c->sres.p, c->soff.p,
                                c->tres.p, c->pool.p, pool_cap, d_out, out_cap, d_exp,
                                (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p, kp, kp ? c->kout : nullptr,
-                               c->h_ctr);
+                               kp ? reinterpret_cast<uint32_t *>(ktk) : nullptr, c->h_ctr);
         };
         // counters and link result start at zero (the last successful call cleared them behind its
         // results, so this memset usually runs only on a context's first call or after an error)
@@ -831,12 +841,12 @@ static int compact_front(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t
     // 1. replay into context-resident tuples; the segment bytes stay in HBM (c->segs)
     size_t nt = 0;
     c->ckeys_ok = false;
-    if (c->ctup.ensure(bytes_in / 64 + 1024) || c->ckeys.ensure(c->ctup.n)) return KVR_ENOMEM;
+    if (c->ctup.ensure(bytes_in / 64 + 1024) || c->ckeys.ensure(c->ctup.n) || c->ctk.ensure(c->ckeys.n)) return KVR_ENOMEM;
     const uint32_t rflags = (flags & KVR_SEGS_ON_DEVICE) | KVR_OUT_ON_DEVICE;
     c->kout = c->ckeys.p;   // the tuples' key prefixes alongside them (k_fold_claim / k_fold_verify)
     int rc = kvr_replay(c, segs, n, rflags, nullptr, 0, c->ctup.p, c->ctup.n, &nt, err);
     if (rc == KVR_CAPACITY) {
-        if (c->ctup.ensure(nt) || c->ckeys.ensure(c->ctup.n)) { c->kout = nullptr; return KVR_ENOMEM; }
+        if (c->ctup.ensure(nt) || c->ckeys.ensure(c->ctup.n) || c->ctk.ensure(c->ckeys.n)) { c->kout = nullptr; return KVR_ENOMEM; }
         c->kout = c->ckeys.p;
         rc = kvr_replay(c, segs, n, rflags, nullptr, 0, c->ctup.p, c->ctup.n, &nt, err);
     }
@@ -888,12 +898,14 @@ static int fold_launch(kvr_ctx *c, size_t nt, bool deferred) {
     c->fold_est = 0;
     c->fold_pending = false;
     const bool tiny = getenv("KVR_FOLD_TINY_TABLE") != nullptr;   // test knob: force the full-size redo
+    const uint2 *tk = (c->ckeys_ok && c->ctk.n >= nt) ? c->ctk.p : nullptr;   // (key tag, key length) per tuple
     if (tiny) {
         hipLaunchKernelGGL(k_fold_setsize, dim3(1), dim3(1), 0, st, c->fsz.p, 15u);
     } else if (nt >= 65536) {
         const uint32_t hb = (uint32_t)std::min<uint64_t>((nt + HLL_T - 1) / HLL_T, 2ull * (uint64_t)c->n_cu);
         if (c->hpart.ensure((uint64_t)hb * HLL_M) || c->hreg.ensure(HLL_M)) return KVR_ENOMEM;
-        hipLaunchKernelGGL(k_hll, dim3(hb), dim3(HLL_T), 0, st, c->ctup.p, (uint64_t)nt, c->hpart.p);
+        // (from the key tags k_compact_s wrote beside the prefixes: 8 B a tuple instead of 32)
+        hipLaunchKernelGGL(k_hll, dim3(hb), dim3(HLL_T), 0, st, c->ctup.p, tk, (uint64_t)nt, c->hpart.p);
         hipLaunchKernelGGL(k_hll_merge, dim3(HLL_M / 16 / HLL_MG), dim3(HLL_MERGE_T), 0, st, c->hpart.p, hb, c->hreg.p);
         hipLaunchKernelGGL(k_hll_size, dim3(1), dim3(HLL_SIZE_T), 0, st, c->hreg.p, full_slots, c->fsz.p);
     } else {
@@ -939,7 +951,7 @@ again:
     HIPCHK(hipMemsetAsync(c->fcnt.p, 0, (FOLD_CNT * FOLD_SPEC_ROUNDS + 1) * sizeof(uint32_t), st));
     if (part) {
         hipLaunchKernelGGL(k_fold_part, dim3((uint32_t)nwg), dim3(FP_T), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p, kd,
-                           c->fsz.p, s_lim, c->frec.p, c->fwoff.p);
+                           tk, c->fsz.p, s_lim, c->frec.p, c->fwoff.p);
         // (a synced fold serves kvr_compact_stage, whose k_cand reads every tuple's entry)
         hipLaunchKernelGGL(k_fold_lds, dim3((uint32_t)p_host), dim3(FP_T), 0, st, c->ctup.p, c->segs.p, c->fsz.p, s_lim,
                            c->frec.p, c->fwoff.p, (uint32_t)nwg, c->fent.p, c->flist.p, c->fcnt.p, c->cslot.p,
@@ -1029,18 +1041,16 @@ static bool fold_check_eval(kvr_ctx *c, const FoldCheck &fc) {
 }
 
 // after the caller's sync point: did the deferred rounds finish the fold?  Reads the counters
-// (and, when last2 is given, the live totals cpos[nt - 1], cflag[nt - 1]) with one sync; if the
-// fold was not complete it is redone synchronously and *redone is set (the caller then redoes
-// what it derived from the table).
-static int fold_settle(kvr_ctx *c, size_t nt, bool *redone, uint32_t *last2) {
+// (and, when n_live is given, the live count fold_derive's scan left in dl_tot[1]) with one sync;
+// if the fold was not complete it is redone synchronously and *redone is set (the caller then
+// redoes what it derived from the table).
+static int fold_settle(kvr_ctx *c, size_t nt, bool *redone, uint64_t *n_live) {
+    (void)nt;
     *redone = false;
     hipStream_t st = c->stream;
     FoldCheck fc{};
     HIPCHK(fold_check_enqueue(c, &fc));
-    if (last2) {
-        HIPCHK(hipMemcpyAsync(&last2[0], c->cpos.p + nt - 1, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(&last2[1], c->cflag.p + nt - 1, 4, hipMemcpyDeviceToHost, st));
-    }
+    if (n_live) HIPCHK(hipMemcpyAsync(n_live, c->dl_tot.p + 1, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     if (fold_check_eval(c, fc)) return KVR_OK;
     *redone = true;
@@ -1049,18 +1059,24 @@ static int fold_settle(kvr_ctx *c, size_t nt, bool *redone, uint32_t *last2) {
 
 // live flags (and, for a rewrite, record sizes) of the tuples from the fold table
 // (keep_del: the last record of every key, tombstones included)
-static hipError_t live_flags(kvr_ctx *c, size_t nt, bool sizes, bool keep_del = false, bool packed = false) {
+// (sparse: a byte per tuple in cfl8 instead, for kvr_compact's dense list, k_dl_*)
+static hipError_t live_flags(kvr_ctx *c, size_t nt, bool sizes, bool keep_del = false, bool sparse = false) {
     hipStream_t st = c->stream;
-    hipError_t e = packed ? hipSuccess : hipMemsetAsync(c->cflag.p, 0, nt * 4, st);
-    if (e == hipSuccess && (sizes || packed)) e = hipMemsetAsync(c->csize.p, 0, nt * 8, st);
+    const uint64_t nfl = (nt + DL_CH - 1) / DL_CH * DL_CH;
+    if (sparse && c->cfl8.ensure(nfl)) return hipErrorOutOfMemory;
+    hipError_t e = sparse ? hipMemsetAsync(c->cfl8.p, 0, nfl, st) : hipMemsetAsync(c->cflag.p, 0, nt * 4, st);
+    if (e == hipSuccess && sizes && !sparse) e = hipMemsetAsync(c->csize.p, 0, nt * 8, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_live_ent, dim3(fold_grid(c)), dim3(256), 0, st, c->fent.p, c->fsz.p, c->ctup.p,
-                       (sizes || packed) ? c->csize.p : nullptr, packed ? nullptr : c->cflag.p, keep_del ? 1u : 0u);
+                       (sizes && !sparse) ? c->csize.p : nullptr, sparse ? nullptr : c->cflag.p,
+                       sparse ? c->cfl8.p : nullptr, keep_del ? 1u : 0u);
     return hipGetLastError();
 }
-// kvr_compact's sizes and live flags in one word (size << 24 | live), one scan for both
+// kvr_compact's dense live list from byte flags (k_dl_count / k_dl_scan / k_dl_fill); the two scans
+// over every tuple (sizes, live flags) remain as a test and timing knob
 static bool compact_packed(const kvr_ctx *c, size_t nt) {
-    return nt < (1ull << 24) && c->cstats.bytes_in < (1ull << 40) && getenv("KVR_COMPACT_TWO_SCANS") == nullptr;
+    (void)c; (void)nt;
+    return getenv("KVR_COMPACT_TWO_SCANS") == nullptr;
 }
 
 // sizes and live flags are in csize / cflag: scans, dense live list, cuts, gather, output
@@ -1072,11 +1088,13 @@ static int compact_back(kvr_ctx *c, uint32_t flags, uint64_t seg_target, uint8_t
     hipStream_t st = c->stream;
     const uint32_t g = (uint32_t)((nt + 255) / 256);
     size_t tb = c->ctmp.n;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->csize.p, c->coff.p, (int)nt, st));
+    const uint32_t nb = (uint32_t)((nt + DL_CH - 1) / DL_CH);
     if (packed) {
-        hipLaunchKernelGGL(k_ctotals_p, dim3(1), dim3(64), 0, st, c->csize.p, c->coff.p, (uint64_t)nt, c->l_off.p,
-                           c->ctot.p);
+        if (c->dl_cnt.ensure(nb) || c->dl_bytes.ensure(nb)) return KVR_ENOMEM;
+        hipLaunchKernelGGL(k_dl_count, dim3(nb), dim3(DL_T), 0, st, c->cfl8.p, c->ctup.p, c->dl_cnt.p, c->dl_bytes.p);
+        hipLaunchKernelGGL(k_dl_scan, dim3(1), dim3(DL_ST), 0, st, c->dl_cnt.p, c->dl_bytes.p, nb, c->l_off.p, c->ctot.p);
     } else {
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->csize.p, c->coff.p, (int)nt, st));
         tb = c->ctmp.n;
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->cflag.p, c->cpos.p, (int)nt, st));
         hipLaunchKernelGGL(k_ctotals, dim3(1), dim3(64), 0, st, c->csize.p, c->coff.p, c->cflag.p, c->cpos.p,
@@ -1088,8 +1106,8 @@ static int compact_back(kvr_ctx *c, uint32_t flags, uint64_t seg_target, uint8_t
     const uint64_t max_cuts = seg_target ? bytes_in / seg_target + 1 : 1;
     if (c->ccuts.ensure(max_cuts)) return KVR_ENOMEM;
     if (packed)
-        hipLaunchKernelGGL(k_scatter_p, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p, c->csize.p,
-                           c->coff.p, c->l_src.p, c->l_off.p);
+        hipLaunchKernelGGL(k_dl_fill, dim3(nb), dim3(DL_T), 0, st, c->cfl8.p, c->ctup.p, c->segs.p, c->dl_cnt.p,
+                           c->dl_bytes.p, c->l_src.p, c->l_off.p);
     else
         hipLaunchKernelGGL(k_scatter, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->segs.p, c->csize.p,
                            c->coff.p, c->cflag.p, c->cpos.p, c->l_src.p, c->l_off.p);

@@ -127,12 +127,14 @@ __device__ __forceinline__ uint32_t hll_mix(uint32_t h) {   // independent of ht
     h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
     return h;
 }
-__global__ void __launch_bounds__(HLL_T) k_hll(const kvr_tuple *__restrict__ tup, uint64_t n, uint8_t *__restrict__ part) {
+// (tk: (key tag, key length) per tuple, written by k_compact_s beside the key prefixes; else the tuples')
+__global__ void __launch_bounds__(HLL_T) k_hll(const kvr_tuple *__restrict__ tup, const uint2 *__restrict__ tk,
+                                               uint64_t n, uint8_t *__restrict__ part) {
     __shared__ uint32_t reg[HLL_M];
     for (int j = threadIdx.x; j < HLL_M; j += HLL_T) reg[j] = 0;
     __syncthreads();
     for (uint64_t i = (uint64_t)blockIdx.x * HLL_T + threadIdx.x; i < n; i += (uint64_t)gridDim.x * HLL_T) {
-        const uint32_t x = hll_mix(tup[i].key_tag);
+        const uint32_t x = hll_mix(tk ? tk[i].x : tup[i].key_tag);
         const uint32_t rank = (uint32_t)__clz((x << HLL_P) | (1u << (HLL_P - 1))) + 1u;
         atomicMax(&reg[x >> (32 - HLL_P)], rank);
     }
@@ -405,6 +407,7 @@ __device__ uint32_t block_excl_scan(uint32_t *a, uint32_t n, uint32_t *wsum) {
 // An LDS histogram gives each tuple its rank in its bucket, its prefix sum the buckets' offsets.
 __global__ void __launch_bounds__(FP_T, 8) k_fold_part(const kvr_tuple *__restrict__ tup, uint64_t n,
                                                        const SegDesc *__restrict__ segs, const uint4 *__restrict__ kd,
+                                                       const uint2 *__restrict__ tk,
                                                        const uint32_t *__restrict__ fsz, uint32_t s_lim,
                                                        FPRec *__restrict__ rec, uint32_t *__restrict__ woff) {
     __shared__ uint32_t hist[FP_PMAX + 1];
@@ -419,8 +422,14 @@ __global__ void __launch_bounds__(FP_T, 8) k_fold_part(const kvr_tuple *__restri
     for (int u = 0; u < FP_PER; ++u) {
         const uint64_t i = base + (uint64_t)u * FP_T;
         if (i < n) {
-            tag[u] = tup[i].key_tag;
-            kl[u] = tup[i].key_len;
+            if (tk) {   // (8 B a tuple instead of the tuple's 32)
+                const uint2 q = tk[i];
+                tag[u] = q.x;
+                kl[u] = q.y;
+            } else {
+                tag[u] = tup[i].key_tag;
+                kl[u] = tup[i].key_len;
+            }
             const uint32_t b = (ht_mix(tag[u]) & G.mask) >> G.shift;
             bk[u] = b << 13 | atomicAdd(&hist[b], 1u);
         }
@@ -692,9 +701,10 @@ __device__ __forceinline__ bool is_last(const FoldEnt *ent, const uint32_t *slot
 // (keep_del: every key's last record, a DEL included — the per-GPU reduction of a sharded store,
 // whose tombstones may delete a key another GPU SET)
 // (grid-stride over the table size on the device)
+// (flag8: one byte a tuple instead, for the dense list above; size and flag are then null)
 __global__ void k_live_ent(const FoldEnt *__restrict__ ent, const uint32_t *__restrict__ fsz,
                            const kvr_tuple *__restrict__ tup, uint64_t *__restrict__ size,
-                           uint32_t *__restrict__ flag, uint32_t keep_del) {
+                           uint32_t *__restrict__ flag, uint8_t *__restrict__ flag8, uint32_t keep_del) {
     const uint64_t n_slots = (uint64_t)fsz[0] + 1;
     for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n_slots; h += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 a = reinterpret_cast<const uint4 *>(&ent[h])[0];
@@ -702,12 +712,175 @@ __global__ void k_live_ent(const FoldEnt *__restrict__ ent, const uint32_t *__re
         const uint32_t j = ~a.z;
         const kvr_tuple t = tup[j];
         if (t.op != 0 && !keep_del) continue;
+        if (flag8) {
+            flag8[j] = 1u;
+            continue;
+        }
         if (!flag) {   // packed (kvr_compact): size << 24 | 1, one scan gives offsets and positions
             size[j] = (9ull + t.key_len + t.val_len) << 24 | 1ull;
             continue;
         }
         flag[j] = 1u;
         if (size) size[j] = 9ull + t.key_len + t.val_len;   // SET framing, engine.rs:169-173
+    }
+}
+
+// ---- the dense live list from byte flags (kvr_compact; round 4) ----------------------------------
+// k_live_ent marks each live tuple with a byte (flag8; 0.5 M of cfg4's 8 M tuples), then: per block of
+// DL_CH tuples its live count and bytes (k_dl_count, 16 flags a thread as one 16-B load, the tuple
+// read only when live), one workgroup scans the blocks (k_dl_scan), and each block writes its live
+// records' sources and output offsets (k_dl_fill).  No per-tuple size array, no scan over every
+// tuple: the flags are nt bytes, against 8 B a tuple for the packed scan this replaces.
+constexpr int DL_T = 256, DL_PER = 16, DL_CH = DL_T * DL_PER;   // tuples per block: 4096
+__device__ __forceinline__ uint64_t rec_size(const kvr_tuple &t) { return 9ull + t.key_len + t.val_len; }   // engine.rs:169-173
+// (flags of the thread's 16 tuples: flag8 holds nt bytes rounded up to DL_CH, zero past nt)
+__device__ __forceinline__ uint4 dl_flags(const uint8_t *flag8, uint64_t i0) {
+    return *reinterpret_cast<const uint4 *>(flag8 + i0);
+}
+// the thread's live count and bytes over its 16 tuples (tup null: the count alone)
+__device__ __forceinline__ void dl_sums(const uint4 f, const kvr_tuple *tup, uint64_t i0, uint32_t &c, uint64_t &by) {
+    const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
+    c = 0;
+    by = 0;
+#pragma unroll
+    for (int k = 0; k < DL_PER; ++k) {
+        if ((fw[k >> 2] >> (8 * (k & 3))) & 255u) {
+            ++c;
+            if (tup) by += rec_size(tup[i0 + k]);
+        }
+    }
+}
+// block-wide exclusive prefix of (count, bytes) over DL_T threads; returns the block's totals
+__device__ __forceinline__ void dl_block_scan(uint32_t &c, uint64_t &by, uint32_t &tc, uint64_t &tby) {
+    __shared__ uint32_t wc[DL_T / 64];
+    __shared__ uint64_t wb[DL_T / 64];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    uint32_t xc = c;
+    uint64_t xb = by;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t yc = __shfl_up(xc, d, 64);
+        const uint64_t yb = __shfl_up(xb, d, 64);
+        if (lane >= d) { xc += yc; xb += yb; }
+    }
+    if (lane == 63u) { wc[w] = xc; wb[w] = xb; }
+    __syncthreads();
+    uint32_t pc = 0;
+    uint64_t pb = 0;
+    tc = 0;
+    tby = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < DL_T / 64; ++k) {
+        if (k < w) { pc += wc[k]; pb += wb[k]; }
+        tc += wc[k];
+        tby += wb[k];
+    }
+    c = pc + xc - c;
+    by = pb + xb - by;
+}
+__global__ void __launch_bounds__(DL_T) k_dl_count(const uint8_t *__restrict__ flag8, const kvr_tuple *__restrict__ tup,
+                                                   uint32_t *__restrict__ bcnt, uint64_t *__restrict__ bbytes) {
+    const uint64_t i0 = (uint64_t)blockIdx.x * DL_CH + (uint64_t)threadIdx.x * DL_PER;
+    uint32_t c;
+    uint64_t by;
+    dl_sums(dl_flags(flag8, i0), tup, i0, c, by);
+    uint32_t tc;
+    uint64_t tby;
+    dl_block_scan(c, by, tc, tby);
+    if (threadIdx.x == 0) { bcnt[blockIdx.x] = tc; bbytes[blockIdx.x] = tby; }
+}
+// one workgroup: the blocks' exclusive prefixes in place, 1024 blocks a pass; the totals to
+// totals[0] (bytes), totals[1] (live records) and the dense offsets' end sentinel l_off[live]
+constexpr int DL_ST = 1024;
+__global__ void __launch_bounds__(DL_ST) k_dl_scan(uint32_t *__restrict__ bcnt, uint64_t *__restrict__ bbytes, uint32_t nb,
+                                                   uint64_t *__restrict__ l_off, uint64_t *__restrict__ totals) {
+    __shared__ uint32_t wc[DL_ST / 64];
+    __shared__ uint64_t wb[DL_ST / 64];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    uint32_t carry_c = 0;
+    uint64_t carry_b = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += DL_ST) {
+        const uint32_t b = b0 + threadIdx.x;
+        const uint32_t c = b < nb ? bcnt[b] : 0u;
+        const uint64_t by = b < nb ? bbytes[b] : 0ull;
+        uint32_t xc = c;
+        uint64_t xb = by;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t yc = __shfl_up(xc, d, 64);
+            const uint64_t yb = __shfl_up(xb, d, 64);
+            if (lane >= d) { xc += yc; xb += yb; }
+        }
+        if (lane == 63u) { wc[w] = xc; wb[w] = xb; }
+        __syncthreads();
+        uint32_t pc = carry_c, tc = 0;
+        uint64_t pb = carry_b, tb = 0;
+        for (uint32_t k = 0; k < DL_ST / 64; ++k) {
+            if (k < w) { pc += wc[k]; pb += wb[k]; }
+            tc += wc[k];
+            tb += wb[k];
+        }
+        if (b < nb) { bcnt[b] = pc + xc - c; bbytes[b] = pb + xb - by; }
+        carry_c += tc;
+        carry_b += tb;
+        __syncthreads();   // (wc / wb are rewritten by the next pass)
+    }
+    if (threadIdx.x == 0) {
+        totals[0] = carry_b;
+        totals[1] = carry_c;
+        if (l_off) l_off[carry_c] = carry_b;
+    }
+}
+__global__ void __launch_bounds__(DL_T) k_dl_fill(const uint8_t *__restrict__ flag8, const kvr_tuple *__restrict__ tup,
+                                                  const SegDesc *__restrict__ segs, const uint32_t *__restrict__ bcnt,
+                                                  const uint64_t *__restrict__ bbytes, uint64_t *__restrict__ l_src,
+                                                  uint64_t *__restrict__ l_off) {
+    const uint64_t i0 = (uint64_t)blockIdx.x * DL_CH + (uint64_t)threadIdx.x * DL_PER;
+    const uint4 f = dl_flags(flag8, i0);
+    uint32_t c;
+    uint64_t by;
+    dl_sums(f, tup, i0, c, by);
+    uint32_t tc;
+    uint64_t tby;
+    dl_block_scan(c, by, tc, tby);
+    if (tc == 0) return;
+    uint64_t d = (uint64_t)bcnt[blockIdx.x] + c, o = bbytes[blockIdx.x] + by;
+    const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+    for (int k = 0; k < DL_PER; ++k) {
+        if ((fw[k >> 2] >> (8 * (k & 3))) & 255u) {
+            const kvr_tuple t = tup[i0 + k];
+            l_src[d] = reinterpret_cast<uint64_t>(segs[t.seg_idx].base + t.rec_off);
+            l_off[d] = o;
+            ++d;
+            o += rec_size(t);
+        }
+    }
+}
+
+// the same dense list for the index (fold_derive): the live tuples themselves, and each live
+// tuple's place in the list (pos, read by k_index_from_fold at the live tuples only)
+__global__ void __launch_bounds__(DL_T) k_dl_fill_tup(const uint8_t *__restrict__ flag8, const kvr_tuple *__restrict__ tup,
+                                                      const uint32_t *__restrict__ bcnt, kvr_tuple *__restrict__ out,
+                                                      uint32_t *__restrict__ pos) {
+    const uint64_t i0 = (uint64_t)blockIdx.x * DL_CH + (uint64_t)threadIdx.x * DL_PER;
+    const uint4 f = dl_flags(flag8, i0);
+    uint32_t c;
+    uint64_t by;
+    dl_sums(f, nullptr, i0, c, by);
+    uint32_t tc;
+    uint64_t tby;
+    dl_block_scan(c, by, tc, tby);
+    if (tc == 0) return;
+    uint32_t d = bcnt[blockIdx.x] + c;
+    const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+    for (int k = 0; k < DL_PER; ++k) {
+        if ((fw[k >> 2] >> (8 * (k & 3))) & 255u) {
+            out[d] = tup[i0 + k];
+            pos[i0 + k] = d;
+            ++d;
+        }
     }
 }
 
@@ -734,29 +907,6 @@ __global__ void k_scatter(const kvr_tuple *__restrict__ tup, uint64_t n, const S
     const uint32_t j = pos[i];
     l_src[j] = reinterpret_cast<uint64_t>(segs[t.seg_idx].base + t.rec_off);
     l_off[j] = off[i];
-}
-
-// the packed forms (kvr_compact when n < 2^24 and the bytes < 2^40): sz[i] = size << 24 | live,
-// its exclusive scan off[i] = offset << 24 | position
-__global__ void k_ctotals_p(const uint64_t *__restrict__ sz, const uint64_t *__restrict__ off, uint64_t n,
-                            uint64_t *__restrict__ l_off, uint64_t *__restrict__ totals) {
-    if (threadIdx.x || blockIdx.x) return;
-    const uint64_t e = n ? off[n - 1] + sz[n - 1] : 0;
-    const uint64_t bytes = e >> 24, live = e & 0xFFFFFFull;
-    l_off[live] = bytes;
-    totals[0] = bytes;
-    totals[1] = live;
-}
-__global__ void k_scatter_p(const kvr_tuple *__restrict__ tup, uint64_t n, const SegDesc *__restrict__ segs,
-                            const uint64_t *__restrict__ sz, const uint64_t *__restrict__ off,
-                            uint64_t *__restrict__ l_src, uint64_t *__restrict__ l_off) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !(sz[i] & 1ull)) return;
-    const kvr_tuple t = tup[i];
-    const uint64_t o = off[i];
-    const uint64_t j = o & 0xFFFFFFull;
-    l_src[j] = reinterpret_cast<uint64_t>(segs[t.seg_idx].base + t.rec_off);
-    l_off[j] = o >> 24;
 }
 
 // one wave per live record (grid-stride over records): the record's source and

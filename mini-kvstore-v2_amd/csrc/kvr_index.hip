@@ -15,13 +15,6 @@
  */
 
 namespace {
-// live list: tuple i -> out[pos[i]] if flag[i]
-__global__ void k_live_tuples(const kvr_tuple *__restrict__ tup, uint64_t n, const uint32_t *__restrict__ flag,
-                              const uint32_t *__restrict__ pos, kvr_tuple *__restrict__ out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n && flag[i]) out[pos[i]] = tup[i];
-}
-
 // the home slot of a key tag (kvr_index_hash, host and device): the fold table's hash, since
 // the index IS the fold table, entry for entry
 __host__ __device__ __forceinline__ uint32_t ix_hash(uint32_t h) { return ht_mix(h); }
@@ -32,7 +25,7 @@ constexpr uint32_t IX_DEAD = 0xFFFFFFFFu;   // a key whose last record is a DEL:
 // deleted key -> IX_DEAD (keeps the probe sequences of the keys behind it intact).  No atomics:
 // the fold already placed every key.
 __global__ void k_index_from_fold(const FoldEnt *__restrict__ ent, const uint32_t *__restrict__ fsz,
-                                  const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
+                                  const uint8_t *__restrict__ flag8, const uint32_t *__restrict__ pos,
                                   uint32_t *__restrict__ slots) {
     const uint64_t n_slots = (uint64_t)fsz[0] + 1;   // the fold table's size on the device; grid-stride
     for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n_slots; h += (uint64_t)gridDim.x * blockDim.x) {
@@ -40,7 +33,7 @@ __global__ void k_index_from_fold(const FoldEnt *__restrict__ ent, const uint32_
         uint32_t v = 0;
         if (!(a.x == 0xFFFFFFFFu && a.y == 0xFFFFFFFFu)) {
             const uint32_t j = ~a.z;
-            v = flag[j] ? pos[j] + 1u : IX_DEAD;
+            v = flag8[j] ? pos[j] + 1u : IX_DEAD;
         }
         slots[h] = v;
     }
@@ -68,20 +61,24 @@ uint64_t index_slots(uint64_t n_live) {
     return s;
 }
 
-// after compact_front: live flags, their scan and the dense live list in c->lout (room for every
-// tuple), and with index the key table in c->islots (room for the largest table); no host sync —
-// n_live = cpos[nt - 1] + cflag[nt - 1], read by fold_settle (keep_del: every key's last record
-// instead, tombstones included)
+// after compact_front: live flags (a byte per tuple), the dense live list in c->lout (room for every
+// tuple) from per-block counts and one workgroup's scan of them (k_dl_*, as kvr_compact's), and
+// with index the key table in c->islots (room for the largest table); no host sync — n_live =
+// dl_tot[1], read by fold_settle (keep_del: every key's last record instead, tombstones included)
 int fold_derive(kvr_ctx *c, size_t nt, bool keep_del, bool index) {
     hipStream_t st = c->stream;
-    const uint32_t g = (uint32_t)((nt + 255) / 256);
-    if (c->lout.ensure(nt) || (index && c->islots.ensure(c->fent.n))) return KVR_ENOMEM;
-    HIPCHK(live_flags(c, nt, false, keep_del));
-    size_t tb = c->ctmp.n;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->ctmp.p, tb, c->cflag.p, c->cpos.p, (int)nt, st));
-    hipLaunchKernelGGL(k_live_tuples, dim3(g), dim3(256), 0, st, c->ctup.p, (uint64_t)nt, c->cflag.p, c->cpos.p, c->lout.p);
+    const uint32_t nb = (uint32_t)((nt + DL_CH - 1) / DL_CH);
+    if (c->lout.ensure(nt) || (index && c->islots.ensure(c->fent.n)) || c->dl_cnt.ensure(nb) || c->dl_bytes.ensure(nb) ||
+        c->dl_tot.ensure(2))
+        return KVR_ENOMEM;
+    HIPCHK(live_flags(c, nt, false, keep_del, true));
+    hipLaunchKernelGGL(k_dl_count, dim3(nb), dim3(DL_T), 0, st, c->cfl8.p, (const kvr_tuple *)nullptr, c->dl_cnt.p,
+                       c->dl_bytes.p);
+    hipLaunchKernelGGL(k_dl_scan, dim3(1), dim3(DL_ST), 0, st, c->dl_cnt.p, c->dl_bytes.p, nb, (uint64_t *)nullptr,
+                       c->dl_tot.p);
+    hipLaunchKernelGGL(k_dl_fill_tup, dim3(nb), dim3(DL_T), 0, st, c->cfl8.p, c->ctup.p, c->dl_cnt.p, c->lout.p, c->cpos.p);
     if (index)
-        hipLaunchKernelGGL(k_index_from_fold, dim3(fold_grid(c)), dim3(256), 0, st, c->fent.p, c->fsz.p, c->cflag.p,
+        hipLaunchKernelGGL(k_index_from_fold, dim3(fold_grid(c)), dim3(256), 0, st, c->fent.p, c->fsz.p, c->cfl8.p,
                            c->cpos.p, c->islots.p);
     HIPCHK(hipGetLastError());
     return KVR_OK;
@@ -89,14 +86,14 @@ int fold_derive(kvr_ctx *c, size_t nt, bool keep_del, bool index) {
 
 // fold_settle + fold_derive again if the deferred fold had to be redone; *total = n_live
 int derive_settle(kvr_ctx *c, size_t nt, bool keep_del, bool index, uint64_t *total) {
-    uint32_t last2[2] = {0, 0};
+    uint64_t n_live = 0;
     bool redone = false;
-    int rc = fold_settle(c, nt, &redone, last2);
+    int rc = fold_settle(c, nt, &redone, &n_live);
     if (rc == KVR_OK && redone) {
         rc = fold_derive(c, nt, keep_del, index);
-        if (rc == KVR_OK) rc = fold_settle(c, nt, &redone, last2);   // (not pending: reads the totals)
+        if (rc == KVR_OK) rc = fold_settle(c, nt, &redone, &n_live);   // (not pending: reads the totals)
     }
-    *total = (uint64_t)last2[0] + last2[1];
+    *total = n_live;
     return rc;
 }
 

@@ -284,7 +284,7 @@ constexpr int CB = CT;            // tiles per chunk of k_compact_s
 // Thread k2 moves half k2 & 1 of tuple k2 >> 1 as one 16-B load and store, so a wave's loads and
 // stores are 1 KiB contiguous; the second half holds val_len, crc32, key_tag, op and flags, so
 // its thread also does the expected-CRC check, and moves the key prefix when the call keeps one
-// (kpool -> kout, the fold's keys).
+// (kpool -> kout, the fold's keys) and writes (key tag, key length) beside it (ktk).
 __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ segs, const StripeDesc *__restrict__ stripes,
                                                   const StripeRes *__restrict__ sres,
                                                   const uint64_t *__restrict__ soff, const TileRes *__restrict__ tres,
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
                                                   const uint32_t *__restrict__ expected, uint64_t n_expected,
                                                   Counters *ctr, const LinkResult *__restrict__ link,
                                                   const uint4 *__restrict__ kpool, uint4 *__restrict__ kout,
-                                                  Counters *hctr) {
+                                                  uint32_t *__restrict__ ktk, Counters *hctr) {
     if (link->status != 0 || ctr->overflow) return;
     __shared__ uint64_t off[CB + 1];
     __shared__ uint64_t part[CT];
@@ -310,6 +310,9 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
         if (o < out_cap) {
             reinterpret_cast<uint4 *>(out + o)[half] = v;
             if (half && kout) kout[o] = kpool[src];
+            // (key tag, key length) for the fold's estimate and partition: each half has one of them,
+            // so a wave's stores are 256 B contiguous
+            if (ktk) ktk[2 * o + (half ^ 1u)] = half ? v.z : v.w;
         }
     };
     // the CRC failures go to the host's pinned mirror (a system-scope atomic, only for a wave

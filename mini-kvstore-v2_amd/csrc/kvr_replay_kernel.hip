@@ -104,6 +104,9 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #ifndef KVR_CANDFRAME   // 1: candidate-chain rounds for what the stride round leaves (records of varying lengths)
 #define KVR_CANDFRAME 1
 #endif
+#ifndef KVR_SPEC   // 1: a tile after a clean stride round of equal SETs runs its unit loop on the predicted
+#define KVR_SPEC 1    // framing and verifies it after (the next tile's load then runs under the decode)
+#endif
 #ifndef KVR_SUCC   // 1: the candidate chain follows precomputed successor slots (0: a ballot per record)
 #define KVR_SUCC 1
 #endif
@@ -847,6 +850,8 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
     uint32_t err_kind = 0, total = 0;
     uint32_t stride = 0, fast_skip = 0;           // lane-parallel framing: the last record length, tiles
                                                   // left to the scalar hop loop
+    bool spec_next = false, no_spec = false;      // the last stride round was one clean round of equal
+    uint32_t spec_ku = 0, spec_vu = 0;            // SETs (key and value lengths): KVR_SPEC's prediction
     uint32_t run_first = N32;                     // the stripe's first pool slot, while its tuples are one run
     bool run_contig = true;                       // (no second chunk claimed after its first tuple)
     uint32_t carry = 0, c_state = 0;              // 1: a long value crosses the tile start (c_state: its register);
@@ -1059,7 +1064,200 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             }
             any_long = true;
         };
-        if (walk) {
+#if KVR_LANEFRAME
+        // ---- lane-parallel framing ---------------------------------------------------------------
+        // decode(c): the record that would start at tile offset c (per lane; act: the lane takes
+        // part), from a window of the segment bytes: opcode, key length, value length, every
+        // engine.rs framing check, and where its successor starts.  The value-length field is read
+        // out of the window for the key length of lane kl (one length for every key is the usual
+        // case); a lane with another key length reads it from memory (vmem) or leaves its
+        // successor unknown (nx = UNK, resolved when the chain reaches it).
+        struct Dec {
+            uint32_t win[WINW];
+            uint32_t s, op, klen, vlen, vb, nx;
+            bool ok;
+        };
+        constexpr uint32_t UNK = 0xFFFFFFFEu;
+        const int32_t vhiT = (int32_t)vhi_r, remT = (int32_t)rem;   // (used only when !huge)
+        // (pre: the window already loaded, the speculative tile's; null: loaded here)
+        auto decode = [&](int32_t c, bool act, int kl, bool vmem, const uint32_t *pre) -> Dec {
+            Dec d;
+            const int32_t a = c & ~3;
+            d.s = (uint32_t)c & 3u;
+            // (a lane that takes no part reads past the resource, which yields 0 with no memory
+            // access: the loads need no exec mask, so no branch around each of them)
+            const int32_t ao = act ? a : (int32_t)0x7FFFFF00;
+            if (pre) {
+#pragma unroll
+                for (int i = 0; i < WINW; ++i) d.win[i] = pre[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < WINW; ++i) d.win[i] = ts.w32a(ao + 4 * i);
+            }
+            const uint32_t x0 = __builtin_amdgcn_alignbyte(d.win[1], d.win[0], d.s);
+            const uint32_t x1 = __builtin_amdgcn_alignbyte(d.win[2], d.win[1], d.s);
+            d.op = x0 & 255u;
+            d.klen = (x0 >> 8) | (x1 << 24);
+            // engine.rs framing checks, tile-relative in 32 bits (rem < 2^31)
+            const uint32_t room = (uint32_t)(remT - c);
+            bool ok = act && d.op <= 1u && c < vhiT && room >= 5u && d.klen <= room - 5u;
+            const uint32_t e = (uint32_t)c + 5u + (ok ? d.klen : 0u);   // < 2^31
+            const bool need_v = ok && d.op == 0u;
+            ok = ok && (!need_v || (uint32_t)remT - e >= 4u);
+            const uint32_t ku = rl32(d.klen, kl);
+            d.vlen = 0;
+            bool vdone = false;
+            {
+                const uint32_t dd = 5u + ku, B0 = dd >> 2;
+                if (B0 >= 1u && B0 <= (uint32_t)(WINW - 3)) {
+                    uint32_t wa = 0, wb = 0, wc = 0;
+#pragma unroll
+                    for (int bb = 1; bb <= WINW - 3; ++bb)
+                        if (B0 == (uint32_t)bb) { wa = d.win[bb]; wb = d.win[bb + 1]; wc = d.win[bb + 2]; }
+                    const uint32_t oo = d.s + (dd & 3u);
+                    const bool cy = oo >= 4u;
+                    d.vlen = __builtin_amdgcn_alignbyte(cy ? wc : wb, cy ? wb : wa, oo & 3u);
+                    vdone = d.klen == ku;
+                }
+            }
+            bool unk = false;
+            if (need_v && ok && !vdone) {
+                if (vmem) d.vlen = ts.u32((int64_t)e);
+                else unk = true;
+            }
+            d.vb = e + 4u;
+            ok = ok && (!need_v || unk || d.vlen <= (uint32_t)remT - d.vb);
+            d.ok = ok;
+            d.nx = unk ? UNK : (d.op == 1u ? e : d.vb + d.vlen);
+            return d;
+        };
+        // emit: the records of a framing round.  Lane j with `on` emits record nrec + rk (rk: its
+        // rank on the chain, rank order = position order); lead / lastl: the lanes of the round's
+        // first and last records.  strided: record j starts at cur0 + j L (the stride round), so the
+        // long values of a round of equal SETs fold into the units by arithmetic.
+        // (it calls no other lambda: the caller claims the pool slots and runs the long-value
+        // fold it asks for, so no closure object has to live in memory)
+        struct Fold { uint32_t lmark; int kind; };   // kind 0: none, 1: fold_uniform, 2: fold_views
+        auto emit = [&](const Dec &d, int32_t c, bool on, uint32_t rk, uint32_t n_on, int lead, int lastl,
+                        bool strided, uint32_t slot0) -> Fold {
+            if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
+            const uint32_t klen = d.klen, op = d.op, vlen = d.vlen, vb = d.vb, s = d.s;
+            Fold fo{0u, 0};
+            // one key length for the batch (the first record's, ku): no per-lane byte masks
+            const uint32_t ku = rl32(klen, lead);
+            const bool kuni = __ballot(on && klen != ku) == 0ull && ku <= 4u * KEYW;
+            const uint32_t kmx = kuni ? ku : wave_max(on ? klen : 0u);
+            uint32_t rerr = N32, rkind = 0;
+            uint64_t raux = 0;
+            if (on && !(KVR_ABLATE & 1)) {
+                const uint32_t kc = kmx > 4u * KEYW ? 4u * KEYW : kmx;
+                const uint32_t nw = (kc + 3u) >> 2;   // key words of the longest key
+                uint32_t kr[KEYW + 1];
+#pragma unroll
+                for (int i = 0; i <= KEYW; ++i) kr[i] = s == 3u ? d.win[i + 2] : d.win[i + 1];
+                const int kb = c + 5;
+                uint32_t cc = ~0u, bad = 0x80u;
+                if (kuni) cc = crc_words_u<KEYW>(kr, K, (s + 1u) & 3u, ku, &bad);
+                else if (klen <= 4u * KEYW) cc = crc_words<KEYW>(kr, K, (s + 1u) & 3u, klen, nw, &bad);
+                if (bad != 0u) {              // non-ASCII or long key: the full UTF-8 check
+                    uint64_t vu = 0;
+                    uint32_t el = 0;
+                    if (!utf8_check(ts, kb, klen, &vu, &el)) {   // engine.rs:114
+                        rerr = nrec + rk; rkind = KVR_E_UTF8; raux = vu | ((uint64_t)el << 32);
+                    } else {
+                        cc = crc_long(ts, ~0u, kb, klen, K);
+                    }
+                }
+                if (rerr == N32) {
+                    kvr_tuple t;
+                    t.rec_off = (uint64_t)(lo + c);
+                    t.seg_idx = sd.seg;
+                    t.key_len = klen;
+                    t.val_len = op == 0u ? vlen : 0u;
+                    t.crc32 = op == 0u ? short_value_crc(ts, K, (int)vb, vlen) : 0u;
+                    t.key_tag = ~cc;
+                    t.op = (uint8_t)op;
+                    t.flags = 0;
+                    t.reserved = 0;
+                    pool[slot0 + rk] = t;
+                    // the key prefix for the fold (only calls that fold ask for it)
+                    if (kpool) kpool[slot0 + rk] = key_prefix_words(kr, (s + 1u) & 3u, klen);
+                }
+            }
+            // long values crossing a unit boundary: marked at their first unit (a scatter through
+            // this wave's LDS row; the mark carries the rank, so the prefix max finds the latest,
+            // and the lane), then folded into every unit's view
+            const bool lv = on && op == 0u && vlen > (uint32_t)SMALL && ((vb ^ (vb + vlen - 1u)) >> SC_LOG) != 0u;
+            const uint64_t lvm = __ballot(lv);
+            // a round of SETs of one key and one value length (longer than a unit)
+            const uint32_t vu = rl32(vlen, lead);
+            const bool vuni = KVR_UNIFOLD && strided && vu > (uint32_t)SC &&
+                              __ballot(on && (op != 0u || vlen != vu || klen != ku)) == 0ull;
+            if (lvm && !(KVR_ABLATE & 32)) {
+                uint32_t lmark = 0;
+                if (!vuni) {
+                    MK[lane] = 0u;
+                    __builtin_amdgcn_wave_barrier();
+                    if (lv && vb < (uint32_t)TILE) MK[vb >> SC_LOG] = ((rk + 1u) << 6) | (uint32_t)lane;
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    lmark = MK[lane];
+                }
+                // a long value starting past the tile end (only the last record's): carried
+                if ((lvm >> lastl) & 1ull) {
+                    const uint32_t vbl = rl32(vb, lastl);
+                    if (vbl >= (uint32_t)TILE) {
+                        n_carry = 2; n_vb = (uint64_t)(lo + (int64_t)vbl);
+                        n_ve = (uint64_t)(lo + (int64_t)vbl + rl32(vlen, lastl));
+                        n_ref = nrec + n_on - 1u;
+                        n_abs = false;
+                    }
+                }
+                fo.lmark = lmark;
+                fo.kind = vuni ? 1 : 2;
+            } else if (lvm) {
+                any_long = true;
+            }
+            // the first error of the batch (lowest record index)
+            if (__ballot(rerr != N32)) {
+                const uint32_t mn = ~wave_max(~rerr);
+                const int el = (int)__builtin_ctzll(__ballot(rerr == mn));
+                err_rec = mn;
+                err_kind = rl32(rkind, el);
+                err_aux = rl64(raux, el);
+                err_pos = (uint64_t)(lo + (int64_t)(int32_t)rl32((uint32_t)c, el));
+            }
+            if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
+            return fo;
+        };
+#endif
+        // ---- speculative tile (KVR_SPEC) -------------------------------------------------------
+        // After a clean stride round of equal SETs the records of this tile are predicted exactly:
+        // they start at cur + j L with the same key and value lengths.  The long values' views are
+        // then folded from the prediction alone (fold_uniform), the unit loop runs on them, the next
+        // tile's load goes out, and only then are the records decoded, checked against the
+        // prediction and emitted: the decode's window loads, issued before that load, do not wait
+        // for it, and its latency runs under the decode, the records, the scan and the finalize.
+        // A record that differs sends the tile back to the top (its registers reloaded) to be
+        // framed as usual; nothing was written for it yet.
+        bool spec = false;
+        int32_t s_cur = 0;
+        uint32_t s_n = 0;
+#if KVR_LANEFRAME
+        if (KVR_SPEC && !KVR_ABLATE && spec_next && !no_spec && walk && rem <= 0x7FFFFFFFll && fast_skip == 0u) {
+            const int64_t pp = (int64_t)entry - lo;
+            const uint32_t L = stride;
+            if (pp >= 0 && L > (uint32_t)SC && L < (uint32_t)TILE && pp + 64ll * (int64_t)L >= vhi_r) {
+                s_cur = (int32_t)pp;
+                s_n = (uint32_t)((vhi_r - pp + (int64_t)L - 1) / (int64_t)L);   // records starting in the tile
+                spec = true;
+                fold_uniform(s_cur + 9 + (int32_t)spec_ku, (int32_t)L, s_n, (int32_t)spec_vu, nrec);
+            }
+        }
+#endif
+        no_spec = false;
+        if (walk && !spec) {
+            spec_next = false;
             // positions are tile-relative, in 32 bits unless the segment runs more than 2 GiB past
             // the tile (then the 64-bit copy of the exact hop loop takes the whole tile)
             const bool huge = rem > 0x7FFFFFFFll;
@@ -1068,165 +1266,6 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             if (KVR_ABLATE & 4) p = vhi_r;
             if (KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
 #if KVR_LANEFRAME
-            // ---- lane-parallel framing ---------------------------------------------------------------
-            // decode(c): the record that would start at tile offset c (per lane; act: the lane takes
-            // part), from a window of the segment bytes: opcode, key length, value length, every
-            // engine.rs framing check, and where its successor starts.  The value-length field is read
-            // out of the window for the key length of lane kl (one length for every key is the usual
-            // case); a lane with another key length reads it from memory (vmem) or leaves its
-            // successor unknown (nx = UNK, resolved when the chain reaches it).
-            struct Dec {
-                uint32_t win[WINW];
-                uint32_t s, op, klen, vlen, vb, nx;
-                bool ok;
-            };
-            constexpr uint32_t UNK = 0xFFFFFFFEu;
-            const int32_t vhiT = (int32_t)vhi_r, remT = (int32_t)rem;   // (used only when !huge)
-            auto decode = [&](int32_t c, bool act, int kl, bool vmem) -> Dec {
-                Dec d;
-                const int32_t a = c & ~3;
-                d.s = (uint32_t)c & 3u;
-                // (a lane that takes no part reads past the resource, which yields 0 with no memory
-                // access: the loads need no exec mask, so no branch around each of them)
-                const int32_t ao = act ? a : (int32_t)0x7FFFFF00;
-#pragma unroll
-                for (int i = 0; i < WINW; ++i) d.win[i] = ts.w32a(ao + 4 * i);
-                const uint32_t x0 = __builtin_amdgcn_alignbyte(d.win[1], d.win[0], d.s);
-                const uint32_t x1 = __builtin_amdgcn_alignbyte(d.win[2], d.win[1], d.s);
-                d.op = x0 & 255u;
-                d.klen = (x0 >> 8) | (x1 << 24);
-                // engine.rs framing checks, tile-relative in 32 bits (rem < 2^31)
-                const uint32_t room = (uint32_t)(remT - c);
-                bool ok = act && d.op <= 1u && c < vhiT && room >= 5u && d.klen <= room - 5u;
-                const uint32_t e = (uint32_t)c + 5u + (ok ? d.klen : 0u);   // < 2^31
-                const bool need_v = ok && d.op == 0u;
-                ok = ok && (!need_v || (uint32_t)remT - e >= 4u);
-                const uint32_t ku = rl32(d.klen, kl);
-                d.vlen = 0;
-                bool vdone = false;
-                {
-                    const uint32_t dd = 5u + ku, B0 = dd >> 2;
-                    if (B0 >= 1u && B0 <= (uint32_t)(WINW - 3)) {
-                        uint32_t wa = 0, wb = 0, wc = 0;
-#pragma unroll
-                        for (int bb = 1; bb <= WINW - 3; ++bb)
-                            if (B0 == (uint32_t)bb) { wa = d.win[bb]; wb = d.win[bb + 1]; wc = d.win[bb + 2]; }
-                        const uint32_t oo = d.s + (dd & 3u);
-                        const bool cy = oo >= 4u;
-                        d.vlen = __builtin_amdgcn_alignbyte(cy ? wc : wb, cy ? wb : wa, oo & 3u);
-                        vdone = d.klen == ku;
-                    }
-                }
-                bool unk = false;
-                if (need_v && ok && !vdone) {
-                    if (vmem) d.vlen = ts.u32((int64_t)e);
-                    else unk = true;
-                }
-                d.vb = e + 4u;
-                ok = ok && (!need_v || unk || d.vlen <= (uint32_t)remT - d.vb);
-                d.ok = ok;
-                d.nx = unk ? UNK : (d.op == 1u ? e : d.vb + d.vlen);
-                return d;
-            };
-            // emit: the records of a framing round.  Lane j with `on` emits record nrec + rk (rk: its
-            // rank on the chain, rank order = position order); lead / lastl: the lanes of the round's
-            // first and last records.  strided: record j starts at cur0 + j L (the stride round), so the
-            // long values of a round of equal SETs fold into the units by arithmetic.
-            // (it calls no other lambda: the caller claims the pool slots and runs the long-value
-            // fold it asks for, so no closure object has to live in memory)
-            struct Fold { uint32_t lmark; int kind; };   // kind 0: none, 1: fold_uniform, 2: fold_views
-            auto emit = [&](const Dec &d, int32_t c, bool on, uint32_t rk, uint32_t n_on, int lead, int lastl,
-                            bool strided, uint32_t slot0) -> Fold {
-                if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
-                const uint32_t klen = d.klen, op = d.op, vlen = d.vlen, vb = d.vb, s = d.s;
-                Fold fo{0u, 0};
-                // one key length for the batch (the first record's, ku): no per-lane byte masks
-                const uint32_t ku = rl32(klen, lead);
-                const bool kuni = __ballot(on && klen != ku) == 0ull && ku <= 4u * KEYW;
-                const uint32_t kmx = kuni ? ku : wave_max(on ? klen : 0u);
-                uint32_t rerr = N32, rkind = 0;
-                uint64_t raux = 0;
-                if (on && !(KVR_ABLATE & 1)) {
-                    const uint32_t kc = kmx > 4u * KEYW ? 4u * KEYW : kmx;
-                    const uint32_t nw = (kc + 3u) >> 2;   // key words of the longest key
-                    uint32_t kr[KEYW + 1];
-#pragma unroll
-                    for (int i = 0; i <= KEYW; ++i) kr[i] = s == 3u ? d.win[i + 2] : d.win[i + 1];
-                    const int kb = c + 5;
-                    uint32_t cc = ~0u, bad = 0x80u;
-                    if (kuni) cc = crc_words_u<KEYW>(kr, K, (s + 1u) & 3u, ku, &bad);
-                    else if (klen <= 4u * KEYW) cc = crc_words<KEYW>(kr, K, (s + 1u) & 3u, klen, nw, &bad);
-                    if (bad != 0u) {              // non-ASCII or long key: the full UTF-8 check
-                        uint64_t vu = 0;
-                        uint32_t el = 0;
-                        if (!utf8_check(ts, kb, klen, &vu, &el)) {   // engine.rs:114
-                            rerr = nrec + rk; rkind = KVR_E_UTF8; raux = vu | ((uint64_t)el << 32);
-                        } else {
-                            cc = crc_long(ts, ~0u, kb, klen, K);
-                        }
-                    }
-                    if (rerr == N32) {
-                        kvr_tuple t;
-                        t.rec_off = (uint64_t)(lo + c);
-                        t.seg_idx = sd.seg;
-                        t.key_len = klen;
-                        t.val_len = op == 0u ? vlen : 0u;
-                        t.crc32 = op == 0u ? short_value_crc(ts, K, (int)vb, vlen) : 0u;
-                        t.key_tag = ~cc;
-                        t.op = (uint8_t)op;
-                        t.flags = 0;
-                        t.reserved = 0;
-                        pool[slot0 + rk] = t;
-                        // the key prefix for the fold (only calls that fold ask for it)
-                        if (kpool) kpool[slot0 + rk] = key_prefix_words(kr, (s + 1u) & 3u, klen);
-                    }
-                }
-                // long values crossing a unit boundary: marked at their first unit (a scatter through
-                // this wave's LDS row; the mark carries the rank, so the prefix max finds the latest,
-                // and the lane), then folded into every unit's view
-                const bool lv = on && op == 0u && vlen > (uint32_t)SMALL && ((vb ^ (vb + vlen - 1u)) >> SC_LOG) != 0u;
-                const uint64_t lvm = __ballot(lv);
-                // a round of SETs of one key and one value length (longer than a unit)
-                const uint32_t vu = rl32(vlen, lead);
-                const bool vuni = KVR_UNIFOLD && strided && vu > (uint32_t)SC &&
-                                  __ballot(on && (op != 0u || vlen != vu || klen != ku)) == 0ull;
-                if (lvm && !(KVR_ABLATE & 32)) {
-                    uint32_t lmark = 0;
-                    if (!vuni) {
-                        MK[lane] = 0u;
-                        __builtin_amdgcn_wave_barrier();
-                        if (lv && vb < (uint32_t)TILE) MK[vb >> SC_LOG] = ((rk + 1u) << 6) | (uint32_t)lane;
-                        __builtin_amdgcn_wave_barrier();
-                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                        lmark = MK[lane];
-                    }
-                    // a long value starting past the tile end (only the last record's): carried
-                    if ((lvm >> lastl) & 1ull) {
-                        const uint32_t vbl = rl32(vb, lastl);
-                        if (vbl >= (uint32_t)TILE) {
-                            n_carry = 2; n_vb = (uint64_t)(lo + (int64_t)vbl);
-                            n_ve = (uint64_t)(lo + (int64_t)vbl + rl32(vlen, lastl));
-                            n_ref = nrec + n_on - 1u;
-                            n_abs = false;
-                        }
-                    }
-                    fo.lmark = lmark;
-                    fo.kind = vuni ? 1 : 2;
-                } else if (lvm) {
-                    any_long = true;
-                }
-                // the first error of the batch (lowest record index)
-                if (__ballot(rerr != N32)) {
-                    const uint32_t mn = ~wave_max(~rerr);
-                    const int el = (int)__builtin_ctzll(__ballot(rerr == mn));
-                    err_rec = mn;
-                    err_kind = rl32(rkind, el);
-                    err_aux = rl64(raux, el);
-                    err_pos = (uint64_t)(lo + (int64_t)(int32_t)rl32((uint32_t)c, el));
-                }
-                if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
-                return fo;
-            };
             bool round_broke = false;        // a lane-parallel round ended on a broken record
             if (!huge && p < vhi_r && fast_skip == 0u) {
                 // ---- stride prediction, verified ---------------------------------------------------
@@ -1244,7 +1283,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const bool one = L == 0u || L >= (uint32_t)TILE;   // no usable stride: lane 0 only
                     const int32_t c = cur + (one ? 0 : lane * (int32_t)L);
                     const bool act = lane == 0 || (!one && c < vhiT);
-                    const Dec d = decode(c, act, 0, true);
+                    const Dec d = decode(c, act, 0, true, nullptr);
                     KVR_STAMP(1);
                     // the first lane whose record is broken or whose successor is not the next
                     // prediction (the last active lane's successor is unconstrained)
@@ -1255,9 +1294,11 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const bool okf = rl32(d.ok ? 1u : 0u, f) != 0u;
                     const uint32_t n_on = okf ? (uint32_t)f + 1u : (uint32_t)f;   // records on the chain
                     const uint32_t cf = rl32((uint32_t)c, f);
+                    bool uni = false;
                     if (n_on) {
                         const uint32_t slot0 = claim(n_on);
                         const Fold fo = emit(d, c, (uint32_t)lane < n_on, (uint32_t)lane, n_on, 0, (int)n_on - 1, !one, slot0);
+                        uni = fo.kind == 1;
                         if (fo.kind == 1) {
                             fold_uniform(cur + 9 + (int32_t)rl32(d.klen, 0), (int32_t)L, n_on, (int32_t)rl32(d.vlen, 0), nrec);
                         } else if (fo.kind == 2) {
@@ -1268,6 +1309,10 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     KVR_STAMP(6);
                     if (!okf) { cur = (int32_t)cf; round_broke = true; break; }   // the exact loop reports it
                     const uint32_t nf = rl32(d.nx, f);
+                    // one clean round of equal SETs over the whole tile: the next tile can be speculated
+                    spec_next = uni && !one && mm == 0ull && err_rec == N32 && nf - cf == L && (int32_t)nf >= vhiT;
+                    spec_ku = rl32(d.klen, 0);
+                    spec_vu = rl32(d.vlen, 0);
                     L = nf - cf;                               // record f's length predicts the next tile
                     cur = (int32_t)nf;
                     if (err_rec != N32) break;
@@ -1335,7 +1380,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const int32_t c = lane < (int)tot ? (int32_t)MK[lane] : -1;
                     const bool act = c >= p0 && c < vhiT;
                     const uint64_t at0 = __ballot(act && c == p0);
-                    Dec d = decode(act ? c : p0, act, at0 ? (int)__builtin_ctzll(at0) : 0, false);
+                    Dec d = decode(act ? c : p0, act, at0 ? (int)__builtin_ctzll(at0) : 0, false, nullptr);
                     const uint32_t nxp = act && d.ok ? d.nx : N32;
                     const int32_t wend = cover < vhiT ? cover : vhiT;
                     // each candidate's successor slot (KVR_SUCC): the row slots of the successor's unit
@@ -1538,24 +1583,33 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             if (KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(0);
             tile_exit = broke ? ERRP : (uint64_t)(lo + p);
         }
-        if (c1 == N32) c1 = nrec;
         // the tile's result record, stored ahead of the next tile's load, so that the wait for that
-        // load at the loop top does not also wait for this store's ack
-        if (in_stripe && lane == 0) {
-            TileRes tr;
-            tr.pool_off = nrec ? (uint64_t)b1 : 0ull;
-            tr.pool_off2 = b2;
-            tr.count = nrec;
-            tr.count1 = c1 < nrec ? c1 : nrec;
-            tres[sg.tile0 + k] = tr;
-        }
+        // load at the loop top does not also wait for this store's ack (a speculative tile stores it
+        // once its records are emitted)
+        auto tile_result = [&]() {
+            if (c1 == N32) c1 = nrec;
+            if (in_stripe && lane == 0) {
+                TileRes tr;
+                tr.pool_off = nrec ? (uint64_t)b1 : 0ull;
+                tr.pool_off2 = b2;
+                tr.count = nrec;
+                tr.count1 = c1 < nrec ? c1 : nrec;
+                tres[sg.tile0 + k] = tr;
+            }
+        };
         // a record index of this tile -> its pool slot
         auto slot_of = [&](uint32_t ref, bool is_abs) -> uint32_t {
             return is_abs ? ref : (ref < c1 ? b1 + ref : b2 + (ref - c1));
         };
-        if (n_carry == 2u && !n_abs) n_ref = slot_of(n_ref, false);
-        // the stripe goes on past this tile (a value running past its end is carried on)
-        const bool need_next = err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry || out);
+        if (!spec) {
+            tile_result();
+            if (n_carry == 2u && !n_abs) n_ref = slot_of(n_ref, false);
+        }
+        // the stripe goes on past this tile (a value running past its end is carried on; a
+        // speculative tile's last value may start past it)
+        const bool need_next = err_pos == NONE && k + 1 < sg.n_tiles &&
+                               (k + 1 < sd.t_end || n_carry || out ||
+                                (spec && s_cur + (int32_t)((s_n - 1u) * stride + 9u + spec_ku) >= TILE));
         KVR_STAMP(2);
         // the word of a value end's partial tail, for the finalize (its latency runs under the unit loop)
         uint32_t wm = 0;
@@ -1617,8 +1671,9 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 sn = qm == UW ? cb : (snx ^ wm);
             }
             // the unit loop was the tile registers' last reader: the next tile's load is issued
-            // here and its latency runs under the scan and the finalize
-            if (need_next && !loaded) {
+            // here and its latency runs under the scan and the finalize (a speculative tile's, after
+            // the scan, behind its windows)
+            if (need_next && !loaded && !spec) {
                 load_unit(abase, d0, len, k + 1, lane, w);
                 loaded = true;
             }
@@ -1666,6 +1721,38 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             KVR_STAMP(10);
             uint32_t sin = dpp<0x138>(v);        // wave_shr:1: the state at this unit's start
             if (lane == 0) sin = c_state;
+#if KVR_LANEFRAME
+            if (spec) {   // the speculative tile's records: decoded, checked against the prediction, emitted
+                const int32_t sc = s_cur + lane * (int32_t)stride;
+                const bool act = (uint32_t)lane < s_n;
+                // its windows first, then the next tile's load: the decode waits for the windows alone
+                uint32_t sw[WINW];
+                const int32_t ao = act ? (sc & ~3) : (int32_t)0x7FFFFF00;
+#pragma unroll
+                for (int i = 0; i < WINW; ++i) sw[i] = ts.w32a(ao + 4 * i);
+                if (need_next && !loaded) {
+                    load_unit(abase, d0, len, k + 1, lane, w);
+                    loaded = true;
+                }
+                Dec d = decode(sc, act, 0, false, sw);
+                const bool bad = act && !(d.ok && d.op == 0u && d.klen == spec_ku && d.vlen == spec_vu);
+                if (__ballot(bad)) {   // not as predicted: frame the tile as usual
+                    no_spec = true;
+                    spec_next = false;
+                    loaded = false;
+                    if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(0);
+                    --k;
+                    continue;
+                }
+                const uint32_t slot0 = claim(s_n);
+                (void)emit(d, sc, act, (uint32_t)lane, s_n, 0, (int)s_n - 1, true, slot0);
+                nrec = err_rec != N32 ? err_rec : nrec + s_n;
+                tile_exit = (uint64_t)(lo + (int64_t)(int32_t)rl32(d.nx, (int)s_n - 1));
+                tile_result();
+                if (n_carry == 2u && !n_abs) n_ref = slot_of(n_ref, false);
+                if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(KVR_FIN_PRIO);   // (emit left the framing's)
+            }
+#endif
             // the value ending in this unit at m: its register is sin * x^(8m) ^ raw[0, m), and
             // raw[0, 4 qm) is A's snapshot, or all of A pushed through 4 (qm - H) bytes ^ B's: so
             // (base * x^(8*4q) ^ sn) with base = sin, q = qm, or base = sin * x^(8*4H) ^ A, q = qm - H

@@ -201,8 +201,8 @@ def test_gpu_compact_generated(gctx, name, target):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", list(SPECS))
 def test_gpu_compact_two_scans(gctx, monkeypatch, name):
-    """The rewrite's offsets and live positions from two scans (KVR_COMPACT_TWO_SCANS, the form
-    for stores past 2^24 tuples) equal the packed single scan's and the oracle's."""
+    """The rewrite's offsets and live positions from two scans over every tuple
+    (KVR_COMPACT_TWO_SCANS) equal the byte-flag dense list's (k_dl_*) and the oracle's."""
     segs = [K.gen_segment_cpu(SPECS[name], s)[0] for s in range(3)]
     monkeypatch.setenv("KVR_COMPACT_TWO_SCANS", "1")
     check_compact(gctx, segs, 777)
