@@ -9,6 +9,7 @@
  *   walks on through the wrongly speculated stripes after its own, so one round is the usual case).
  */
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <chrono>
@@ -55,11 +56,22 @@ struct DevBuf {
 
 constexpr uint32_t REDO_GRID = 1024;
 constexpr size_t LC_CTR = 64;                     // Counters' offset in the link + counters block
-constexpr size_t LC_BYTES = 128;
+constexpr size_t LC_BYTES = LC_BLOCK;
 static_assert(sizeof(LinkResult) <= LC_CTR && LC_CTR + sizeof(Counters) <= LC_BYTES, "link + counters block");
+// stripes up to which k_compact_s links the stripes itself (each workgroup sums the counts before
+// its stripe: O(stripes^2) reads in all); more, and k_link runs first
+constexpr uint32_t LINKED_MAX_STRIPES = 8192;
 
 // wait for the work queued on st: a host spin on an event for up to 20 ms (a blocking wait wakes
 // tens of microseconds after a short pipeline ends), then a blocking wait
+hipError_t wait_event(hipEvent_t ev) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) return hipEventSynchronize(ev);
+    }
+}
 hipError_t wait_stream(hipStream_t st, hipEvent_t ev) {
     hipError_t e = hipEventRecord(ev, st);
     if (e != hipSuccess) return e;
@@ -76,6 +88,10 @@ hipError_t wait_stream(hipStream_t st, hipEvent_t ev) {
 uint64_t pool_limit() {
     const char *e = getenv("KVR_POOL_LIMIT");
     return e ? std::max<uint64_t>(strtoull(e, nullptr, 10), 1024) : 0xFFFF0000ull;
+}
+bool getenv_flag(const char *name) {
+    const char *e = getenv(name);
+    return e && *e && *e != '0';
 }
 // tuples behind pool_cap that serve a claim past it (k_replay flags the overflow and writes there;
 // the host then grows the pool and runs again): one claim of the largest size
@@ -112,6 +128,7 @@ struct kvr_ctx {
     DevBuf<Counters> ctr;
     DevBuf<uint32_t> seg_bad, seg_err, expected;
     DevBuf<uint64_t> soff;                 // each stripe's output offset (k_link, for k_compact_s)
+    DevBuf<uint32_t> scnt;                 // each stripe's record count, dense (k_replay, for linked k_compact_s)
     DevBuf<uint32_t> crc, kmul, initx;
     DevBuf<GenRecDev> gen;
     // compaction (kvr_compact)
@@ -147,9 +164,11 @@ struct kvr_ctx {
     DevBuf<uint64_t> r_best, r_hk;
     LinkResult *h_link = nullptr;
     Counters *h_ctr = nullptr;
-    // link result and counters share one device allocation (one memset, one copy back per call)
-    // and one pinned host block
+    // link result and counters share one device block (one memset, one copy back per call) and one
+    // pinned host block.  There are two device blocks: a call uses block lc_cur, and the linked
+    // k_compact_s clears the other one for the next call
     DevBuf<uint8_t> lcbuf;
+    uint32_t lc_cur = 0;
     uint8_t *h_lc = nullptr;
     std::vector<SegDesc> h_segs;
     std::vector<StripeDesc> h_stripes;
@@ -296,6 +315,15 @@ int kvr_format_error(const kvr_error *e, const char *path, char *buf, size_t cap
     }
 }
 
+// point link / ctr at device block b of lcbuf
+static void lc_select(kvr_ctx *c, uint32_t b) {
+    c->lc_cur = b;
+    c->link.p = reinterpret_cast<LinkResult *>(c->lcbuf.p + b * LC_BYTES);
+    c->link.n = 1;
+    c->ctr.p = reinterpret_cast<Counters *>(c->lcbuf.p + b * LC_BYTES + LC_CTR);
+    c->ctr.n = 1;
+}
+
 int kvr_ctx_create(int device, kvr_ctx **out) {
     if (!out) return KVR_EINVAL;
     *out = nullptr;
@@ -322,14 +350,11 @@ int kvr_ctx_create(int device, kvr_ctx **out) {
     std::vector<uint32_t> crc, kmul, initx;
     build_tables(crc, kmul, initx);
     if (c->crc.ensure(crc.size()) || c->kmul.ensure(kmul.size()) || c->initx.ensure(initx.size()) ||
-        c->lcbuf.ensure(LC_BYTES)) {
+        c->lcbuf.ensure(2 * LC_BYTES)) {
         kvr_ctx_destroy(c);
         return KVR_ENOMEM;
     }
-    c->link.p = reinterpret_cast<LinkResult *>(c->lcbuf.p);
-    c->link.n = 1;
-    c->ctr.p = reinterpret_cast<Counters *>(c->lcbuf.p + LC_CTR);
-    c->ctr.n = 1;
+    lc_select(c, 0);
     if (hipMemcpy(c->crc.p, crc.data(), crc.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->kmul.p, kmul.data(), kmul.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->initx.p, initx.data(), initx.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
@@ -348,7 +373,7 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->pool.release(); c->dense.release(); c->redo.release();
     c->link.p = nullptr; c->ctr.p = nullptr;   // (inside lcbuf)
     c->lcbuf.release();
-    c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->soff.release();
+    c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->soff.release(); c->scnt.release();
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
     c->kpool.release(); c->ckeys.release(); c->ctk.release();
     c->ctup.release(); c->lout.release(); c->fent.release(); c->flist.release(); c->fcnt.release(); c->fsz.release();
@@ -601,7 +626,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
 
     if (c->segs.ensure(n) || c->stripes.ensure(n_stripes) || c->sres.ensure(n_stripes) ||
         c->tres.ensure(n_tiles) || c->redo.ensure(std::max<uint32_t>(n_stripes, REDO_GRID)) ||
-        c->seg_bad.ensure(n) || c->seg_err.ensure(n) || c->soff.ensure(n_stripes))
+        c->seg_bad.ensure(n) || c->seg_err.ensure(n) || c->soff.ensure(n_stripes) || c->scnt.ensure(n_stripes))
         return KVR_ENOMEM;
     // (the same segments as the last call: the descriptors on the device are still these)
     if (c->up_segs_p != c->segs.p || c->up_segs.size() != n ||
@@ -665,43 +690,83 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         }
         // the ordered gather pool -> output: one workgroup per stripe from the stripe offsets k_link
         // computes
-        auto launch_compact = [&]() {
-            hipLaunchKernelGGL(k_compact_s, dim3(n_stripes), dim3(CT), 0, st, c->segs.p, c->stripes.p, c->sres.p, c->soff.p,
+        // linked: k_compact_s links the stripes itself (no k_link launch); KVR_LINK_KERNEL=1 keeps
+        // k_link first (test and timing knob)
+        const bool linked = n_stripes <= LINKED_MAX_STRIPES && !getenv_flag("KVR_LINK_KERNEL");
+        uint8_t *const lc = reinterpret_cast<uint8_t *>(c->link.p);   // this call's device block
+        uint4 *const lc_next = reinterpret_cast<uint4 *>(c->lcbuf.p + (c->lc_cur ^ 1u) * LC_BYTES);
+        // the kernels' own start / end timestamps (the dispatch packets' completion signals, as
+        // rocprofv3 reads them) time k_replay and the pipeline: no marker packets between the
+        // kernels.  KVR_EVENT_MARKERS=1 records separate events instead (timing knob)
+        const bool markers = getenv_flag("KVR_EVENT_MARKERS");
+        auto launch_compact = [&](bool lk, hipEvent_t stop) {
+            hipExtLaunchKernelGGL(k_compact_s, dim3(n_stripes), dim3(CT), 0, st, nullptr, markers ? nullptr : stop, 0u,
+                               c->segs.p, c->stripes.p, c->sres.p, c->soff.p,
                                c->tres.p, c->pool.p, pool_cap, d_out, out_cap, d_exp,
                                (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p, kp, kp ? c->kout : nullptr,
-                               kp ? reinterpret_cast<uint32_t *>(ktk) : nullptr, c->h_ctr);
+                               kp ? reinterpret_cast<uint32_t *>(ktk) : nullptr, c->h_ctr,
+                               lk ? c->scnt.p : nullptr, n_stripes, (uint32_t)KR_TILE, lc_next);
+        };
+        auto launch_link = [&]() {
+            hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
+                               c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p, (uint32_t)KR_TILE,
+                               c->soff.p, c->ctr.p, c->h_link, c->h_ctr);
         };
         // counters and link result start at zero (the last successful call cleared them behind its
         // results, so this memset usually runs only on a context's first call or after an error)
-        if (!c->lc_zero || attempt) HIPCHK(hipMemsetAsync(c->lcbuf.p, 0, LC_BYTES, st));
+        if (!c->lc_zero || attempt) HIPCHK(hipMemsetAsync(lc, 0, LC_BYTES, st));
         c->lc_zero = false;
-        HIPCHK(hipEventRecord(c->ev[0], st));
-        hipLaunchKernelGGL(KR_KERNEL, dim3((n_stripes + KR_WPB - 1) / KR_WPB), dim3(KR_RT), 0, st, c->segs.p, c->stripes.p, n_stripes,
-                           c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, pool_chunk, kp);
+        if (linked) {   // the host mirror the linked k_compact_s writes into (no kernel of this context runs)
+            c->h_ctr->unlinked = 0;
+            c->h_ctr->crc_fail = 0;
+            c->h_ctr->overflow = 0;
+        }
+        if (markers) HIPCHK(hipEventRecord(c->ev[0], st));
+        hipExtLaunchKernelGGL(KR_KERNEL, dim3((n_stripes + KR_WPB - 1) / KR_WPB), dim3(KR_RT), 0, st,
+                              markers ? nullptr : c->ev[0], markers ? nullptr : c->ev[1], 0u, c->segs.p, c->stripes.p,
+                              n_stripes, c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, pool_chunk, kp, c->scnt.p);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(c->ev[1], st));
-        hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
-                           c->redo.p, (uint32_t)c->redo.n, c->link.p, c->seg_bad.p, c->seg_err.p, (uint32_t)KR_TILE,
-                           c->soff.p, c->ctr.p, c->h_link, c->h_ctr);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(c->ev[2], st));
+        if (markers) HIPCHK(hipEventRecord(c->ev[1], st));
+        if (!linked) {
+            launch_link();
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(c->ev[2], st));
+        }
         // compaction is launched right away: it does nothing unless linking succeeded (status 0),
         // which is the common case; otherwise the host re-walks and compacts again below
-        launch_compact();
+        launch_compact(linked, c->ev[3]);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(c->ev[3], st));
-        // link result + counters: k_link writes them into the pinned mirror h_lc (and clears the
-        // device block after a clean pass), k_compact_s adds its CRC failures there; when the call
-        // did not end cleanly the device block is copied as it is
-        HIPCHK(wait_stream(st, c->ev[5]));
+        if (markers) HIPCHK(hipEventRecord(c->ev[3], st));
+        // link result + counters: k_link (or the linked k_compact_s) writes them into the pinned
+        // mirror h_lc (and clears a device block after a clean pass), k_compact_s adds its CRC
+        // failures there; when the call did not end cleanly the device block is copied as it is
+        HIPCHK(wait_event(c->ev[3]));
+        bool lc_switch = false;   // a clean linked pass: the next call uses the other (cleared) block
+        if (linked) {
+            if (c->h_ctr->overflow) {
+                c->h_link->status = 0;   // (the pool is grown below)
+            } else if (c->h_ctr->unlinked) {
+                // a stripe did not link on its own (an error, a wrong speculation, a pass-through
+                // stripe it could not check): k_link and the plain gather, as without linking
+                launch_link();
+                launch_compact(false, nullptr);
+                HIPCHK(hipGetLastError());
+                HIPCHK(wait_stream(st, c->ev[5]));
+            } else {
+                c->h_link->status = 0;
+                c->h_link->n_redo = 0;
+                c->h_link->passes = 1;
+                lc_switch = true;
+            }
+        }
         const bool clean = c->h_link->status == 0 && !c->h_ctr->overflow;
         if (!clean) {
-            HIPCHK(hipMemcpyAsync(c->h_lc, c->lcbuf.p, LC_BYTES, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(c->h_lc, lc, LC_BYTES, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
         }
         c->stats.ms_replay = ev_ms(c->ev[0], c->ev[1]);
-        c->stats.ms_link = ev_ms(c->ev[1], c->ev[2]);
-        c->stats.ms_compact = ev_ms(c->ev[2], c->ev[3]);
+        c->stats.ms_link = linked ? 0.0f : ev_ms(c->ev[1], c->ev[2]);
+        c->stats.ms_compact = ev_ms(linked ? c->ev[1] : c->ev[2], c->ev[3]);
         c->stats.ms_total = ev_ms(c->ev[0], c->ev[3]);
 
         // rare: more re-walk rounds (a speculated entry was wrong twice in a row)
@@ -769,10 +834,11 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             fprintf(stderr, "kvr: stripe linking did not converge after %u rounds\n", guard);
             return KVR_EHIP;
         }
-        const bool cleared = clean;   // k_link cleared the block after a clean first pass
+        const bool cleared = clean;   // k_link cleared the block after a clean first pass (or, linked, the
+                                      // other block is clear: lc_switch)
         if (recompact && c->h_link->status == 0 && !c->h_ctr->overflow) {
             c->h_ctr->crc_fail = 0;
-            launch_compact();   // (its CRC failures go to h_ctr)
+            launch_compact(false, nullptr);   // (its CRC failures go to h_ctr)
             HIPCHK(hipGetLastError());
             HIPCHK(hipStreamSynchronize(st));
         }
@@ -799,8 +865,9 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         c->stats.n_crc_fail = c->h_ctr->crc_fail;
         *n_out = total;
         // the block is clear for the next call (else clear it now, behind this call's work)
+        if (lc_switch) lc_select(c, c->lc_cur ^ 1u);
         if (cleared) c->lc_zero = true;
-        else if (hipMemsetAsync(c->lcbuf.p, 0, LC_BYTES, st) == hipSuccess) c->lc_zero = true;
+        else if (hipMemsetAsync(c->link.p, 0, LC_BYTES, st) == hipSuccess) c->lc_zero = true;
         if (!(flags & KVR_OUT_ON_DEVICE) && cap) {
             const uint64_t m = std::min<uint64_t>(total, cap);
             if (m) {

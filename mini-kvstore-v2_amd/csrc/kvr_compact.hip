@@ -572,7 +572,6 @@ __global__ void __launch_bounds__(FP_T, 8) k_fold_lds(const kvr_tuple *__restric
 #pragma unroll
       for (uint32_t u = 0; u < FP_U; ++u) {
         if (q0 + u * FP_T >= n_lds) break;
-        const uint32_t k = cnt - 1 - (q0 + u * FP_T);   // latest first (regions in tuple order)
         const FPRec &r = rr[u];
         uint32_t h = ht_mix(r.tag) & G.mask & (G.s - 1);
         const unsigned long long mine = ((unsigned long long)r.tag << 32) | r.i;

@@ -89,8 +89,10 @@ struct Counters {         // device scratch, reset per call
     unsigned long long total_tuples;
     unsigned long long crc_fail;
     uint32_t overflow;
-    uint32_t pad;
+    uint32_t unlinked;    // host mirror: k_compact_s (linked mode) found a stripe it cannot link alone
 };
+
+constexpr uint32_t LC_BLOCK = 128;   // one link + counters block (LinkResult at 0, Counters at 64)
 
 struct Tables {           // read-only tables in global memory (copied to LDS per workgroup)
     const uint32_t *crc8;   // [16][256] slice-by-16 byte tables (k_replay replicates the first 2)

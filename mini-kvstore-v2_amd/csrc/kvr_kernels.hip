@@ -285,6 +285,29 @@ constexpr int CB = CT;            // tiles per chunk of k_compact_s
 // stores are 1 KiB contiguous; the second half holds val_len, crc32, key_tag, op and flags, so
 // its thread also does the expected-CRC check, and moves the key prefix when the call keeps one
 // (kpool -> kout, the fold's keys) and writes (key tag, key length) beside it (ktk).
+//
+// Linked mode (scnt != null, the replay pipeline's common case: no k_link before it).  Each
+// workgroup links its own stripe: its speculated entry must be the exit of the last earlier stripe
+// of the segment with a record start (a stripe without one must be crossed by that exit), and it
+// must hold no error.  Its output offset is the sum of the earlier stripes' counts (scnt, dense,
+// written by k_replay).  A stripe that fails either test sets hctr->unlinked and moves nothing;
+// the host then runs k_link and this kernel in its plain mode, which rewrite every output slot.
+// Workgroup 0 mirrors the pool counters to the host and clears the other link + counters block
+// (lc_next, the next call's), the last workgroup writes the total.
+__device__ __forceinline__ bool stripe_links(const SegDesc *__restrict__ segs, const StripeDesc *__restrict__ stripes,
+                                             const StripeRes *__restrict__ sres, uint32_t s, uint32_t tile) {
+    const StripeRes r = sres[s];
+    const StripeDesc d = stripes[s];
+    if (r.err_kind != 0u) return false;
+    if (d.pad) return true;                 // the segment's first stripe: its entry is offset 0
+    uint32_t j = s - 1;                     // (the segment's first stripe always has a record start)
+    while (sres[j].entry == NONE && !stripes[j].pad) --j;
+    const StripeRes p = sres[j];
+    if (p.entry == NONE || p.exit == ERRP || p.exit == NONE) return false;
+    if (r.entry == NONE) return p.exit >= stripe_hi(d, segs[d.seg], tile);   // a pass-through stripe
+    return r.entry == p.exit;
+}
+
 __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ segs, const StripeDesc *__restrict__ stripes,
                                                   const StripeRes *__restrict__ sres,
                                                   const uint64_t *__restrict__ soff, const TileRes *__restrict__ tres,
@@ -293,10 +316,38 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
                                                   const uint32_t *__restrict__ expected, uint64_t n_expected,
                                                   Counters *ctr, const LinkResult *__restrict__ link,
                                                   const uint4 *__restrict__ kpool, uint4 *__restrict__ kout,
-                                                  uint32_t *__restrict__ ktk, Counters *hctr) {
-    if (link->status != 0 || ctr->overflow) return;
+                                                  uint32_t *__restrict__ ktk, Counters *hctr,
+                                                  const uint32_t *__restrict__ scnt, uint32_t n_stripes, uint32_t tile,
+                                                  uint4 *__restrict__ lc_next) {
     __shared__ uint64_t off[CB + 1];
     __shared__ uint64_t part[CT];
+    __shared__ uint32_t s_ok;
+    uint64_t o_lk = 0;                      // linked mode: this stripe's output offset
+    if (scnt) {
+        const uint32_t ov = ctr->overflow;
+        if (blockIdx.x == 0) {
+            if (threadIdx.x == 0) { hctr->pool_cursor = ctr->pool_cursor; hctr->overflow = ov; }
+            if (threadIdx.x < LC_BLOCK / 16) lc_next[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
+        }
+        if (ov) return;
+        const uint32_t s = blockIdx.x;
+        if (threadIdx.x == 0) s_ok = stripe_links(segs, stripes, sres, s, tile) ? 1u : 0u;
+        unsigned long long a = 0;
+        for (uint32_t i = threadIdx.x; i < s; i += CT) a += scnt[i];
+        for (int d = 32; d >= 1; d >>= 1) a += __shfl_xor(a, d, 64);
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = a;
+        __syncthreads();
+        for (int i = 0; i < CT / 64; ++i) o_lk += part[i];
+        if (!s_ok) {
+            if (threadIdx.x == 0) atomicOr_system(&hctr->unlinked, 1u);
+            return;
+        }
+        if (s + 1 == n_stripes && threadIdx.x == 0) hctr->total_tuples = o_lk + scnt[s];
+        __syncthreads();   // (part is rewritten below)
+    } else if (link->status != 0 || ctr->overflow) {
+        return;
+    }
+    const uint64_t o_base = scnt ? o_lk : soff[blockIdx.x];
     uint32_t fails = 0;
     // the tuple of output slot o from pool slot src: half k2 & 1 per thread, the manifest check
     // on the second half (a SET: op in byte 0 of w), the key prefix beside it
@@ -326,7 +377,7 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
     };
     const uint64_t run = sres[blockIdx.x].pool_run;
     if (run != NONE) {   // the stripe's tuples are one run of the pool: a straight copy
-        const uint64_t n = sres[blockIdx.x].count, o0 = soff[blockIdx.x];
+        const uint64_t n = sres[blockIdx.x].count, o0 = o_base;
         for (uint64_t k2 = threadIdx.x; k2 < 2 * n; k2 += CT) move(run + (k2 >> 1), o0 + (k2 >> 1), (uint32_t)k2 & 1u);
         finish();
         return;
@@ -334,7 +385,7 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
     const StripeDesc sd = stripes[blockIdx.x];
     const uint32_t tile0 = segs[sd.seg].tile0;
     const uint32_t t_end = tile0 + sd.t_end;
-    uint64_t carry = soff[blockIdx.x];
+    uint64_t carry = o_base;
     for (uint32_t tb = tile0 + sd.t_begin; tb < t_end; tb += CB) {
         const uint32_t nt = min((uint32_t)CB, t_end - tb);
         const uint32_t t = tb + threadIdx.x;

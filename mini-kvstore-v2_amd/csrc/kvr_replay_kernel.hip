@@ -785,7 +785,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                                             kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
                                             Tables tb, const RedoEnt *__restrict__ redo,
                                             const LinkResult *__restrict__ link, uint32_t pool_chunk,
-                                            uint4 *__restrict__ kpool) {
+                                            uint4 *__restrict__ kpool, uint32_t *__restrict__ scnt) {
     constexpr bool redo_mode = REDO;
     __shared__ Smem S;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1817,6 +1817,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
         r.pool_run = run_contig && run_first != N32 ? (uint64_t)run_first : NONE;
         r.pad = 0;
         sres[si] = r;
+        if (scnt) scnt[si] = total;   // (dense, for k_compact_s's own stripe offsets)
     }
     // ---- redo pass: walk on into the next stripe of the segment --------------------------------
     // while its speculated result (last pass) disagrees with the chain position this walk reached,
@@ -1841,8 +1842,10 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                                                const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
                                                StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
                                                kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
-                                               Tables tb, uint32_t pool_chunk, uint4 *__restrict__ kpool) {
-    replay_body<false>(segs, stripes, n_stripes, sres, tres, pool, pool_cap, ctr, tb, nullptr, nullptr, pool_chunk, kpool);
+                                               Tables tb, uint32_t pool_chunk, uint4 *__restrict__ kpool,
+                                               uint32_t *__restrict__ scnt) {
+    replay_body<false>(segs, stripes, n_stripes, sres, tres, pool, pool_cap, ctr, tb, nullptr, nullptr, pool_chunk, kpool,
+                       scnt);
 }
 
 __global__ __launch_bounds__(RT) void k_rewalk(const SegDesc *__restrict__ segs,
@@ -1852,7 +1855,8 @@ __global__ __launch_bounds__(RT) void k_rewalk(const SegDesc *__restrict__ segs,
                                                Tables tb, const RedoEnt *__restrict__ redo,
                                                const LinkResult *__restrict__ link, uint32_t pool_chunk,
                                                uint4 *__restrict__ kpool) {
-    replay_body<true>(segs, stripes, n_stripes, sres, tres, pool, pool_cap, ctr, tb, redo, link, pool_chunk, kpool);
+    replay_body<true>(segs, stripes, n_stripes, sres, tres, pool, pool_cap, ctr, tb, redo, link, pool_chunk, kpool,
+                      nullptr);
 }
 
 }  // namespace kvr

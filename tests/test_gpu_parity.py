@@ -370,6 +370,33 @@ def test_repeated_calls_reuse_and_refresh_descriptors(gctx):
         check_parity(gctx, segs)
 
 
+@pytest.mark.parametrize("link_kernel", [False, True])
+@pytest.mark.parametrize("tps", [0, 2])
+@pytest.mark.parametrize("name", ["cfg2_1k", "cfg3_64k", "cfg4_del", "cfg5_zipf", "flips"])
+def test_linked_gather_and_link_kernel(gctx, monkeypatch, name, tps, link_kernel):
+    """The replay pipeline's two ways to order the pool: k_compact_s linking every stripe itself
+    (the default: no k_link launch; a stripe it cannot link alone sends the call to k_link), and
+    k_link first (KVR_LINK_KERNEL=1).  Same tuples, CRC flags and first error; a corrupted call
+    between clean ones (the double-buffered counter blocks) changes nothing after it."""
+    if link_kernel:
+        monkeypatch.setenv("KVR_LINK_KERNEL", "1")
+    spec = SPECS[name]
+    segs, exps = zip(*[K.gen_segment_cpu(spec, s) for s in range(3)])
+    segs = [s.tobytes() for s in segs]
+    exp = np.concatenate(exps)
+    bad = segs[:2] + [segs[2][: len(segs[2]) * 2 // 3 + 5]]
+    gctx.set_tiles_per_stripe(tps)
+    try:
+        for i, (ss, ee) in enumerate(((segs, exp), (segs, exp), (bad, None), (segs, exp))):
+            rg = check_parity(gctx, ss, expected=ee)
+            if ee is not None:
+                assert rg.stats.n_crc_fail == int(np.sum((rg.tuples["flags"] & K.TF_CRC_FAIL) != 0))
+            if link_kernel:
+                assert rg.stats.n_link_passes >= 1
+    finally:
+        gctx.set_tiles_per_stripe(0)
+
+
 def _varied_store(seed, n_bytes, del_frac, klen_rng, vlen_rng, zero_values=False, key_alphabet=None):
     """Records of varying lengths (the candidate rounds' case): keys of random length from
     key_alphabet (ASCII letters by default), values random or all zero."""
