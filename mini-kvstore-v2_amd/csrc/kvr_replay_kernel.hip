@@ -53,6 +53,7 @@ constexpr int SC_LOG = 7;
 static_assert(SC == 1 << SC_LOG, "unit size");
 static_assert(TILE == 64 * SC, "one unit per lane");
 static_assert(UW == 32, "unit = 32 dwords");
+static_assert(TILE == 1 << 13, "tile offsets >> 13 (the speculative batch)");
 constexpr uint32_t N32 = 0xFFFFFFFFu;
 constexpr uint32_t POOL_CHUNK = 2048;     // pool slots a wave claims at once
 constexpr uint32_t TILE_RECS = TILE / 5 + 1;   // most record starts a tile can hold
@@ -106,6 +107,9 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #endif
 #ifndef KVR_SPEC   // 1: a tile after a clean stride round of equal SETs runs its unit loop on the predicted
 #define KVR_SPEC 1    // framing and verifies it after (the next tile's load then runs under the decode)
+#endif
+#ifndef KVR_SPEC_BATCH   // 1: a speculative tile verifies and emits the predicted records of the next
+#define KVR_SPEC_BATCH 1   // tiles of its stripe too, up to 64 (one framing and records phase per ~8 tiles)
 #endif
 #ifndef KVR_SUCC   // 1: the candidate chain follows precomputed successor slots (0: a ballot per record)
 #define KVR_SUCC 1
@@ -848,6 +852,10 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
     }
     uint64_t err_pos = NONE, err_aux = 0;
     uint32_t err_kind = 0, total = 0;
+    // (fast_skip bits 16 on: the records of the next tiles a speculative tile's batch already verified and
+    // emitted, whole tiles; their slots are the last ones claimed, chunk_base - that count on.  Kept in
+    // fast_skip, which is 0 whenever a speculative tile runs: one more loop-carried value made the
+    // register allocator spill the tile registers to scratch)
     uint32_t stride = 0, fast_skip = 0;           // lane-parallel framing: the last record length, tiles
                                                   // left to the scalar hop loop
     bool spec_next = false, no_spec = false;      // the last stride round was one clean round of equal
@@ -1080,7 +1088,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
         constexpr uint32_t UNK = 0xFFFFFFFEu;
         const int32_t vhiT = (int32_t)vhi_r, remT = (int32_t)rem;   // (used only when !huge)
         // (pre: the window already loaded, the speculative tile's; null: loaded here)
-        auto decode = [&](int32_t c, bool act, int kl, bool vmem, const uint32_t *pre) -> Dec {
+        auto decode = [&](int32_t c, bool act, int kl, bool vmem, const uint32_t *pre, int32_t cend) -> Dec {
             Dec d;
             const int32_t a = c & ~3;
             d.s = (uint32_t)c & 3u;
@@ -1100,7 +1108,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             d.klen = (x0 >> 8) | (x1 << 24);
             // engine.rs framing checks, tile-relative in 32 bits (rem < 2^31)
             const uint32_t room = (uint32_t)(remT - c);
-            bool ok = act && d.op <= 1u && c < vhiT && room >= 5u && d.klen <= room - 5u;
+            bool ok = act && d.op <= 1u && c < cend && room >= 5u && d.klen <= room - 5u;
             const uint32_t e = (uint32_t)c + 5u + (ok ? d.klen : 0u);   // < 2^31
             const bool need_v = ok && d.op == 0u;
             ok = ok && (!need_v || (uint32_t)remT - e >= 4u);
@@ -1240,11 +1248,16 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
         // for it, and its latency runs under the decode, the records, the scan and the finalize.
         // A record that differs sends the tile back to the top (its registers reloaded) to be
         // framed as usual; nothing was written for it yet.
+        // A speculative tile decodes, checks and emits in one batch the predicted records of as many
+        // whole tiles ahead as 64 lanes hold (KVR_SPEC_BATCH): the tiles after it in the batch
+        // (`pre`: ahead > 0) only fold, CRC and finalize, with no framing or records phase.
         bool spec = false;
         int32_t s_cur = 0;
         uint32_t s_n = 0;
+        const uint32_t ahead = fast_skip >> 16;
+        const bool pre = ahead != 0u;
 #if KVR_LANEFRAME
-        if (KVR_SPEC && !KVR_ABLATE && spec_next && !no_spec && walk && rem <= 0x7FFFFFFFll && fast_skip == 0u) {
+        if (pre || (KVR_SPEC && !KVR_ABLATE && spec_next && !no_spec && walk && rem <= 0x7FFFFFFFll && fast_skip == 0u)) {
             const int64_t pp = (int64_t)entry - lo;
             const uint32_t L = stride;
             if (pp >= 0 && L > (uint32_t)SC && L < (uint32_t)TILE && pp + 64ll * (int64_t)L >= vhi_r) {
@@ -1255,6 +1268,15 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             }
         }
 #endif
+#ifdef KVR_PROF
+        prof_acc[14] += spec ? 1u : 0u;   // (counts, not cycles: speculative tiles, and those of them in a batch)
+        prof_acc[15] += pre ? 1u : 0u;
+#endif
+        if (pre && (!spec || s_n > ahead)) {   // bug trap: a batch always ends at a tile boundary
+            if (lane == 0) atomicOr(&ctr->overflow, 4u);
+            spec = false;
+            fast_skip &= 0xFFFFu;
+        }
         no_spec = false;
         if (walk && !spec) {
             spec_next = false;
@@ -1283,7 +1305,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const bool one = L == 0u || L >= (uint32_t)TILE;   // no usable stride: lane 0 only
                     const int32_t c = cur + (one ? 0 : lane * (int32_t)L);
                     const bool act = lane == 0 || (!one && c < vhiT);
-                    const Dec d = decode(c, act, 0, true, nullptr);
+                    const Dec d = decode(c, act, 0, true, nullptr, vhiT);
                     KVR_STAMP(1);
                     // the first lane whose record is broken or whose successor is not the next
                     // prediction (the last active lane's successor is unconstrained)
@@ -1380,7 +1402,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const int32_t c = lane < (int)tot ? (int32_t)MK[lane] : -1;
                     const bool act = c >= p0 && c < vhiT;
                     const uint64_t at0 = __ballot(act && c == p0);
-                    Dec d = decode(act ? c : p0, act, at0 ? (int)__builtin_ctzll(at0) : 0, false, nullptr);
+                    Dec d = decode(act ? c : p0, act, at0 ? (int)__builtin_ctzll(at0) : 0, false, nullptr, vhiT);
                     const uint32_t nxp = act && d.ok ? d.nx : N32;
                     const int32_t wend = cover < vhiT ? cover : vhiT;
                     // each candidate's successor slot (KVR_SUCC): the row slots of the successor's unit
@@ -1723,8 +1745,16 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             if (lane == 0) sin = c_state;
 #if KVR_LANEFRAME
             if (spec) {   // the speculative tile's records: decoded, checked against the prediction, emitted
-                const int32_t sc = s_cur + lane * (int32_t)stride;
-                const bool act = (uint32_t)lane < s_n;
+                // (KVR_SPEC_BATCH: the predicted records of the next tiles of the stripe too, up to 64;
+                // the whole tiles before the first record that is not as predicted are emitted now, and
+                // those tiles (pre) then run this code with no lane taking part -- the same code, so
+                // that the register allocation stays the one without batches)
+                const int32_t L = (int32_t)stride;
+                const int64_t bt = (int64_t)s_hi - lo;                     // the stripe's end (< 2^31 here)
+                const uint32_t s_all = pre ? 0u : KVR_SPEC_BATCH ? (uint32_t)((bt - s_cur + L - 1) / L) : s_n;
+                const uint32_t s_nb = s_all < 64u ? s_all : 64u;            // (>= s_n: bt >= vhi_r)
+                const int32_t sc = s_cur + lane * L;
+                const bool act = (uint32_t)lane < s_nb;
                 // its windows first, then the next tile's load: the decode waits for the windows alone
                 uint32_t sw[WINW];
                 const int32_t ao = act ? (sc & ~3) : (int32_t)0x7FFFFF00;
@@ -1734,9 +1764,11 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     load_unit(abase, d0, len, k + 1, lane, w);
                     loaded = true;
                 }
-                Dec d = decode(sc, act, 0, false, sw);
+                Dec d = decode(sc, act, 0, false, sw, (int32_t)bt);
                 const bool bad = act && !(d.ok && d.op == 0u && d.klen == spec_ku && d.vlen == spec_vu);
-                if (__ballot(bad)) {   // not as predicted: frame the tile as usual
+                const uint64_t mbad = __ballot(bad);
+                const uint32_t f = mbad ? (uint32_t)__builtin_ctzll(mbad) : s_nb;   // first record not as predicted
+                if (!pre && f < s_n) {   // not as predicted in this tile: frame the tile as usual
                     no_spec = true;
                     spec_next = false;
                     loaded = false;
@@ -1744,10 +1776,30 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     --k;
                     continue;
                 }
-                const uint32_t slot0 = claim(s_n);
-                (void)emit(d, sc, act, (uint32_t)lane, s_n, 0, (int)s_n - 1, true, slot0);
+                // records of whole tiles only: up to the tile of the first record not verified
+                uint32_t ne = s_nb;
+                if (f < s_all) {
+                    const int32_t tcut = (s_cur + (int32_t)f * L) >> 13;   // (TILE = 2^13)
+                    const uint32_t nt = (uint32_t)((tcut * TILE - s_cur + L - 1) / L);
+                    ne = nt < f ? nt : f;
+                }
+                // (pre: claim(0) only sets b1 to chunk_base; the tile's slots are the last `ahead` claimed)
+                const uint32_t slot0 = claim(ne) - (pre ? ahead : 0u);
+                b1 = pre ? slot0 : b1;
+                (void)emit(d, sc, (uint32_t)lane < ne, (uint32_t)lane, s_n, 0, (int)s_n - 1, true, slot0);
                 nrec = err_rec != N32 ? err_rec : nrec + s_n;
-                tile_exit = (uint64_t)(lo + (int64_t)(int32_t)rl32(d.nx, (int)s_n - 1));
+                fast_skip = pre ? fast_skip - (s_n << 16) : (err_rec != N32 ? 0u : (ne - s_n) << 16);
+                tile_exit = pre ? (uint64_t)(lo + (int64_t)s_cur + (int64_t)s_n * L)
+                                : (uint64_t)(lo + (int64_t)(int32_t)rl32(d.nx, (int)s_n - 1));
+                // a pre tile's last record with a long value starting past the tile: carried (emit's rule)
+                const uint32_t vbl = (uint32_t)(s_cur + ((int32_t)s_n - 1) * L + 9 + (int32_t)spec_ku);
+                const bool pc = pre && spec_vu > (uint32_t)SMALL && vbl >= (uint32_t)TILE &&
+                                ((vbl ^ (vbl + spec_vu - 1u)) >> SC_LOG) != 0u;
+                n_carry = pc ? 2u : n_carry;
+                n_vb = pc ? (uint64_t)(lo + (int64_t)vbl) : n_vb;
+                n_ve = pc ? (uint64_t)(lo + (int64_t)vbl) + spec_vu : n_ve;
+                n_ref = pc ? s_n - 1u : n_ref;
+                n_abs = pc ? false : n_abs;
                 tile_result();
                 if (n_carry == 2u && !n_abs) n_ref = slot_of(n_ref, false);
                 if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(KVR_FIN_PRIO);   // (emit left the framing's)

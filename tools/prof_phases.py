@@ -58,11 +58,14 @@ for it in range(3):
     lib.kvr_prof_read(prof, 0)
 # KVR_STAMP slots of kvr_replay_kernel.hip (unused slots print 0)
 names = ["setup(load)", "stride-decode", "hop-loop+rest", "finalize", "bookkeep", "wait(vmcnt)", "stride-emit",
-         "cand-swar", "crc-entry", "unit-loop+kmul", "scan", "cand-decode", "cand-walk", "cand-emit", "-", "-"]
+         "cand-swar", "crc-entry", "unit-loop+kmul", "scan", "cand-decode", "cand-walk", "cand-emit", "spec tiles", "batched tiles"]
 tiles = st.n_tiles
-tot_c = sum(prof[i] for i in range(16))
+tot_c = sum(prof[i] for i in range(14))   # (slots 14, 15: tile counts, KVR_PROF builds)
 print(f"{cfg}: rc={rc} n={n.value}/{nrec} bytes={tot} tiles={tiles} stripes={st.n_stripes} ms_replay={st.ms_replay:.3f}"
       f" GB/s={tot / st.ms_replay / 1e6:.1f}")
 for i, nm in enumerate(names):
+    if i >= 14:
+        print(f"  {nm:10s} {prof[i] / tiles:10.3f} of the tiles")
+        continue
     print(f"  {nm:10s} {prof[i] / tiles:10.0f} cycles/tile  {100 * prof[i] / max(tot_c, 1):5.1f}%")
 print(f"  total      {tot_c / tiles:10.0f} cycles/tile (wave-0 lane-0 view)")
