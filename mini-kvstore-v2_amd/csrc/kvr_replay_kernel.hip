@@ -1758,13 +1758,26 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 // its windows first, then the next tile's load: the decode waits for the windows alone
                 uint32_t sw[WINW];
                 const int32_t ao = act ? (sc & ~3) : (int32_t)0x7FFFFF00;
+                if (!pre) {
 #pragma unroll
-                for (int i = 0; i < WINW; ++i) sw[i] = ts.w32a(ao + 4 * i);
+                    for (int i = 0; i < WINW; ++i) sw[i] = ts.w32a(ao + 4 * i);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < WINW; ++i) sw[i] = 0u;
+                }
                 if (need_next && !loaded) {
                     load_unit(abase, d0, len, k + 1, lane, w);
                     loaded = true;
                 }
-                Dec d = decode(sc, act, 0, false, sw, (int32_t)bt);
+                Dec d;
+                if (!pre) {
+                    d = decode(sc, act, 0, false, sw, (int32_t)bt);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < WINW; ++i) d.win[i] = 0u;
+                    d.s = d.op = d.klen = d.vlen = d.vb = d.nx = 0u;
+                    d.ok = false;
+                }
                 const bool bad = act && !(d.ok && d.op == 0u && d.klen == spec_ku && d.vlen == spec_vu);
                 const uint64_t mbad = __ballot(bad);
                 const uint32_t f = mbad ? (uint32_t)__builtin_ctzll(mbad) : s_nb;   // first record not as predicted
@@ -1786,7 +1799,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 // (pre: claim(0) only sets b1 to chunk_base; the tile's slots are the last `ahead` claimed)
                 const uint32_t slot0 = claim(ne) - (pre ? ahead : 0u);
                 b1 = pre ? slot0 : b1;
-                (void)emit(d, sc, (uint32_t)lane < ne, (uint32_t)lane, s_n, 0, (int)s_n - 1, true, slot0);
+                if (!pre) (void)emit(d, sc, (uint32_t)lane < ne, (uint32_t)lane, s_n, 0, (int)s_n - 1, true, slot0);
                 nrec = err_rec != N32 ? err_rec : nrec + s_n;
                 fast_skip = pre ? fast_skip - (s_n << 16) : (err_rec != N32 ? 0u : (ne - s_n) << 16);
                 tile_exit = pre ? (uint64_t)(lo + (int64_t)s_cur + (int64_t)s_n * L)
