@@ -397,6 +397,58 @@ def test_linked_gather_and_link_kernel(gctx, monkeypatch, name, tps, link_kernel
         gctx.set_tiles_per_stripe(0)
 
 
+def _equal_store(n_rec, klen=10, vlen=1000, change=None):
+    """n_rec equal SETs (the batched speculative tiles' case: ~8 records a tile), record i's key
+    and value derived from i; change = (i, kind) alters record i: 'utf8' (an invalid key byte),
+    'opcode' (opcode 7), 'vlen' (a shorter value, a valid record), 'del' (a DEL instead),
+    'klen' (a longer key, valid)."""
+    out = bytearray()
+    for i in range(n_rec):
+        k = (b"k%09d" % i)[:klen].ljust(klen, b"x")
+        v = bytes((i * 7 + j) & 255 for j in range(vlen))
+        if change and change[0] == i:
+            kind = change[1]
+            if kind == "utf8":
+                k = k[:3] + b"\xff" + k[4:]
+            elif kind == "vlen":
+                v = v[: vlen - 123]
+            elif kind == "klen":
+                k = k + b"yyyy"
+            elif kind == "del":
+                out += rec_del(k)
+                continue
+            if kind == "opcode":
+                out += b"\x07" + len(k).to_bytes(4, "little") + k + len(v).to_bytes(4, "little") + v
+                continue
+        out += rec_set(k, v)
+    return bytes(out)
+
+
+@pytest.mark.parametrize("tps", [0, 8, 64])
+@pytest.mark.parametrize("change", [None, "utf8", "opcode", "vlen", "del", "klen", "trunc"])
+def test_batched_speculative_tiles(gctx, tps, change):
+    """Equal records over long stripes: speculative tiles verify and emit the predicted records of
+    the next whole tiles in one batch.  A record several tiles into a batch that is not as
+    predicted (another value or key length, a DEL: valid; a bad opcode, an invalid UTF-8 key:
+    errors, the latter found only by the records phase) and a segment cut mid-record must give
+    the oracle's tuples or first error, at several record indices past a tile boundary."""
+    n_rec = 2200                                   # ~2.2 MB: 280 tiles
+    picks = [None] if change is None else [41, 97, 530, 1777]
+    gctx.set_tiles_per_stripe(tps)
+    try:
+        for i in picks:
+            if change == "trunc":
+                seg = _equal_store(n_rec)
+                cut = i * 1019 + 600                   # inside record i's value
+                segs = [seg[:cut]]
+            else:
+                segs = [_equal_store(n_rec, change=None if i is None else (i, change))]
+            segs = segs + [_equal_store(300)]          # a clean segment behind it
+            check_parity(gctx, segs)
+    finally:
+        gctx.set_tiles_per_stripe(0)
+
+
 def _varied_store(seed, n_bytes, del_frac, klen_rng, vlen_rng, zero_values=False, key_alphabet=None):
     """Records of varying lengths (the candidate rounds' case): keys of random length from
     key_alphabet (ASCII letters by default), values random or all zero."""
