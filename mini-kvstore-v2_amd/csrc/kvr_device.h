@@ -9,7 +9,7 @@
  *     one tile ahead.  The tile never goes to LDS: the framing reads headers out of the
  *     registers (readlane), records read their keys through a range-checked buffer resource.
  *   - CRC-32 (reflected 0xEDB88320, crc32fast semantics, src/volume/storage.rs:27) runs on
- *     lane-replicated slice-by-2 byte tables in LDS; register states move across units with
+ *     lane-replicated slice-by-4 byte tables in LDS; register states move across units with
  *     the constants x^(8*128*d) (nibble tables), never with a variable GF(2) multiply.
  */
 #ifndef KVR_DEVICE_H
