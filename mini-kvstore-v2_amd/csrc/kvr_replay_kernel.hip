@@ -111,6 +111,9 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #ifndef KVR_SPEC_BATCH   // 1: a speculative tile verifies and emits the predicted records of the next
 #define KVR_SPEC_BATCH 1   // tiles of its stripe too, up to 64 (one framing and records phase per ~8 tiles)
 #endif
+#ifndef KVR_SPEC_BATCH_MAX   // records a batch decodes at most (<= 64 lanes; >= the records of one tile)
+#define KVR_SPEC_BATCH_MAX 32
+#endif
 #ifndef KVR_SUCC   // 1: the candidate chain follows precomputed successor slots (0: a ballot per record)
 #define KVR_SUCC 1
 #endif
@@ -1752,7 +1755,8 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 const int32_t L = (int32_t)stride;
                 const int64_t bt = (int64_t)s_hi - lo;                     // the stripe's end (< 2^31 here)
                 const uint32_t s_all = pre ? 0u : KVR_SPEC_BATCH ? (uint32_t)((bt - s_cur + L - 1) / L) : s_n;
-                const uint32_t s_nb = s_all < 64u ? s_all : 64u;            // (>= s_n: bt >= vhi_r)
+                const uint32_t s_cap = s_n > (uint32_t)KVR_SPEC_BATCH_MAX ? s_n : (uint32_t)KVR_SPEC_BATCH_MAX;
+                const uint32_t s_nb = s_all < s_cap ? s_all : s_cap;         // (>= s_n: bt >= vhi_r)
                 const int32_t sc = s_cur + lane * L;
                 const bool act = (uint32_t)lane < s_nb;
                 // its windows first, then the next tile's load: the decode waits for the windows alone
