@@ -129,7 +129,9 @@ int  kvr_ctx_set_tiles_per_stripe(kvr_ctx *ctx, uint32_t tiles);
  * expected_crc (optional, may be NULL): expected CRC per record in tuple order, e.g. the
  * ETags BlobStorage::put returned (storage.rs:27); records with index < n_expected get
  * KVR_TF_VERIFIED and, on mismatch, KVR_TF_CRC_FAIL.
- * Returns KVR_OK, KVR_CORRUPTED (*err), KVR_CAPACITY (*n_out = required) or < 0. */
+ * Returns KVR_OK, KVR_CORRUPTED (*err), KVR_CAPACITY (*n_out = required) or < 0.
+ * Slots of out past *n_out are unspecified: a call whose linked gather falls back may have written
+ * scratch tuples there (always inside out[0..cap)). */
 int  kvr_replay(kvr_ctx *ctx, const kvr_segment *segs, size_t n_segs, uint32_t flags,
                 const uint32_t *expected_crc, size_t n_expected,
                 kvr_tuple *out, size_t cap, size_t *n_out, kvr_error *err);

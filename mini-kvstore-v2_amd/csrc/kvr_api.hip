@@ -129,6 +129,7 @@ struct kvr_ctx {
     DevBuf<uint32_t> seg_bad, seg_err, expected;
     DevBuf<uint64_t> soff;                 // each stripe's output offset (k_link, for k_compact_s)
     DevBuf<uint32_t> scnt;                 // each stripe's record count, dense (k_replay, for linked k_compact_s)
+    DevBuf<PieceHand> hand;                // k_piece -> k_replay: where each stripe's tile loop resumes
     DevBuf<uint32_t> crc, kmul, initx;
     DevBuf<GenRecDev> gen;
     // compaction (kvr_compact)
@@ -373,7 +374,7 @@ void kvr_ctx_destroy(kvr_ctx *c) {
     c->pool.release(); c->dense.release(); c->redo.release();
     c->link.p = nullptr; c->ctr.p = nullptr;   // (inside lcbuf)
     c->lcbuf.release();
-    c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->soff.release(); c->scnt.release();
+    c->seg_bad.release(); c->seg_err.release(); c->expected.release(); c->soff.release(); c->scnt.release(); c->hand.release();
     c->crc.release(); c->kmul.release(); c->initx.release(); c->gen.release();
     c->kpool.release(); c->ckeys.release(); c->ctk.release();
     c->ctup.release(); c->lout.release(); c->fent.release(); c->flist.release(); c->fcnt.release(); c->fsz.release();
@@ -626,7 +627,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
 
     if (c->segs.ensure(n) || c->stripes.ensure(n_stripes) || c->sres.ensure(n_stripes) ||
         c->tres.ensure(n_tiles) || c->redo.ensure(std::max<uint32_t>(n_stripes, REDO_GRID)) ||
-        c->seg_bad.ensure(n) || c->seg_err.ensure(n) || c->soff.ensure(n_stripes) || c->scnt.ensure(n_stripes))
+        c->seg_bad.ensure(n) || c->seg_err.ensure(n) || c->soff.ensure(n_stripes) || c->scnt.ensure(n_stripes) || c->hand.ensure(n_stripes))
         return KVR_ENOMEM;
     // (the same segments as the last call: the descriptors on the device are still these)
     if (c->up_segs_p != c->segs.p || c->up_segs.size() != n ||
@@ -722,9 +723,19 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             c->h_ctr->overflow = 0;
         }
         if (markers) HIPCHK(hipEventRecord(c->ev[0], st));
+        // k_piece takes every stripe first (runs of equal SETs, value-aligned) and hands the rest of a
+        // stripe to k_replay's tile loop; ms_replay spans both
+        const bool piece = !getenv_flag("KVR_NO_PIECE");
+        if (piece) {
+            hipExtLaunchKernelGGL(k_piece, dim3((n_stripes + KR_WPB - 1) / KR_WPB), dim3(KR_RT), 0, st,
+                                  markers ? nullptr : c->ev[0], nullptr, 0u, c->segs.p, c->stripes.p, n_stripes, c->sres.p,
+                                  c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, pool_chunk, kp, c->scnt.p, c->hand.p);
+            HIPCHK(hipGetLastError());
+        }
         hipExtLaunchKernelGGL(KR_KERNEL, dim3((n_stripes + KR_WPB - 1) / KR_WPB), dim3(KR_RT), 0, st,
-                              markers ? nullptr : c->ev[0], markers ? nullptr : c->ev[1], 0u, c->segs.p, c->stripes.p,
-                              n_stripes, c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, pool_chunk, kp, c->scnt.p);
+                              markers || piece ? nullptr : c->ev[0], markers ? nullptr : c->ev[1], 0u, c->segs.p, c->stripes.p,
+                              n_stripes, c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, pool_chunk, kp, c->scnt.p,
+                              piece ? c->hand.p : nullptr);
         HIPCHK(hipGetLastError());
         if (markers) HIPCHK(hipEventRecord(c->ev[1], st));
         if (!linked) {
@@ -742,16 +753,21 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         // failures there; when the call did not end cleanly the device block is copied as it is
         HIPCHK(wait_event(c->ev[3]));
         bool lc_switch = false;   // a clean linked pass: the next call uses the other (cleared) block
+        bool relinked = false;    // the linked gather gave up: k_link and the plain gather ran after it
         if (linked) {
             if (c->h_ctr->overflow) {
                 c->h_link->status = 0;   // (the pool is grown below)
             } else if (c->h_ctr->unlinked) {
                 // a stripe did not link on its own (an error, a wrong speculation, a pass-through
-                // stripe it could not check): k_link and the plain gather, as without linking
+                // stripe it could not check): k_link and the plain gather, as without linking.  The
+                // stats then time the pipeline to this gather's end, k_link included.
+                HIPCHK(hipEventRecord(c->ev[2], st));
                 launch_link();
-                launch_compact(false, nullptr);
+                HIPCHK(hipEventRecord(c->ev[4], st));
+                launch_compact(false, c->ev[3]);
                 HIPCHK(hipGetLastError());
                 HIPCHK(wait_stream(st, c->ev[5]));
+                relinked = true;
             } else {
                 c->h_link->status = 0;
                 c->h_link->n_redo = 0;
@@ -765,8 +781,8 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             HIPCHK(hipStreamSynchronize(st));
         }
         c->stats.ms_replay = ev_ms(c->ev[0], c->ev[1]);
-        c->stats.ms_link = linked ? 0.0f : ev_ms(c->ev[1], c->ev[2]);
-        c->stats.ms_compact = ev_ms(linked ? c->ev[1] : c->ev[2], c->ev[3]);
+        c->stats.ms_link = relinked ? ev_ms(c->ev[2], c->ev[4]) : linked ? 0.0f : ev_ms(c->ev[1], c->ev[2]);
+        c->stats.ms_compact = relinked ? ev_ms(c->ev[4], c->ev[3]) : ev_ms(linked ? c->ev[1] : c->ev[2], c->ev[3]);
         c->stats.ms_total = ev_ms(c->ev[0], c->ev[3]);
 
         // rare: more re-walk rounds (a speculated entry was wrong twice in a row)

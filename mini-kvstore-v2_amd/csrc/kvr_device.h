@@ -73,6 +73,20 @@ struct TileRes {          // a tile's tuples in the pool: [pool_off, + count1) t
 
 struct RedoEnt { uint32_t stripe; uint32_t pad; uint64_t entry; };
 
+struct PieceHand {        // k_piece -> k_replay, one per stripe: where the tile loop resumes
+    uint64_t entry;       // its chain position (NONE: the entry search goes on from tile k)
+    uint64_t stripe_entry;   // the stripe's first record start (NONE: not found yet)
+    uint32_t k;           // the tile it resumes at
+    uint32_t ahead;       // records starting in tile k that k_piece emitted (the wave's last claimed slots)
+    uint32_t stride;      // the last record length (the stride round's prediction; 0: none)
+    uint32_t total;       // records of the tiles before k
+    uint32_t chunk_base, chunk_left;   // the wave's pool chunk
+    uint32_t run_first, run_contig;    // the stripe's tuples so far: one run of the pool from run_first
+    uint32_t done;        // 1: k_piece finished the stripe (StripeRes, scnt and every TileRes written)
+    uint32_t pad;
+};
+static_assert(sizeof(PieceHand) == 56, "PieceHand layout");
+
 struct LinkResult {
     int32_t  status;      // 0 ok, 1 corrupted, 3 unresolved (re-walk needed)
     uint32_t n_redo;

@@ -615,10 +615,11 @@ int kvs_open_ex(const char *dir, kvr_ctx *ctx, uint32_t flags, kvs_store **out, 
         sizes.push_back(dir_like ? 0 : (uint64_t)fs.st_size);
     }
     // test knob: segment i's file disappears between discovery and the read (the race that
-    // test_open_vanished_segment drives deterministically)
+    // test_open_vanished_segment drives deterministically).  Nothing is deleted: the loader is given a
+    // path that does not exist in place of the file's, so its open fails as for a vanished file.
     if (const char *vn = getenv("KVS_TEST_VANISH")) {
         const size_t vi = (size_t)strtoull(vn, nullptr, 10);
-        if (vi < n_ok) unlink(paths[vi].c_str());
+        if (vi < n_ok) paths[vi] = std::string("/nonexistent/kvs-test-vanished/") + std::to_string(vi);
     }
 
     std::unique_ptr<kvs_store> s(new kvs_store());

@@ -53,7 +53,7 @@ constexpr int SC_LOG = 7;
 static_assert(SC == 1 << SC_LOG, "unit size");
 static_assert(TILE == 64 * SC, "one unit per lane");
 static_assert(UW == 32, "unit = 32 dwords");
-static_assert(TILE == 1 << 13, "tile offsets >> 13 (the speculative batch)");
+static_assert(TILE == 1 << 13, "tile of a segment position: (pos + d0) >> 13 (the piece mode)");
 constexpr uint32_t N32 = 0xFFFFFFFFu;
 constexpr uint32_t POOL_CHUNK = 2048;     // pool slots a wave claims at once
 constexpr uint32_t TILE_RECS = TILE / 5 + 1;   // most record starts a tile can hold
@@ -105,15 +105,17 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #ifndef KVR_CANDFRAME   // 1: candidate-chain rounds for what the stride round leaves (records of varying lengths)
 #define KVR_CANDFRAME 1
 #endif
-#ifndef KVR_SPEC   // 1: a tile after a clean stride round of equal SETs runs its unit loop on the predicted
-#define KVR_SPEC 1    // framing and verifies it after (the next tile's load then runs under the decode)
+#ifndef KVR_UMODE   // 1: runs of SETs of one key and one value length go through the piece mode (uniform_run)
+#define KVR_UMODE 1
 #endif
-#ifndef KVR_SPEC_BATCH   // 1: a speculative tile verifies and emits the predicted records of the next
-#define KVR_SPEC_BATCH 1   // tiles of its stripe too, up to 64 (one framing and records phase per ~8 tiles)
+#ifndef KVR_PDB     // 1: k_piece loads step s + 1 before it processes step s (two piece buffers)
+#define KVR_PDB 0
 #endif
-#ifndef KVR_SPEC_BATCH_MAX   // records a batch decodes at most (<= 64 lanes; >= the records of one tile)
-#define KVR_SPEC_BATCH_MAX 32
+#ifndef KVR_UMIN    // the shortest value the piece mode takes (pieces are 128 B: shorter values waste lanes)
+#define KVR_UMIN 128
 #endif
+constexpr uint32_t UMAXV = 1u << 24;     // the piece mode's longest value (window offsets stay in 32 bits)
+constexpr int UKEYW = 9;                 // ... and longest key: 4 UKEYW bytes, in the 48-B header window
 #ifndef KVR_SUCC   // 1: the candidate chain follows precomputed successor slots (0: a ballot per record)
 #define KVR_SUCC 1
 #endif
@@ -781,21 +783,104 @@ __device__ __forceinline__ TileSeg tile_seg(const uint8_t *abase, const uint8_t 
 }
 
 // ---------------------------------------------------------------------------------------
+// the piece mode (uniform_run in replay_body)
+// ---------------------------------------------------------------------------------------
+// a lane's 128-B piece at byte offset o of the resource (any alignment: byte-unaligned 16-B buffer
+// loads; offsets past the resource read 0)
+__device__ __forceinline__ void load_piece(__amdgpu_buffer_rsrc_t rs, int o, uint32_t (&w)[UW]) {
+#pragma unroll
+    for (int i = 0; i < UW / 4; ++i) {
+        const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16 * i, 0, 0);
+        w[4 * i] = a.x; w[4 * i + 1] = a.y; w[4 * i + 2] = a.z; w[4 * i + 3] = a.w;
+    }
+}
+// zero the first zb (wave-uniform, < SC) bytes of the piece on lanes with `on` (a value's first
+// piece: the bytes before the value start; leading zeros leave a CRC register of 0 unchanged)
+__device__ __forceinline__ void mask_lead(uint32_t (&w)[UW], bool on, uint32_t zb) {
+    const uint32_t zw = zb >> 2, part = on ? ~0u << (8u * (zb & 3u)) : ~0u;
+#pragma unroll
+    for (int i = 0; i < UW; ++i) {
+        if ((uint32_t)i < zw) w[i] = on ? 0u : w[i];
+        else if ((uint32_t)i == zw) w[i] &= part;
+    }
+}
+// the raw CRC register (from 0) of the lane's 128 B: two slice-by-4 chains over words 0-15 and
+// 16-31 (no value boundary inside), the first pushed through the second's 64 bytes
+__device__ __forceinline__ uint32_t piece_raw(const uint32_t (&w)[UW], const Crc &K, const Smem &S) {
+    constexpr int H = UW / 2;
+    uint32_t xa = w[0], xb = w[H], ca = 0, cb = 0;
+#pragma unroll
+    for (int kk = 0; kk < H; ++kk) {
+        uint32_t ta, a3, tb, b3;
+        look4x2(xa, xb, K, ta, a3, tb, b3);
+        if (kk + 1 < H) {
+            xa = xor3(ta, a3, w[kk + 1]);
+            xb = xor3(tb, b3, w[kk + 1 + H]);
+        } else {
+            ca = ta ^ a3;
+            cb = tb ^ b3;
+        }
+    }
+    return kmul(ca, S.KQ2) ^ cb;
+}
+// segmented inclusive XOR scan over the lanes (DPP only): fm all ones starts a segment
+__device__ __forceinline__ uint32_t seg_xscan(uint32_t v, uint32_t fm) {
+    uint32_t ov;
+    ov = dpp<0x111>(v); v = bitop3_xandn(v, ov, fm); fm |= dpp<0x111>(fm);
+    ov = dpp<0x112>(v); v = bitop3_xandn(v, ov, fm); fm |= dpp<0x112>(fm);
+    ov = dpp<0x114>(v); v = bitop3_xandn(v, ov, fm); fm |= dpp<0x114>(fm);
+    ov = dpp<0x118>(v); v = bitop3_xandn(v, ov, fm); fm |= dpp<0x118>(fm);
+    ov = dpp<0x142, 0xA, false>(v); v = bitop3_xandn(v, ov, fm); fm |= dpp<0x142, 0xA, false>(fm);
+    return bitop3_xandn(v, dpp<0x143, 0xC, false>(v), fm);
+}
+// a buffer resource over segment bytes [pos, len) (at most 2^31 - 256 of them; none past len)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t seg_rsrc(const uint8_t *seg, uint64_t pos, uint64_t len) {
+    const uint64_t n = pos < len ? len - pos : 0ull;
+    const int nr = n > 0x7FFFFF00ull ? 0x7FFFFF00 : (int)n;
+    const uint64_t b = (uint64_t)(seg + pos);
+    const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)b), bhi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)bhi << 32) | blo), (short)0,
+                                             __builtin_amdgcn_readfirstlane(nr), 0x00020000);
+}
+
+// ---------------------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------------------
-// REDO: the re-walk pass (k_rewalk) over k_link's list, with the walk-on into later stripes; the
-// first pass (k_replay) walks every stripe once
-template <bool REDO>
-__device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
-                                            const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
-                                            StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
-                                            kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
-                                            Tables tb, const RedoEnt *__restrict__ redo,
-                                            const LinkResult *__restrict__ link, uint32_t pool_chunk,
-                                            uint4 *__restrict__ kpool, uint32_t *__restrict__ scnt) {
-    constexpr bool redo_mode = REDO;
-    __shared__ Smem S;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+// The stripe's entry in tile [lo, lo + TILE): its first plausible record start, or NONE (k_link
+// verifies it).  Candidate op bytes (0x00 / 0x01) come straight from the registers, kept only when the
+// top byte of the key length after them (byte b of the next word) does not exceed the top byte of the
+// segment bytes left: a necessary condition, word-wide (SWAR).  plausible() (memory reads, the exact
+// tests) runs on the survivors alone, one per lane and round, so the lanes' dependent loads run side
+// by side; a lane keeps its lowest plausible start, and lanes above the lowest lane holding one stop
+// (unit positions grow with the lane).  [o0, o1): this lane's unit offsets inside the segment.
+__device__ inline uint64_t find_entry(const uint32_t (&w)[UW], const TileSeg &ts, int64_t lo, int64_t rem, int o0, int o1,
+                                      int lane) {
+    const int us = lane * SC;
+    uint32_t cm[4];
+    cand_masks(w, rem, cm);
+    int cand = -1;
+    uint32_t m0 = cm[0], m1 = cm[1], m2 = cm[2], m3 = cm[3];
+#pragma unroll 1
+    for (;;) {
+        const uint64_t fnd = __ballot(cand >= 0);
+        if (fnd != 0ull && lane > (int)__builtin_ctzll(fnd)) { m0 = m1 = m2 = m3 = 0u; }
+        if (__ballot((m0 | m1 | m2 | m3) != 0u) == 0ull) break;
+        if ((m0 | m1 | m2 | m3) != 0u) {
+            const int q = m0 ? 0 : m1 ? 1 : m2 ? 2 : 3;
+            const uint32_t mb = q == 0 ? m0 : q == 1 ? m1 : q == 2 ? m2 : m3;
+            const uint32_t nb = mb & (mb - 1u);
+            m0 = q == 0 ? nb : m0; m1 = q == 1 ? nb : m1; m2 = q == 2 ? nb : m2; m3 = q == 3 ? nb : m3;
+            const int t = __builtin_ctz(mb);
+            const int o = us + 32 * q + 4 * (t & 7) + (t >> 3);
+            if (o >= o0 && o < o1 && (cand < 0 || o < cand) && plausible(ts, o)) cand = o;
+        }
+    }
+    const uint64_t fnd = __ballot(cand >= 0);
+    return fnd == 0ull ? NONE : (uint64_t)(lo + (int64_t)rl32((uint32_t)cand, (int)__builtin_ctzll(fnd)));
+}
+
+// the CRC and multiply tables, global -> LDS (every workgroup of k_replay, k_rewalk and k_piece)
+__device__ __forceinline__ void stage_tables(Smem &S, const Tables &tb, int tid) {
     for (int i = tid; i < 256 * 64; i += RT) S.C2[i] = tb.crc8[c2_table(i & 63) * 256 + (i >> 6)];
     for (int i = tid; i < 8 * 16 * KR_PITCH; i += RT) {
         const int row = i / KR_PITCH, kk = i - row * KR_PITCH;   // row = 16 i + n
@@ -807,6 +892,27 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
     }
     for (int i = tid; i < 2 * 8 * 16; i += RT) S.KQ2[i] = tb.kmul[(KSET_Q + (i < 128 ? SC / 8 : SC / 4)) * 8 * 16 + (i & 127)];
     if (tid < NIX) S.IX[tid] = tb.initx[tid];
+}
+
+// REDO: the re-walk pass (k_rewalk) over k_link's list, with the walk-on into later stripes; the
+// first pass (k_replay) walks every stripe once
+template <bool REDO>
+__device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
+                                            const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
+                                            StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
+                                            kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
+                                            Tables tb, const RedoEnt *__restrict__ redo,
+                                            const LinkResult *__restrict__ link, uint32_t pool_chunk,
+                                            uint4 *__restrict__ kpool, uint32_t *__restrict__ scnt,
+                                            const PieceHand *__restrict__ hand) {
+    constexpr bool redo_mode = REDO;
+    __shared__ Smem S;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (!REDO && hand) {   // after k_piece: a workgroup whose stripes it all finished has nothing to do
+        const uint32_t g = blockIdx.x * WPB + (uint32_t)wv;
+        if (!__syncthreads_or(g < n_stripes && !hand[g].done)) return;
+    }
+    stage_tables(S, tb, tid);
     __syncthreads();   // the only workgroup barrier: from here on every wave is on its own
     uint32_t *const MK = S.MK[wv];   // this wave's long-value marks
 
@@ -855,14 +961,9 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
     }
     uint64_t err_pos = NONE, err_aux = 0;
     uint32_t err_kind = 0, total = 0;
-    // (fast_skip bits 16 on: the records of the next tiles a speculative tile's batch already verified and
-    // emitted, whole tiles; their slots are the last ones claimed, chunk_base - that count on.  Kept in
-    // fast_skip, which is 0 whenever a speculative tile runs: one more loop-carried value made the
-    // register allocator spill the tile registers to scratch)
-    uint32_t stride = 0, fast_skip = 0;           // lane-parallel framing: the last record length, tiles
-                                                  // left to the scalar hop loop
-    bool spec_next = false, no_spec = false;      // the last stride round was one clean round of equal
-    uint32_t spec_ku = 0, spec_vu = 0;            // SETs (key and value lengths): KVR_SPEC's prediction
+    // (fast_skip bits 16 on: the records of the tile k_piece handed back that it emitted, the last ones
+    // claimed (chunk_base - that count on); bits 0-15: tiles left to the scalar hop loop)
+    uint32_t stride = 0, fast_skip = 0;           // lane-parallel framing: the last record length
     uint32_t run_first = N32;                     // the stripe's first pool slot, while its tuples are one run
     bool run_contig = true;                       // (no second chunk claimed after its first tuple)
     uint32_t carry = 0, c_state = 0;              // 1: a long value crosses the tile start (c_state: its register);
@@ -872,6 +973,21 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
     uint32_t w[UW];     // this lane's unit of the tile (the next tile's load is issued as soon as the
     bool loaded = false;   // CRC phase is done with these registers, see the end of the loop body)
     uint32_t k = sd.t_begin;
+    if (!REDO && hand) {   // k_piece went first: it finished the stripe, or hands it back from tile h.k on
+        const PieceHand h = hand[si];
+        if (h.done) break;
+        entry = h.entry;
+        search = entry == NONE;
+        stripe_entry = h.stripe_entry;
+        k = h.k;
+        fast_skip = h.ahead << 16;
+        stride = h.stride;
+        total = h.total;
+        chunk_base = h.chunk_base;
+        chunk_left = h.chunk_left;
+        run_first = h.run_first;
+        run_contig = h.run_contig != 0u;
+    }
 #ifdef KVR_PROF
     unsigned long long t_last = __builtin_amdgcn_s_memtime();
     unsigned long long prof_acc[16] = {};
@@ -913,36 +1029,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
         KVR_STAMP(0);
         // ---- F + R. framing and records -------------------------------------------------------
         if (in_stripe && search) {   // the stripe's entry: the first plausible record start
-            const int o0 = us > (int)vlo_r ? us : (int)vlo_r, o1 = ue < (int)vhi_r ? ue : (int)vhi_r;
-            // candidate op bytes (0x00 / 0x01) straight from the registers, kept only when the top
-            // byte of the key length after them (byte b of the next word) does not exceed the top
-            // byte of the segment bytes left: a necessary condition, word-wide (SWAR).  plausible()
-            // (memory reads, the exact tests) runs on the survivors alone.  cm[g] bit 8 b + j:
-            // byte 4 (8 g + j) + b of the lane's unit.
-            uint32_t cm[4];
-            cand_masks(w, rem, cm);
-            // each round every lane tests one survivor, so the lanes' plausible() calls (dependent
-            // loads) run side by side; a lane keeps its lowest plausible start, and lanes above the
-            // lowest lane holding one stop (unit positions grow with the lane)
-            int cand = -1;
-            uint32_t m0 = cm[0], m1 = cm[1], m2 = cm[2], m3 = cm[3];
-#pragma unroll 1
-            for (;;) {
-                const uint64_t fnd = __ballot(cand >= 0);
-                if (fnd != 0ull && lane > (int)__builtin_ctzll(fnd)) { m0 = m1 = m2 = m3 = 0u; }
-                if (__ballot((m0 | m1 | m2 | m3) != 0u) == 0ull) break;
-                if ((m0 | m1 | m2 | m3) != 0u) {
-                    const int q = m0 ? 0 : m1 ? 1 : m2 ? 2 : 3;
-                    const uint32_t mb = q == 0 ? m0 : q == 1 ? m1 : q == 2 ? m2 : m3;
-                    const uint32_t nb = mb & (mb - 1u);
-                    m0 = q == 0 ? nb : m0; m1 = q == 1 ? nb : m1; m2 = q == 2 ? nb : m2; m3 = q == 3 ? nb : m3;
-                    const int t = __builtin_ctz(mb);
-                    const int o = us + 32 * q + 4 * (t & 7) + (t >> 3);
-                    if (o >= o0 && o < o1 && (cand < 0 || o < cand) && plausible(ts, o)) cand = o;
-                }
-            }
-            const uint64_t fnd = __ballot(cand >= 0);
-            const uint64_t mn = fnd == 0ull ? NONE : (uint64_t)(lo + (int64_t)rl32((uint32_t)cand, (int)__builtin_ctzll(fnd)));
+            const uint64_t mn = find_entry(w, ts, lo, rem, us > (int)vlo_r ? us : (int)vlo_r, ue < (int)vhi_r ? ue : (int)vhi_r, lane);
             if (mn != NONE) { entry = mn; search = false; stripe_entry = mn; }
         }
         const bool walk = in_stripe && !search && entry < vhi;
@@ -979,9 +1066,12 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             else { n_carry = 2; n_vb = c_vb; n_ve = c_ve; n_ref = c_slot; }   // still further on
         }
         // pool slots: the tile's records take at most two runs, [b1, b1 + c1) then [b2, ...)
-        uint32_t b1 = 0, b2 = 0;
+        // (the tile k_piece handed back: its first `ahead` records were emitted, the last slots claimed)
+        const uint32_t ahead = fast_skip >> 16;
+        fast_skip &= 0xFFFFu;
+        uint32_t b1 = chunk_base - ahead, b2 = 0;
         uint32_t c1 = N32;
-        uint32_t nrec = 0, err_rec = N32;    // records emitted; index of the tile's first error
+        uint32_t nrec = ahead, err_rec = N32;   // records emitted; index of the tile's first error
         // claim pool slots for nb more records of the tile (one run: a fresh chunk holds any
         // tile's rest); returns the first slot
         auto claim = [&](uint32_t nb) -> uint32_t {
@@ -1090,21 +1180,15 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
         };
         constexpr uint32_t UNK = 0xFFFFFFFEu;
         const int32_t vhiT = (int32_t)vhi_r, remT = (int32_t)rem;   // (used only when !huge)
-        // (pre: the window already loaded, the speculative tile's; null: loaded here)
-        auto decode = [&](int32_t c, bool act, int kl, bool vmem, const uint32_t *pre, int32_t cend) -> Dec {
+        auto decode = [&](int32_t c, bool act, int kl, bool vmem, int32_t cend) -> Dec {
             Dec d;
             const int32_t a = c & ~3;
             d.s = (uint32_t)c & 3u;
             // (a lane that takes no part reads past the resource, which yields 0 with no memory
             // access: the loads need no exec mask, so no branch around each of them)
             const int32_t ao = act ? a : (int32_t)0x7FFFFF00;
-            if (pre) {
 #pragma unroll
-                for (int i = 0; i < WINW; ++i) d.win[i] = pre[i];
-            } else {
-#pragma unroll
-                for (int i = 0; i < WINW; ++i) d.win[i] = ts.w32a(ao + 4 * i);
-            }
+            for (int i = 0; i < WINW; ++i) d.win[i] = ts.w32a(ao + 4 * i);
             const uint32_t x0 = __builtin_amdgcn_alignbyte(d.win[1], d.win[0], d.s);
             const uint32_t x1 = __builtin_amdgcn_alignbyte(d.win[2], d.win[1], d.s);
             d.op = x0 & 255u;
@@ -1242,47 +1326,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             return fo;
         };
 #endif
-        // ---- speculative tile (KVR_SPEC) -------------------------------------------------------
-        // After a clean stride round of equal SETs the records of this tile are predicted exactly:
-        // they start at cur + j L with the same key and value lengths.  The long values' views are
-        // then folded from the prediction alone (fold_uniform), the unit loop runs on them, the next
-        // tile's load goes out, and only then are the records decoded, checked against the
-        // prediction and emitted: the decode's window loads, issued before that load, do not wait
-        // for it, and its latency runs under the decode, the records, the scan and the finalize.
-        // A record that differs sends the tile back to the top (its registers reloaded) to be
-        // framed as usual; nothing was written for it yet.
-        // A speculative tile decodes, checks and emits in one batch the predicted records of as many
-        // whole tiles ahead as 64 lanes hold (KVR_SPEC_BATCH): the tiles after it in the batch
-        // (`pre`: ahead > 0) only fold, CRC and finalize, with no framing or records phase.
-        bool spec = false;
-        int32_t s_cur = 0;
-        uint32_t s_n = 0;
-        const uint32_t ahead = fast_skip >> 16;
-        const bool pre = ahead != 0u;
-#if KVR_LANEFRAME
-        if (pre || (KVR_SPEC && !KVR_ABLATE && spec_next && !no_spec && walk && rem <= 0x7FFFFFFFll && fast_skip == 0u)) {
-            const int64_t pp = (int64_t)entry - lo;
-            const uint32_t L = stride;
-            if (pp >= 0 && L > (uint32_t)SC && L < (uint32_t)TILE && pp + 64ll * (int64_t)L >= vhi_r) {
-                s_cur = (int32_t)pp;
-                s_n = (uint32_t)((vhi_r - pp + (int64_t)L - 1) / (int64_t)L);   // records starting in the tile
-                spec = true;
-                fold_uniform(s_cur + 9 + (int32_t)spec_ku, (int32_t)L, s_n, (int32_t)spec_vu, nrec);
-            }
-        }
-#endif
-#ifdef KVR_PROF
-        prof_acc[14] += spec ? 1u : 0u;   // (counts, not cycles: speculative tiles, and those of them in a batch)
-        prof_acc[15] += pre ? 1u : 0u;
-#endif
-        if (pre && (!spec || s_n > ahead)) {   // bug trap: a batch always ends at a tile boundary
-            if (lane == 0) atomicOr(&ctr->overflow, 4u);
-            spec = false;
-            fast_skip &= 0xFFFFu;
-        }
-        no_spec = false;
-        if (walk && !spec) {
-            spec_next = false;
+        if (walk) {
             // positions are tile-relative, in 32 bits unless the segment runs more than 2 GiB past
             // the tile (then the 64-bit copy of the exact hop loop takes the whole tile)
             const bool huge = rem > 0x7FFFFFFFll;
@@ -1308,7 +1352,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const bool one = L == 0u || L >= (uint32_t)TILE;   // no usable stride: lane 0 only
                     const int32_t c = cur + (one ? 0 : lane * (int32_t)L);
                     const bool act = lane == 0 || (!one && c < vhiT);
-                    const Dec d = decode(c, act, 0, true, nullptr, vhiT);
+                    const Dec d = decode(c, act, 0, true, vhiT);
                     KVR_STAMP(1);
                     // the first lane whose record is broken or whose successor is not the next
                     // prediction (the last active lane's successor is unconstrained)
@@ -1319,11 +1363,9 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const bool okf = rl32(d.ok ? 1u : 0u, f) != 0u;
                     const uint32_t n_on = okf ? (uint32_t)f + 1u : (uint32_t)f;   // records on the chain
                     const uint32_t cf = rl32((uint32_t)c, f);
-                    bool uni = false;
                     if (n_on) {
                         const uint32_t slot0 = claim(n_on);
                         const Fold fo = emit(d, c, (uint32_t)lane < n_on, (uint32_t)lane, n_on, 0, (int)n_on - 1, !one, slot0);
-                        uni = fo.kind == 1;
                         if (fo.kind == 1) {
                             fold_uniform(cur + 9 + (int32_t)rl32(d.klen, 0), (int32_t)L, n_on, (int32_t)rl32(d.vlen, 0), nrec);
                         } else if (fo.kind == 2) {
@@ -1334,10 +1376,6 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     KVR_STAMP(6);
                     if (!okf) { cur = (int32_t)cf; round_broke = true; break; }   // the exact loop reports it
                     const uint32_t nf = rl32(d.nx, f);
-                    // one clean round of equal SETs over the whole tile: the next tile can be speculated
-                    spec_next = uni && !one && mm == 0ull && err_rec == N32 && nf - cf == L && (int32_t)nf >= vhiT;
-                    spec_ku = rl32(d.klen, 0);
-                    spec_vu = rl32(d.vlen, 0);
                     L = nf - cf;                               // record f's length predicts the next tile
                     cur = (int32_t)nf;
                     if (err_rec != N32) break;
@@ -1405,7 +1443,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     const int32_t c = lane < (int)tot ? (int32_t)MK[lane] : -1;
                     const bool act = c >= p0 && c < vhiT;
                     const uint64_t at0 = __ballot(act && c == p0);
-                    Dec d = decode(act ? c : p0, act, at0 ? (int)__builtin_ctzll(at0) : 0, false, nullptr, vhiT);
+                    Dec d = decode(act ? c : p0, act, at0 ? (int)__builtin_ctzll(at0) : 0, false, vhiT);
                     const uint32_t nxp = act && d.ok ? d.nx : N32;
                     const int32_t wend = cover < vhiT ? cover : vhiT;
                     // each candidate's successor slot (KVR_SUCC): the row slots of the successor's unit
@@ -1609,8 +1647,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             tile_exit = broke ? ERRP : (uint64_t)(lo + p);
         }
         // the tile's result record, stored ahead of the next tile's load, so that the wait for that
-        // load at the loop top does not also wait for this store's ack (a speculative tile stores it
-        // once its records are emitted)
+        // load at the loop top does not also wait for this store's ack
         auto tile_result = [&]() {
             if (c1 == N32) c1 = nrec;
             if (in_stripe && lane == 0) {
@@ -1626,15 +1663,10 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
         auto slot_of = [&](uint32_t ref, bool is_abs) -> uint32_t {
             return is_abs ? ref : (ref < c1 ? b1 + ref : b2 + (ref - c1));
         };
-        if (!spec) {
-            tile_result();
-            if (n_carry == 2u && !n_abs) n_ref = slot_of(n_ref, false);
-        }
-        // the stripe goes on past this tile (a value running past its end is carried on; a
-        // speculative tile's last value may start past it)
-        const bool need_next = err_pos == NONE && k + 1 < sg.n_tiles &&
-                               (k + 1 < sd.t_end || n_carry || out ||
-                                (spec && s_cur + (int32_t)((s_n - 1u) * stride + 9u + spec_ku) >= TILE));
+        tile_result();
+        if (n_carry == 2u && !n_abs) n_ref = slot_of(n_ref, false);
+        // the stripe goes on past this tile (a value running past its end is carried on)
+        const bool need_next = err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry || out);
         KVR_STAMP(2);
         // the word of a value end's partial tail, for the finalize (its latency runs under the unit loop)
         uint32_t wm = 0;
@@ -1698,7 +1730,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             // the unit loop was the tile registers' last reader: the next tile's load is issued
             // here and its latency runs under the scan and the finalize (a speculative tile's, after
             // the scan, behind its windows)
-            if (need_next && !loaded && !spec) {
+            if (need_next && !loaded) {
                 load_unit(abase, d0, len, k + 1, lane, w);
                 loaded = true;
             }
@@ -1746,82 +1778,6 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             KVR_STAMP(10);
             uint32_t sin = dpp<0x138>(v);        // wave_shr:1: the state at this unit's start
             if (lane == 0) sin = c_state;
-#if KVR_LANEFRAME
-            if (spec) {   // the speculative tile's records: decoded, checked against the prediction, emitted
-                // (KVR_SPEC_BATCH: the predicted records of the next tiles of the stripe too, up to 64;
-                // the whole tiles before the first record that is not as predicted are emitted now, and
-                // those tiles (pre) then run this code with no lane taking part -- the same code, so
-                // that the register allocation stays the one without batches)
-                const int32_t L = (int32_t)stride;
-                const int64_t bt = (int64_t)s_hi - lo;                     // the stripe's end (< 2^31 here)
-                const uint32_t s_all = pre ? 0u : KVR_SPEC_BATCH ? (uint32_t)((bt - s_cur + L - 1) / L) : s_n;
-                const uint32_t s_cap = s_n > (uint32_t)KVR_SPEC_BATCH_MAX ? s_n : (uint32_t)KVR_SPEC_BATCH_MAX;
-                const uint32_t s_nb = s_all < s_cap ? s_all : s_cap;         // (>= s_n: bt >= vhi_r)
-                const int32_t sc = s_cur + lane * L;
-                const bool act = (uint32_t)lane < s_nb;
-                // its windows first, then the next tile's load: the decode waits for the windows alone
-                uint32_t sw[WINW];
-                const int32_t ao = act ? (sc & ~3) : (int32_t)0x7FFFFF00;
-                if (!pre) {
-#pragma unroll
-                    for (int i = 0; i < WINW; ++i) sw[i] = ts.w32a(ao + 4 * i);
-                } else {
-#pragma unroll
-                    for (int i = 0; i < WINW; ++i) sw[i] = 0u;
-                }
-                if (need_next && !loaded) {
-                    load_unit(abase, d0, len, k + 1, lane, w);
-                    loaded = true;
-                }
-                Dec d;
-                if (!pre) {
-                    d = decode(sc, act, 0, false, sw, (int32_t)bt);
-                } else {
-#pragma unroll
-                    for (int i = 0; i < WINW; ++i) d.win[i] = 0u;
-                    d.s = d.op = d.klen = d.vlen = d.vb = d.nx = 0u;
-                    d.ok = false;
-                }
-                const bool bad = act && !(d.ok && d.op == 0u && d.klen == spec_ku && d.vlen == spec_vu);
-                const uint64_t mbad = __ballot(bad);
-                const uint32_t f = mbad ? (uint32_t)__builtin_ctzll(mbad) : s_nb;   // first record not as predicted
-                if (!pre && f < s_n) {   // not as predicted in this tile: frame the tile as usual
-                    no_spec = true;
-                    spec_next = false;
-                    loaded = false;
-                    if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(0);
-                    --k;
-                    continue;
-                }
-                // records of whole tiles only: up to the tile of the first record not verified
-                uint32_t ne = s_nb;
-                if (f < s_all) {
-                    const int32_t tcut = (s_cur + (int32_t)f * L) >> 13;   // (TILE = 2^13)
-                    const uint32_t nt = (uint32_t)((tcut * TILE - s_cur + L - 1) / L);
-                    ne = nt < f ? nt : f;
-                }
-                // (pre: claim(0) only sets b1 to chunk_base; the tile's slots are the last `ahead` claimed)
-                const uint32_t slot0 = claim(ne) - (pre ? ahead : 0u);
-                b1 = pre ? slot0 : b1;
-                if (!pre) (void)emit(d, sc, (uint32_t)lane < ne, (uint32_t)lane, s_n, 0, (int)s_n - 1, true, slot0);
-                nrec = err_rec != N32 ? err_rec : nrec + s_n;
-                fast_skip = pre ? fast_skip - (s_n << 16) : (err_rec != N32 ? 0u : (ne - s_n) << 16);
-                tile_exit = pre ? (uint64_t)(lo + (int64_t)s_cur + (int64_t)s_n * L)
-                                : (uint64_t)(lo + (int64_t)(int32_t)rl32(d.nx, (int)s_n - 1));
-                // a pre tile's last record with a long value starting past the tile: carried (emit's rule)
-                const uint32_t vbl = (uint32_t)(s_cur + ((int32_t)s_n - 1) * L + 9 + (int32_t)spec_ku);
-                const bool pc = pre && spec_vu > (uint32_t)SMALL && vbl >= (uint32_t)TILE &&
-                                ((vbl ^ (vbl + spec_vu - 1u)) >> SC_LOG) != 0u;
-                n_carry = pc ? 2u : n_carry;
-                n_vb = pc ? (uint64_t)(lo + (int64_t)vbl) : n_vb;
-                n_ve = pc ? (uint64_t)(lo + (int64_t)vbl) + spec_vu : n_ve;
-                n_ref = pc ? s_n - 1u : n_ref;
-                n_abs = pc ? false : n_abs;
-                tile_result();
-                if (n_carry == 2u && !n_abs) n_ref = slot_of(n_ref, false);
-                if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(KVR_FIN_PRIO);   // (emit left the framing's)
-            }
-#endif
             // the value ending in this unit at m: its register is sin * x^(8m) ^ raw[0, m), and
             // raw[0, 4 qm) is A's snapshot, or all of A pushed through 4 (qm - H) bytes ^ B's: so
             // (base * x^(8*4q) ^ sn) with base = sin, q = qm, or base = sin * x^(8*4H) ^ A, q = qm - H
@@ -1912,9 +1868,9 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                                                StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
                                                kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
                                                Tables tb, uint32_t pool_chunk, uint4 *__restrict__ kpool,
-                                               uint32_t *__restrict__ scnt) {
+                                               uint32_t *__restrict__ scnt, const PieceHand *__restrict__ hand) {
     replay_body<false>(segs, stripes, n_stripes, sres, tres, pool, pool_cap, ctr, tb, nullptr, nullptr, pool_chunk, kpool,
-                       scnt);
+                       scnt, hand);
 }
 
 __global__ __launch_bounds__(RT) void k_rewalk(const SegDesc *__restrict__ segs,
@@ -1925,7 +1881,370 @@ __global__ __launch_bounds__(RT) void k_rewalk(const SegDesc *__restrict__ segs,
                                                const LinkResult *__restrict__ link, uint32_t pool_chunk,
                                                uint4 *__restrict__ kpool) {
     replay_body<true>(segs, stripes, n_stripes, sres, tres, pool, pool_cap, ctr, tb, redo, link, pool_chunk, kpool,
-                      nullptr);
+                      nullptr, nullptr);
+}
+
+
+// ---------------------------------------------------------------------------------------
+// k_piece: the piece mode, first over every stripe.
+// ---------------------------------------------------------------------------------------
+// A stripe that starts with a run of SETs of one key length ku and one value length vu >= KVR_UMIN
+// is replayed value-aligned: every value is cut into P = ceil(vu / 128) pieces that end at its last
+// byte (the first holds r = vu - 128 (P - 1) bytes behind 128 - r masked ones); lane l of a step CRCs
+// piece 64 s + l of the run from a zero register, pushes it by x^(8 128 d) to the lane that completes
+// the value (or carries it on, lane 63), and a segmented XOR scan sums each value there.  No value
+// boundary falls inside a lane's bytes: no snapshot, restart or finalize, ~300 VALU per 8 KiB.  A
+// record's 48-B header window is loaded in the step its value completes; groups of completed records
+// are verified against the prediction (opcode, key length, value length, segment end, UTF-8 key) and
+// emitted with their value CRCs.  The first record not as predicted ends the run, and the stripe is
+// handed to k_replay's tile loop at that record (PieceHand); so is a stripe that does not start with
+// such a record, or whose entry the search has not found in its first tiles.
+__global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, const StripeDesc *__restrict__ stripes,
+                                              uint32_t n_stripes, StripeRes *__restrict__ sres,
+                                              TileRes *__restrict__ tres, kvr_tuple *__restrict__ pool,
+                                              uint64_t pool_cap, Counters *ctr, Tables tb, uint32_t pool_chunk,
+                                              uint4 *__restrict__ kpool, uint32_t *__restrict__ scnt,
+                                              PieceHand *__restrict__ hand) {
+    __shared__ Smem S;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    stage_tables(S, tb, tid);
+    __syncthreads();
+    Crc K;
+    crc_init(K, S.C2, (uint32_t)lane);
+    const uint32_t si = blockIdx.x * WPB + (uint32_t)__builtin_amdgcn_readfirstlane(wv);
+    if (si >= n_stripes) return;
+    const StripeDesc sd = stripes[si];
+    const SegDesc sg = segs[sd.seg];
+    const uint64_t len = sg.len;
+    const int64_t d0 = sg.d0;
+    const int64_t shi_i = (int64_t)sd.t_end * TILE - d0;
+    const uint64_t s_hi = (uint64_t)shi_i > len ? len : (uint64_t)shi_i;
+    const uint8_t *abase = sg.base - d0;
+    uint32_t w[UW];
+    // ---- the entry: offset 0 for a segment's first stripe, else the first plausible record start
+    uint64_t entry = sd.t_begin == 0 ? 0ull : NONE;
+    uint32_t k = sd.t_begin;
+    if (entry == NONE) {
+#pragma unroll 1
+        for (; k < sd.t_end && k < sg.n_tiles; ++k) {
+            load_unit(abase, d0, len, k, lane, w);
+            const int64_t lo = (int64_t)k * TILE - d0;
+            const int64_t vlo_r = lo < 0 ? -lo : 0;
+            const int64_t vhi_r = (lo + TILE > (int64_t)len ? (int64_t)len : lo + TILE) - lo;
+            const int us = lane * SC, ue = us + SC;
+            const TileSeg ts = tile_seg(abase, sg.base, d0, len, k);
+            entry = find_entry(w, ts, lo, (int64_t)len - lo, us > (int)vlo_r ? us : (int)vlo_r,
+                               ue < (int)vhi_r ? ue : (int)vhi_r, lane);
+            if (entry != NONE) break;
+        }
+    }
+    const uint64_t stripe_entry = (entry != NONE && entry >= s_hi) ? NONE : entry;
+    // the wave's pool chunk and the stripe's run of slots
+    uint32_t chunk_base = 0, chunk_left = 0, run_first = N32, total = 0;
+    bool run_contig = true;
+    auto tile_of = [&](uint64_t pos) -> uint32_t { return (uint32_t)((pos + (uint64_t)d0) >> 13); };
+    // hand the stripe to k_replay at the record at pos (tile k_res, `ah` of its records emitted here)
+    auto hand_back = [&](uint64_t pos, uint32_t k_res, uint32_t ah, uint32_t stride) {
+        if (lane == 0) {
+            PieceHand h;
+            h.entry = pos;
+            h.stripe_entry = stripe_entry;
+            h.k = k_res;
+            h.ahead = ah;
+            h.stride = stride;
+            h.total = total;
+            h.chunk_base = chunk_base;
+            h.chunk_left = chunk_left;
+            h.run_first = run_first;
+            h.run_contig = run_contig ? 1u : 0u;
+            h.done = 0;
+            h.pad = 0;
+            hand[si] = h;
+        }
+    };
+    // the stripe is done here (exit: the first record start at or after its end, NONE when none starts in it)
+    auto finish = [&](uint64_t exit) {
+        if (lane == 0) {
+            StripeRes r;
+            r.entry = stripe_entry;
+            r.exit = stripe_entry == NONE ? NONE : exit;
+            r.err_pos = NONE;
+            r.err_aux = 0;
+            r.err_kind = 0;
+            r.count = total;
+            r.forced = 0;
+            r.owned = 0;
+            r.pool_run = run_contig && run_first != N32 ? (uint64_t)run_first : NONE;
+            r.pad = 0;
+            sres[si] = r;
+            if (scnt) scnt[si] = total;
+            PieceHand h = {};
+            h.done = 1;
+            hand[si] = h;
+        }
+    };
+    if (entry == NONE) {   // no record starts in the stripe (or the search ran past its tiles)
+        for (uint32_t t = sd.t_begin + (uint32_t)lane; t < sd.t_end; t += 64u) {
+            TileRes tr;
+            tr.pool_off = 0; tr.pool_off2 = 0; tr.count = 0; tr.count1 = 0;
+            tres[sg.tile0 + t] = tr;
+        }
+        finish(NONE);
+        return;
+    }
+    // ---- the prediction: the record at the entry
+    const uint64_t Pe = entry;
+    uint32_t ku = 0, vu = 0;
+    bool uni = false;
+    if (Pe < s_hi && Pe + 9u <= len) {
+        const __amdgpu_buffer_rsrc_t rs0 = seg_rsrc(sg.base, Pe, len);
+        const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs0, 0, 0, 0);
+        ku = (a.x >> 8) | (a.y << 24);
+        if ((a.x & 255u) == 0u && ku <= 4u * UKEYW && Pe + 9u + ku <= len) {
+            vu = __builtin_amdgcn_raw_buffer_load_b32(rs0, 5 + (int)ku, 0, 0);   // (unaligned)
+            uni = vu >= (uint32_t)KVR_UMIN && vu <= UMAXV && Pe + 9u + ku + vu <= len;
+        }
+        ku = uni32(ku);
+        vu = uni32(vu);
+        uni = __builtin_amdgcn_readfirstlane(uni ? 1 : 0) != 0;
+    }
+    const uint32_t L = 9u + ku + vu;
+    const uint32_t P = (vu + (uint32_t)SC - 1u) >> SC_LOG, r = vu - (uint32_t)SC * (P - 1u);
+    // (a first piece's window starts 128 - r bytes before its value: inside the segment)
+    if (!uni || Pe + 9u + ku + r < (uint64_t)SC || !KVR_UMODE) {
+        for (uint32_t t = sd.t_begin + (uint32_t)lane; t < k; t += 64u) {   // the tiles the search passed
+            TileRes tr;
+            tr.pool_off = 0; tr.pool_off2 = 0; tr.count = 0; tr.count1 = 0;
+            tres[sg.tile0 + t] = tr;
+        }
+        hand_back(Pe, k, 0u, 0u);
+        return;
+    }
+    // ---- the run
+    const uint32_t q_end = (uint32_t)((s_hi - Pe + L - 1u) / L);   // records starting in the stripe (Pe < s_hi)
+    const uint64_t q_fit64 = (len - Pe) / L;                         // records ending inside the segment
+    const uint32_t q_fit = q_fit64 > (uint64_t)q_end ? q_end : (uint32_t)q_fit64;
+    const int32_t G = (int32_t)L - (int32_t)((uint32_t)SC * P);   // window offset per record beyond 128 P
+    const uint32_t IXr = S.IX[r];                                   // ~0 * x^(8 r)
+    const float invP = 1.0f / (float)P;
+    const uint32_t adv_q = 64u / P, adv_p = 64u % P;                // a step: 64 = adv_q P + adv_p pieces
+    const uint32_t zr = (uint32_t)SC - r;                           // masked leading bytes of a first piece
+    // TileRes: tiles [t_done, ...) not yet written; the open run of slots (one chunk) starts at tile
+    // seg_tile, slot seg_b, seg_n records
+    uint32_t t_done = sd.t_begin, seg_tile = tile_of(Pe), seg_b = 0, seg_n = 0;
+    auto close_tiles = [&](uint32_t t_to, uint32_t n_seg) {   // [t_done, t_to): the run at seg_tile, else empty
+        for (uint32_t t = t_done + (uint32_t)lane; t < t_to; t += 64u) {
+            const bool st = t == seg_tile && n_seg != 0u;
+            TileRes tr;
+            tr.pool_off = st ? (uint64_t)seg_b : 0ull;
+            tr.pool_off2 = 0;
+            tr.count = st ? n_seg : 0u;
+            tr.count1 = tr.count;
+            tres[sg.tile0 + t] = tr;
+        }
+    };
+    // the group: records qg .. in lanes 0 .. (their header windows and value CRCs)
+    uint32_t qg = 0, vcrc = 0;
+    bool early = true;   // the first completed records are verified at once: a stripe that is not uniform
+    uint32_t win[12];    // hands back after one step's work
+#pragma unroll
+    for (int i = 0; i < 12; ++i) win[i] = 0u;
+    __amdgpu_buffer_rsrc_t grs = seg_rsrc(sg.base, Pe, len);
+    bool ustop = false;
+    // verify and emit the group's first n records; a record not as predicted stops the run there
+    auto flush = [&](uint32_t n) {
+        const uint64_t GB = Pe + (uint64_t)qg * L;
+        const bool on = (uint32_t)lane < n;
+        const uint32_t op = win[0] & 255u, klen = (win[0] >> 8) | (win[1] << 24);
+        uint32_t vl;
+        {   // the value length at byte 5 + ku of the window
+            const uint32_t t = 5u + ku, tw = t >> 2;
+            uint32_t a = 0, b = 0;
+#pragma unroll
+            for (int i = 0; i < 11; ++i)
+                if (tw == (uint32_t)i) { a = win[i]; b = win[i + 1]; }
+            vl = __builtin_amdgcn_alignbyte(b, a, t & 3u);
+        }
+        // the key CRC from the window; a key with a byte >= 0x80 stops the run (k_replay runs the
+        // full UTF-8 check, engine.rs:114)
+        uint32_t kr[UKEYW + 1];
+#pragma unroll
+        for (int i = 0; i <= UKEYW; ++i) kr[i] = win[i + 1];
+        uint32_t bad = 0;
+        const uint32_t kc = crc_words_u<UKEYW>(kr, K, 1u, ku, &bad);
+        const bool ok = on && op == 0u && klen == ku && vl == vu && bad == 0u && qg + (uint32_t)lane < q_fit;
+        const uint64_t bm = __ballot(on && !ok);
+        const uint32_t f = bm ? (uint32_t)__builtin_ctzll(bm) : n;
+        // slots from the wave's chunk; a fresh chunk only where a tile starts, so that every tile's
+        // records stay one run (k_replay takes a handed-back tile's from chunk_base back)
+        uint32_t m = f < chunk_left ? f : chunk_left;
+        if (m < f && chunk_left == 0u && (qg == 0u || tile_of(GB) != tile_of(GB - L))) {
+            const uint32_t tq = tile_of(GB);
+            close_tiles(tq, seg_n);
+            const uint32_t cmx = pool_chunk > TILE_RECS ? pool_chunk : TILE_RECS;
+            unsigned long long bb = 0;
+            if (lane == 0) {
+                bb = atomicAdd(&ctr->pool_cursor, (unsigned long long)cmx);
+                if (bb + cmx > pool_cap) {   // past the pool: flag it, write into the slack
+                    atomicOr(&ctr->overflow, 1u);
+                    bb = pool_cap;
+                }
+            }
+            chunk_base = uni32((uint32_t)bb);
+            chunk_left = cmx;
+            if (run_first != N32) run_contig = false;
+            t_done = tq;
+            seg_tile = tq;
+            seg_b = chunk_base;
+            seg_n = 0;
+            m = f;
+        }
+        if (m != 0u && run_first == N32) run_first = chunk_base;
+        if ((uint32_t)lane < m) {
+            kvr_tuple t;
+            t.rec_off = GB + (uint64_t)lane * L;
+            t.seg_idx = sd.seg;
+            t.key_len = ku;
+            t.val_len = vu;
+            t.crc32 = vcrc;
+            t.key_tag = ~kc;
+            t.op = 0;
+            t.flags = 0;
+            t.reserved = 0;
+            pool[chunk_base + (uint32_t)lane] = t;
+            if (kpool) kpool[chunk_base + (uint32_t)lane] = key_prefix_words(&win[1], 1u, ku);
+        }
+        chunk_base += m;
+        chunk_left -= m;
+        seg_n += m;
+        qg += m;
+        if (m < n) ustop = true;
+        grs = seg_rsrc(sg.base, Pe + (uint64_t)qg * L, len);
+    };
+    // the steps, lane 0 at piece p_s of record q_s; step s + 1's pieces are loaded before step s is
+    // processed (two piece buffers)
+    struct Geo {
+        uint32_t dq, pv;
+        int32_t o;
+        bool act;
+    };
+    auto geo = [&](uint32_t q_s, uint32_t p_s) -> Geo {
+        Geo g;
+        const uint32_t gr = p_s + (uint32_t)lane;
+        g.dq = P > 64u ? (gr >= P ? 1u : 0u) : (uint32_t)(((float)gr + 0.5f) * invP);
+        g.pv = gr - g.dq * P;
+        g.act = g.dq < q_end - q_s;
+        g.o = g.act ? lane * SC + (int32_t)g.dq * G : 0x7FFFFF00;
+        return g;
+    };
+    auto issue = [&](uint32_t (&x)[UW], uint32_t q_s, uint32_t p_s, const Geo &g) {
+        const uint64_t B = Pe + (uint64_t)q_s * L + 9u + ku + r - (uint64_t)SC + (uint64_t)SC * p_s;
+        load_piece(seg_rsrc(sg.base, B, len), g.o, x);
+    };
+    bool cont = false;
+    uint32_t creg = 0;
+    // a step's piece CRC (raw, from 0), with the first pieces' initial register and the value carried in
+    auto crc_step = [&](uint32_t (&x)[UW], const Geo &g) -> uint32_t {
+        const bool first = g.act && g.pv == 0u;
+        if (zr != 0u && __ballot(first)) mask_lead(x, first, zr);
+        uint32_t raw = piece_raw(x, K, S);
+        raw ^= first ? IXr : 0u;
+        if (cont) {   // lane 0 continues the value lane 63 carried out of the last step
+            const uint32_t cx = kmul(creg, S.KQ2 + 128);
+            raw ^= lane == 0 ? cx : 0u;
+        }
+        return raw;
+    };
+    // the step's push, scan and results; false: the run stops (a record not as predicted)
+    auto finish_step = [&](uint32_t raw, uint32_t q_s, uint32_t p_s, const Geo &g) -> bool {
+        const bool first = g.act && g.pv == 0u;
+        const bool comp = g.act && g.pv == P - 1u;
+        const uint32_t dl = P - 1u - g.pv, dr = 63u - (uint32_t)lane;
+        const uint32_t dd = g.act ? (dl < dr ? dl : dr) : 0u;
+        const uint32_t pushed = kmul_col<KR_OFF, KR_PITCH>(dd ? raw : 0u, S, dd ? 4u * (dd - 1u) : 0u);
+        const uint32_t v = seg_xscan(dd ? pushed : raw, first ? N32 : 0u);
+        cont = ((__ballot(g.act && !comp) >> 63) & 1ull) != 0ull;
+        creg = rl32(v, 63);
+        const uint64_t cmk = __ballot(comp);
+        if (cmk) {   // records [qa, qb) complete in this step
+            const uint32_t qa = q_s + rl32(g.dq, (int)__builtin_ctzll(cmk));
+            const uint32_t qb = q_s + rl32(g.dq, 63 - (int)__builtin_clzll(cmk)) + 1u;
+            if (qb - qg > 64u) {   // the group is full: its records (all before qa) first
+                flush(qa - qg);
+                if (ustop) return false;
+            }
+            const uint32_t qj = qg + (uint32_t)lane;
+            const bool in = qj >= qa && qj < qb;
+            const int32_t src = (int32_t)((qj - q_s) * P + (P - 1u) - p_s);
+            const uint32_t cv = (uint32_t)__builtin_amdgcn_ds_bpermute(in ? 4 * src : 0, (int)~v);
+            vcrc = in ? cv : vcrc;
+            if (in) {
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(grs, lane * (int32_t)L + 16 * i, 0, 0);
+                    win[4 * i] = a.x; win[4 * i + 1] = a.y; win[4 * i + 2] = a.z; win[4 * i + 3] = a.w;
+                }
+            }
+            if (early) {   // (waits for these windows once)
+                early = false;
+                flush(qb - qg);
+                if (ustop) return false;
+            }
+        }
+        return true;
+    };
+    uint32_t q0 = 0, p0 = 0;
+    Geo g0 = geo(q0, p0);
+    issue(w, q0, p0, g0);
+#if KVR_PDB
+    // two piece buffers: step s + 1's pieces are loaded before step s is processed
+    uint32_t wb[UW];
+#pragma unroll 1
+    for (;;) {
+        uint32_t q1 = q0 + adv_q, p1 = p0 + adv_p;
+        if (p1 >= P) { p1 -= P; ++q1; }
+        const bool h1 = q1 < q_end;
+        Geo g1 = g0;
+        if (h1) { g1 = geo(q1, p1); issue(wb, q1, p1, g1); }
+        if (!finish_step(crc_step(w, g0), q0, p0, g0) || !h1) break;
+        uint32_t q2 = q1 + adv_q, p2 = p1 + adv_p;
+        if (p2 >= P) { p2 -= P; ++q2; }
+        const bool h2 = q2 < q_end;
+        Geo g2 = g1;
+        if (h2) { g2 = geo(q2, p2); issue(w, q2, p2, g2); }
+        if (!finish_step(crc_step(wb, g1), q1, p1, g1) || !h2) break;
+        q0 = q2; p0 = p2; g0 = g2;
+    }
+#else
+    // one piece buffer: the next step's pieces are loaded as soon as the CRC has read this step's
+#pragma unroll 1
+    for (;;) {
+        const uint32_t raw = crc_step(w, g0);
+        uint32_t q1 = q0 + adv_q, p1 = p0 + adv_p;
+        if (p1 >= P) { p1 -= P; ++q1; }
+        const bool h1 = q1 < q_end;
+        Geo g1 = g0;
+        if (h1) { g1 = geo(q1, p1); issue(w, q1, p1, g1); }
+        if (!finish_step(raw, q0, p0, g0) || !h1) break;
+        q0 = q1; p0 = p1; g0 = g1;
+    }
+#endif
+    if (!ustop && qg < q_end) flush(q_end - qg);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (a prefetched step the stop left unused)
+    if (!ustop) {
+        close_tiles(sd.t_end, seg_n);
+        total += qg;
+        finish(Pe + (uint64_t)q_end * L);
+        return;
+    }
+    // hand back at record qg: its tile's records emitted here are `ah`, the last slots claimed
+    const uint32_t k_res = tile_of(Pe + (uint64_t)qg * L);
+    const int64_t lt = (int64_t)k_res * TILE - d0;   // the resumed tile's start
+    const uint32_t qt = lt <= (int64_t)Pe ? 0u : (uint32_t)(((uint64_t)lt - Pe + L - 1u) / L);
+    const uint32_t ah = qg - qt;
+    close_tiles(k_res, seg_n - (seg_tile < k_res ? ah : seg_n));
+    total += qg - ah;
+    hand_back(Pe + (uint64_t)qg * L, k_res, ah, L);
 }
 
 }  // namespace kvr

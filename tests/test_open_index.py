@@ -551,7 +551,8 @@ def test_kvs_open_more_segments_than_descriptors(gctx, tmp_path):
 @pytest.mark.parametrize("flags", [0, K.OPEN_PREAD, K.OPEN_PREAD | K.OPEN_NO_PIN])
 def test_kvs_open_vanished_segment(gctx, tmp_path, monkeypatch, flags):
     """A segment file that disappears between discovery and the read (engine.rs:80-83 would fail
-    its open): kvs_open_ex answers KVR_EIO after the segments pushed before it were queued for DMA,
+    its open; the knob swaps in a path that does not exist, it deletes nothing): kvs_open_ex
+    answers KVR_EIO after the segments pushed before it were queued for DMA,
     and it waits for those copies (kvr_ingest_abort) before it unmaps the host bytes they read.
     The context stays usable: the same store opens cleanly once the knob is off."""
     spec = K.GenSpec(seed=108, seg_bytes=8 << 20, key_space_log2=14, val_min=0, val_max=2000, del_permille=100)
@@ -563,9 +564,8 @@ def test_kvs_open_vanished_segment(gctx, tmp_path, monkeypatch, flags):
     monkeypatch.setenv("KVS_TEST_VANISH", "5")
     with pytest.raises(K.NativeError, match=str(K.EIO)):
         K.KVStore.open(str(d), gctx, flags=flags)
-    assert not (d / "segment-6.dat").exists()
+    assert (d / "segment-6.dat").read_bytes() == keep   # (the knob never deletes a file)
     monkeypatch.delenv("KVS_TEST_VANISH")
-    (d / "segment-6.dat").write_bytes(keep)
     for f in d.glob("segment-9.dat"):
         f.unlink()
     want, nk, tb = expect(segs, ids)
