@@ -794,23 +794,21 @@ __device__ __forceinline__ void load_piece(__amdgpu_buffer_rsrc_t rs, int o, uin
         w[4 * i] = a.x; w[4 * i + 1] = a.y; w[4 * i + 2] = a.z; w[4 * i + 3] = a.w;
     }
 }
-// zero the first zb (wave-uniform, < SC) bytes of the piece on lanes with `on` (a value's first
-// piece: the bytes before the value start; leading zeros leave a CRC register of 0 unchanged)
-__device__ __forceinline__ void mask_lead(uint32_t (&w)[UW], bool on, uint32_t zb) {
-    const uint32_t zw = zb >> 2, part = on ? ~0u << (8u * (zb & 3u)) : ~0u;
-#pragma unroll
-    for (int i = 0; i < UW; ++i) {
-        if ((uint32_t)i < zw) w[i] = on ? 0u : w[i];
-        else if ((uint32_t)i == zw) w[i] &= part;
-    }
-}
 // the raw CRC register (from 0) of the lane's 128 B: two slice-by-4 chains over words 0-15 and
-// 16-31 (no value boundary inside), the first pushed through the second's 64 bytes
-__device__ __forceinline__ uint32_t piece_raw(const uint32_t (&w)[UW], const Crc &K, const Smem &S) {
+// 16-31 (no value boundary inside), the first pushed through the second's 64 bytes.  On lanes with
+// `on` (a value's first piece) the bytes before byte zb (wave-uniform, < SC) are not part of the value:
+// leading zeros leave a register of 0 unchanged, so such a lane restarts its chain at word zb / 4 with
+// that word's leading bytes masked (the uniform step index makes the restart one select), and the
+// chain over words 0-15 contributes nothing when the restart is in the second half.
+__device__ __forceinline__ uint32_t piece_raw(const uint32_t (&w)[UW], const Crc &K, const Smem &S, bool on,
+                                              uint32_t zb) {
     constexpr int H = UW / 2;
+    const uint32_t zw = zb >> 2, pm = ~0u << (8u * (zb & 3u));
     uint32_t xa = w[0], xb = w[H], ca = 0, cb = 0;
 #pragma unroll
     for (int kk = 0; kk < H; ++kk) {
+        if (zb != 0u && zw == (uint32_t)kk) xa = on ? (w[kk] & pm) : xa;
+        if (zb != 0u && zw == (uint32_t)(kk + H)) xb = on ? (w[kk + H] & pm) : xb;
         uint32_t ta, a3, tb, b3;
         look4x2(xa, xb, K, ta, a3, tb, b3);
         if (kk + 1 < H) {
@@ -821,6 +819,7 @@ __device__ __forceinline__ uint32_t piece_raw(const uint32_t (&w)[UW], const Crc
             cb = tb ^ b3;
         }
     }
+    if (zw >= (uint32_t)H) ca = on ? 0u : ca;
     return kmul(ca, S.KQ2) ^ cb;
 }
 // segmented inclusive XOR scan over the lanes (DPP only): fm all ones starts a segment
@@ -2146,8 +2145,8 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     // a step's piece CRC (raw, from 0), with the first pieces' initial register and the value carried in
     auto crc_step = [&](uint32_t (&x)[UW], const Geo &g) -> uint32_t {
         const bool first = g.act && g.pv == 0u;
-        if (zr != 0u && __ballot(first)) mask_lead(x, first, zr);
-        uint32_t raw = piece_raw(x, K, S);
+        // (values of whole pieces, the benchmark shapes: the chains with no restart)
+        uint32_t raw = zr == 0u ? piece_raw(x, K, S, false, 0u) : piece_raw(x, K, S, first, zr);
         raw ^= first ? IXr : 0u;
         if (cont) {   // lane 0 continues the value lane 63 carried out of the last step
             const uint32_t cx = kmul(creg, S.KQ2 + 128);
