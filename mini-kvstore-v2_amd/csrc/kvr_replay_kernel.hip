@@ -785,14 +785,24 @@ __device__ __forceinline__ TileSeg tile_seg(const uint8_t *abase, const uint8_t 
 // ---------------------------------------------------------------------------------------
 // the piece mode (uniform_run in replay_body)
 // ---------------------------------------------------------------------------------------
-// a lane's 128-B piece at byte offset o of the resource (any alignment: byte-unaligned 16-B buffer
-// loads; offsets past the resource read 0)
-__device__ __forceinline__ void load_piece(__amdgpu_buffer_rsrc_t rs, int o, uint32_t (&w)[UW]) {
+// a lane's 128-B piece at byte offset o of the resource: 16-B loads from the dword that holds its
+// first byte, and the dword after them (byte-unaligned 16-B loads run at half the rate: tools/
+// piece_probe.hip); piece_align shifts the words into place once they have landed.  Offsets past the
+// resource read 0.
+__device__ __forceinline__ void load_piece(__amdgpu_buffer_rsrc_t rs, int o, uint32_t (&w)[UW + 1]) {
+    const int a = o & ~3;
 #pragma unroll
     for (int i = 0; i < UW / 4; ++i) {
-        const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16 * i, 0, 0);
-        w[4 * i] = a.x; w[4 * i + 1] = a.y; w[4 * i + 2] = a.z; w[4 * i + 3] = a.w;
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, a + 16 * i, 0, 0);
+        w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
     }
+    w[UW] = __builtin_amdgcn_raw_buffer_load_b32(rs, a + 4 * UW, 0, 0);
+}
+__device__ __forceinline__ void piece_align(uint32_t (&w)[UW + 1], int o) {
+    const uint32_t sh = (uint32_t)o & 3u;
+    if (__ballot(sh != 0u) == 0ull) return;   // (every lane's piece starts on a dword)
+#pragma unroll
+    for (int i = 0; i < UW; ++i) w[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
 }
 // the raw CRC register (from 0) of the lane's 128 B: two slice-by-4 chains over words 0-15 and
 // 16-31 (no value boundary inside), the first pushed through the second's 64 bytes.  On lanes with
@@ -800,7 +810,7 @@ __device__ __forceinline__ void load_piece(__amdgpu_buffer_rsrc_t rs, int o, uin
 // leading zeros leave a register of 0 unchanged, so such a lane restarts its chain at word zb / 4 with
 // that word's leading bytes masked (the uniform step index makes the restart one select), and the
 // chain over words 0-15 contributes nothing when the restart is in the second half.
-__device__ __forceinline__ uint32_t piece_raw(const uint32_t (&w)[UW], const Crc &K, const Smem &S, bool on,
+__device__ __forceinline__ uint32_t piece_raw(const uint32_t (&w)[UW + 1], const Crc &K, const Smem &S, bool on,
                                               uint32_t zb) {
     constexpr int H = UW / 2;
     const uint32_t zw = zb >> 2, pm = ~0u << (8u * (zb & 3u));
@@ -840,6 +850,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t seg_rsrc(const uint8_t *seg, u
     const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)b), bhi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
     return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)bhi << 32) | blo), (short)0,
                                              __builtin_amdgcn_readfirstlane(nr), 0x00020000);
+}
+// the same over the dwords that hold segment bytes [pos, len): byte pos is at offset adj (0 .. 3) of
+// the resource, so that an offset o + adj with o a multiple of 4 from pos is a dword-aligned address,
+// and the dword holding byte len - 1 is read whole (the range check is per dword: a dword that
+// crosses the end would read 0; its bytes past len are never used)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t seg_rsrc_a(const uint8_t *seg, uint64_t pos, uint64_t len,
+                                                             uint32_t &adj) {
+    adj = (uint32_t)((uint64_t)(seg + pos) & 3u);
+    const uint64_t end = ((uint64_t)(seg + len) + 3u) & ~3ull;   // (the dword holding byte len - 1 ends here)
+    return seg_rsrc(seg, pos - adj, end - (uint64_t)seg);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1919,7 +1939,7 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     const int64_t shi_i = (int64_t)sd.t_end * TILE - d0;
     const uint64_t s_hi = (uint64_t)shi_i > len ? len : (uint64_t)shi_i;
     const uint8_t *abase = sg.base - d0;
-    uint32_t w[UW];
+    uint32_t w[UW + 1];
     // ---- the entry: offset 0 for a segment's first stripe, else the first plausible record start
     uint64_t entry = sd.t_begin == 0 ? 0ull : NONE;
     uint32_t k = sd.t_begin;
@@ -1932,7 +1952,7 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
             const int64_t vhi_r = (lo + TILE > (int64_t)len ? (int64_t)len : lo + TILE) - lo;
             const int us = lane * SC, ue = us + SC;
             const TileSeg ts = tile_seg(abase, sg.base, d0, len, k);
-            entry = find_entry(w, ts, lo, (int64_t)len - lo, us > (int)vlo_r ? us : (int)vlo_r,
+            entry = find_entry(*reinterpret_cast<uint32_t(*)[UW]>(w), ts, lo, (int64_t)len - lo, us > (int)vlo_r ? us : (int)vlo_r,
                                ue < (int)vhi_r ? ue : (int)vhi_r, lane);
             if (entry != NONE) break;
         }
@@ -2045,30 +2065,34 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     // the group: records qg .. in lanes 0 .. (their header windows and value CRCs)
     uint32_t qg = 0, vcrc = 0;
     bool early = true;   // the first completed records are verified at once: a stripe that is not uniform
-    uint32_t win[12];    // hands back after one step's work
-#pragma unroll
-    for (int i = 0; i < 12; ++i) win[i] = 0u;
-    __amdgpu_buffer_rsrc_t grs = seg_rsrc(sg.base, Pe, len);
+    uint32_t win[13], wsh = 0;   // hands back after one step's work.  (A record's window: the 13 dwords
+#pragma unroll                 // from the one holding its first byte, wsh bytes in.)
+    for (int i = 0; i < 13; ++i) win[i] = 0u;
+    uint32_t gadj;
+    __amdgpu_buffer_rsrc_t grs = seg_rsrc_a(sg.base, Pe, len, gadj);
     bool ustop = false;
     // verify and emit the group's first n records; a record not as predicted stops the run there
     auto flush = [&](uint32_t n) {
         const uint64_t GB = Pe + (uint64_t)qg * L;
         const bool on = (uint32_t)lane < n;
-        const uint32_t op = win[0] & 255u, klen = (win[0] >> 8) | (win[1] << 24);
+        uint32_t x[12];   // the record's first 48 bytes
+#pragma unroll
+        for (int i = 0; i < 12; ++i) x[i] = __builtin_amdgcn_alignbyte(win[i + 1], win[i], wsh);
+        const uint32_t op = x[0] & 255u, klen = (x[0] >> 8) | (x[1] << 24);
         uint32_t vl;
         {   // the value length at byte 5 + ku of the window
             const uint32_t t = 5u + ku, tw = t >> 2;
             uint32_t a = 0, b = 0;
 #pragma unroll
             for (int i = 0; i < 11; ++i)
-                if (tw == (uint32_t)i) { a = win[i]; b = win[i + 1]; }
+                if (tw == (uint32_t)i) { a = x[i]; b = x[i + 1]; }
             vl = __builtin_amdgcn_alignbyte(b, a, t & 3u);
         }
         // the key CRC from the window; a key with a byte >= 0x80 stops the run (k_replay runs the
         // full UTF-8 check, engine.rs:114)
         uint32_t kr[UKEYW + 1];
 #pragma unroll
-        for (int i = 0; i <= UKEYW; ++i) kr[i] = win[i + 1];
+        for (int i = 0; i <= UKEYW; ++i) kr[i] = x[i + 1];
         uint32_t bad = 0;
         const uint32_t kc = crc_words_u<UKEYW>(kr, K, 1u, ku, &bad);
         const bool ok = on && op == 0u && klen == ku && vl == vu && bad == 0u && qg + (uint32_t)lane < q_fit;
@@ -2111,39 +2135,44 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
             t.flags = 0;
             t.reserved = 0;
             pool[chunk_base + (uint32_t)lane] = t;
-            if (kpool) kpool[chunk_base + (uint32_t)lane] = key_prefix_words(&win[1], 1u, ku);
+            if (kpool) kpool[chunk_base + (uint32_t)lane] = key_prefix_words(&x[1], 1u, ku);
         }
         chunk_base += m;
         chunk_left -= m;
         seg_n += m;
         qg += m;
         if (m < n) ustop = true;
-        grs = seg_rsrc(sg.base, Pe + (uint64_t)qg * L, len);
+        grs = seg_rsrc_a(sg.base, Pe + (uint64_t)qg * L, len, gadj);
     };
     // the steps, lane 0 at piece p_s of record q_s; step s + 1's pieces are loaded before step s is
     // processed (two piece buffers)
     struct Geo {
+        uint64_t B;       // lane 0's window start (uniform); the resource starts at the dword holding it
         uint32_t dq, pv;
-        int32_t o;
+        int32_t o;        // this lane's window in the resource (its byte offset, adj included)
         bool act;
     };
     auto geo = [&](uint32_t q_s, uint32_t p_s) -> Geo {
         Geo g;
+        g.B = Pe + (uint64_t)q_s * L + 9u + ku + r - (uint64_t)SC + (uint64_t)SC * p_s;
+        const uint32_t adj = (uint32_t)((uint64_t)(sg.base + g.B) & 3u);
         const uint32_t gr = p_s + (uint32_t)lane;
         g.dq = P > 64u ? (gr >= P ? 1u : 0u) : (uint32_t)(((float)gr + 0.5f) * invP);
         g.pv = gr - g.dq * P;
         g.act = g.dq < q_end - q_s;
-        g.o = g.act ? lane * SC + (int32_t)g.dq * G : 0x7FFFFF00;
+        g.o = g.act ? lane * SC + (int32_t)g.dq * G + (int32_t)adj : 0x7FFFFF00;
         return g;
     };
-    auto issue = [&](uint32_t (&x)[UW], uint32_t q_s, uint32_t p_s, const Geo &g) {
-        const uint64_t B = Pe + (uint64_t)q_s * L + 9u + ku + r - (uint64_t)SC + (uint64_t)SC * p_s;
-        load_piece(seg_rsrc(sg.base, B, len), g.o, x);
+    auto issue = [&](uint32_t (&x)[UW + 1], uint32_t q_s, uint32_t p_s, const Geo &g) {
+        uint32_t adj;
+        const __amdgpu_buffer_rsrc_t rs = seg_rsrc_a(sg.base, g.B, len, adj);
+        load_piece(rs, g.o, x);
     };
     bool cont = false;
     uint32_t creg = 0;
     // a step's piece CRC (raw, from 0), with the first pieces' initial register and the value carried in
-    auto crc_step = [&](uint32_t (&x)[UW], const Geo &g) -> uint32_t {
+    auto crc_step = [&](uint32_t (&x)[UW + 1], const Geo &g) -> uint32_t {
+        piece_align(x, g.o);
         const bool first = g.act && g.pv == 0u;
         // (values of whole pieces, the benchmark shapes: the chains with no restart)
         uint32_t raw = zr == 0u ? piece_raw(x, K, S, false, 0u) : piece_raw(x, K, S, first, zr);
@@ -2178,11 +2207,14 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
             const uint32_t cv = (uint32_t)__builtin_amdgcn_ds_bpermute(in ? 4 * src : 0, (int)~v);
             vcrc = in ? cv : vcrc;
             if (in) {
+                const int32_t wo = lane * (int32_t)L + (int32_t)gadj, wa = wo & ~3;
+                wsh = (uint32_t)wo & 3u;
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
-                    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(grs, lane * (int32_t)L + 16 * i, 0, 0);
+                    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(grs, wa + 16 * i, 0, 0);
                     win[4 * i] = a.x; win[4 * i + 1] = a.y; win[4 * i + 2] = a.z; win[4 * i + 3] = a.w;
                 }
+                win[12] = __builtin_amdgcn_raw_buffer_load_b32(grs, wa + 48, 0, 0);
             }
             if (early) {   // (waits for these windows once)
                 early = false;
@@ -2197,7 +2229,7 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     issue(w, q0, p0, g0);
 #if KVR_PDB
     // two piece buffers: step s + 1's pieces are loaded before step s is processed
-    uint32_t wb[UW];
+    uint32_t wb[UW + 1];
 #pragma unroll 1
     for (;;) {
         uint32_t q1 = q0 + adv_q, p1 = p0 + adv_p;
