@@ -74,6 +74,7 @@ constexpr int KQL_PITCH = KVR_KQLPAD ? KR_PITCH : 64;
 struct __align__(16) Smem {
     uint32_t KQ2[2 * 8 * 16];             // [h][i][n]: (n << 4i) * x^(8*4q), q = SC/8 (h 0), SC/4 (h 1): the two
                                           // lane-uniform pushes of the finalize
+    uint32_t KQ4[2 * 8 * 16];             // the same for x^(8*32) (h 0) and x^(8*96) (h 1): k_piece's 4-chain combine
     uint32_t IX[NIX + 3];                 // 0xFFFFFFFF * x^(8j): initial register pushed through j bytes
     uint32_t MK[NWAVE][64];               // per wave: long-value marks by unit (framing)
     uint32_t C2[256 * 64];                // byte tables, row b = 256 B (64 KiB), see Crc
@@ -108,8 +109,11 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #ifndef KVR_UMODE   // 1: runs of SETs of one key and one value length go through the piece mode (uniform_run)
 #define KVR_UMODE 1
 #endif
-#ifndef KVR_PDB     // 1: k_piece loads step s + 1 before it processes step s (two piece buffers)
-#define KVR_PDB 0
+#ifndef KVR_PCHAINS   // k_piece's CRC chains per piece: 2 (16 words each) or 4 (8 words each)
+#define KVR_PCHAINS 2
+#endif
+#ifndef KVR_PABLATE   // diagnostic builds of k_piece only (results wrong): 1 no CRC, 2 no push + scan, 8 no
+#define KVR_PABLATE 0   // realignment
 #endif
 #ifndef KVR_UMIN    // the shortest value the piece mode takes (pieces are 128 B: shorter values waste lanes)
 #define KVR_UMIN 128
@@ -832,6 +836,27 @@ __device__ __forceinline__ uint32_t piece_raw(const uint32_t (&w)[UW + 1], const
     if (zw >= (uint32_t)H) ca = on ? 0u : ca;
     return kmul(ca, S.KQ2) ^ cb;
 }
+// piece_raw with four chains of eight words (half the dependent LDS steps of two chains of sixteen),
+// combined as c0 x^(8*96) ^ c1 x^(8*64) ^ c2 x^(8*32) ^ c3
+__device__ __forceinline__ uint32_t piece_raw4(const uint32_t (&w)[UW + 1], const Crc &K, const Smem &S) {
+    constexpr int Q = UW / 4;
+    uint32_t x0 = w[0], x1 = w[Q], x2 = w[2 * Q], x3 = w[3 * Q], c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#pragma unroll
+    for (int kk = 0; kk < Q; ++kk) {
+        uint32_t t0, a0, t1, a1, t2, a2, t3, a3;
+        look4x2(x0, x1, K, t0, a0, t1, a1);
+        look4x2(x2, x3, K, t2, a2, t3, a3);
+        if (kk + 1 < Q) {
+            x0 = xor3(t0, a0, w[kk + 1]);
+            x1 = xor3(t1, a1, w[kk + 1 + Q]);
+            x2 = xor3(t2, a2, w[kk + 1 + 2 * Q]);
+            x3 = xor3(t3, a3, w[kk + 1 + 3 * Q]);
+        } else {
+            c0 = t0 ^ a0; c1 = t1 ^ a1; c2 = t2 ^ a2; c3 = t3 ^ a3;
+        }
+    }
+    return xor3(kmul(c0, S.KQ4 + 128), kmul(c1, S.KQ2), kmul(c2, S.KQ4)) ^ c3;
+}
 // segmented inclusive XOR scan over the lanes (DPP only): fm all ones starts a segment
 __device__ __forceinline__ uint32_t seg_xscan(uint32_t v, uint32_t fm) {
     uint32_t ov;
@@ -910,6 +935,7 @@ __device__ __forceinline__ void stage_tables(Smem &S, const Tables &tb, int tid)
         S.KQL[i] = q < NQ ? tb.kmul[((KSET_Q + q) * 8 + (row >> 4)) * 16 + (row & 15)] : 0u;
     }
     for (int i = tid; i < 2 * 8 * 16; i += RT) S.KQ2[i] = tb.kmul[(KSET_Q + (i < 128 ? SC / 8 : SC / 4)) * 8 * 16 + (i & 127)];
+    for (int i = tid; i < 2 * 8 * 16; i += RT) S.KQ4[i] = tb.kmul[(KSET_Q + (i < 128 ? SC / 16 : 3 * SC / 16)) * 8 * 16 + (i & 127)];
     if (tid < NIX) S.IX[tid] = tb.initx[tid];
 }
 
@@ -1932,6 +1958,27 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     crc_init(K, S.C2, (uint32_t)lane);
     const uint32_t si = blockIdx.x * WPB + (uint32_t)__builtin_amdgcn_readfirstlane(wv);
     if (si >= n_stripes) return;
+#ifdef KVR_PROF
+    // (diagnostic build: cycles per phase into g_prof 0-5, counts in 6-7; tools/prof_phases.py piece)
+    unsigned long long pt_last = __builtin_amdgcn_s_memtime();
+    unsigned long long pacc[8] = {};
+#define KVR_PSTAMP(i)                                                       \
+    do {                                                                    \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();         \
+        pacc[i] += t_ - pt_last;                                            \
+        pt_last = t_;                                                       \
+    } while (0)
+#define KVR_PCOUNT(i) (pacc[i] += 1)
+#define KVR_PFLUSH()                                                        \
+    do {                                                                    \
+        if (lane == 0)                                                      \
+            for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_prof[i_], pacc[i_]); \
+    } while (0)
+#else
+#define KVR_PSTAMP(i) do { } while (0)
+#define KVR_PCOUNT(i) do { } while (0)
+#define KVR_PFLUSH() do { } while (0)
+#endif
     const StripeDesc sd = stripes[si];
     const SegDesc sg = segs[sd.seg];
     const uint64_t len = sg.len;
@@ -2073,6 +2120,7 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     bool ustop = false;
     // verify and emit the group's first n records; a record not as predicted stops the run there
     auto flush = [&](uint32_t n) {
+        KVR_PCOUNT(7);
         const uint64_t GB = Pe + (uint64_t)qg * L;
         const bool on = (uint32_t)lane < n;
         uint32_t x[12];   // the record's first 48 bytes
@@ -2123,18 +2171,11 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
             m = f;
         }
         if (m != 0u && run_first == N32) run_first = chunk_base;
-        if ((uint32_t)lane < m) {
-            kvr_tuple t;
-            t.rec_off = GB + (uint64_t)lane * L;
-            t.seg_idx = sd.seg;
-            t.key_len = ku;
-            t.val_len = vu;
-            t.crc32 = vcrc;
-            t.key_tag = ~kc;
-            t.op = 0;
-            t.flags = 0;
-            t.reserved = 0;
-            pool[chunk_base + (uint32_t)lane] = t;
+        if ((uint32_t)lane < m) {   // the 32-B tuple as two 16-B stores (kvr_tuple's layout: op, flags 0)
+            const uint64_t ro = GB + (uint64_t)lane * L;
+            uint4 *const tp = reinterpret_cast<uint4 *>(pool + chunk_base + (uint32_t)lane);
+            tp[0] = make_uint4((uint32_t)ro, (uint32_t)(ro >> 32), sd.seg, ku);
+            tp[1] = make_uint4(vu, vcrc, ~kc, 0u);
             if (kpool) kpool[chunk_base + (uint32_t)lane] = key_prefix_words(&x[1], 1u, ku);
         }
         chunk_base += m;
@@ -2172,10 +2213,17 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     uint32_t creg = 0;
     // a step's piece CRC (raw, from 0), with the first pieces' initial register and the value carried in
     auto crc_step = [&](uint32_t (&x)[UW + 1], const Geo &g) -> uint32_t {
-        piece_align(x, g.o);
+        if (!(KVR_PABLATE & 8)) piece_align(x, g.o);
         const bool first = g.act && g.pv == 0u;
         // (values of whole pieces, the benchmark shapes: the chains with no restart)
-        uint32_t raw = zr == 0u ? piece_raw(x, K, S, false, 0u) : piece_raw(x, K, S, first, zr);
+        uint32_t raw;
+        if (KVR_PABLATE & 1) {   // (diagnostic: no CRC; the words only kept alive)
+            raw = 0;
+#pragma unroll
+            for (int i = 0; i <= UW; ++i) raw ^= x[i];
+        } else {
+            raw = zr != 0u ? piece_raw(x, K, S, first, zr) : KVR_PCHAINS == 4 ? piece_raw4(x, K, S) : piece_raw(x, K, S, false, 0u);
+        }
         raw ^= first ? IXr : 0u;
         if (cont) {   // lane 0 continues the value lane 63 carried out of the last step
             const uint32_t cx = kmul(creg, S.KQ2 + 128);
@@ -2183,89 +2231,108 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
         }
         return raw;
     };
-    // the step's push, scan and results; false: the run stops (a record not as predicted)
-    auto finish_step = [&](uint32_t raw, uint32_t q_s, uint32_t p_s, const Geo &g) -> bool {
+    // Before a step's CRC (its pieces are in flight): the records whose values it completes, [qa, qb)
+    // (geometry only), join the group -- after a flush of the group if they would not fit, or of the
+    // run's first records (`early`) -- and their header windows are loaded, ahead of the next step's
+    // pieces (so a flush waits for windows, never for pieces just issued).  A stop (ustop) ends the loop after the step.
+    uint32_t qdone = 0;   // records whose values are complete (their windows loaded, their CRCs in vcrc)
+    // A step's windows land in wt (every lane issues the loads, those of other lanes read past the
+    // resource: no exec mask, so the wait counts stay exact) and move into win at the next step, when
+    // the next step's pieces have been issued behind them: a flush then waits for windows only.
+    uint32_t wt[13], wtsh = 0;
+    bool wpend = false;   // (per lane: wt holds this lane's record's window)
+#pragma unroll
+    for (int i = 0; i < 13; ++i) wt[i] = 0u;
+    auto merge_windows = [&]() {
+#pragma unroll
+        for (int i = 0; i < 13; ++i) win[i] = wpend ? wt[i] : win[i];
+        wsh = wpend ? wtsh : wsh;
+        wpend = false;
+    };
+    auto pre_step = [&](uint32_t q_s, const Geo &g, uint32_t &qa, uint32_t &qb) {
+        merge_windows();
+        if (early && qdone > qg) {
+            early = false;
+            flush(qdone - qg);
+        }
+        const uint64_t cmk = __ballot(g.act && g.pv == P - 1u);
+        qa = qb = 0;
+        if (cmk) {
+            qa = q_s + rl32(g.dq, (int)__builtin_ctzll(cmk));
+            qb = q_s + rl32(g.dq, 63 - (int)__builtin_clzll(cmk)) + 1u;
+            if (qb - qg > 64u && !ustop) flush(qa - qg);   // the group is full: its records (all before qa) first
+        }
+        // (issued on every step, a step that completes nothing reading nothing: a conditional load
+        // would leave the piece waits below conservative)
+        const uint32_t qj = qg + (uint32_t)lane;
+        wpend = qj >= qa && qj < qb;
+        const int32_t wo = lane * (int32_t)L + (int32_t)gadj, wa = wpend ? (wo & ~3) : 0x7FFFFF00;
+        wtsh = (uint32_t)wo & 3u;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const u32x4 v4 = __builtin_amdgcn_raw_buffer_load_b128(grs, wa + 16 * i, 0, 0);
+            wt[4 * i] = v4.x; wt[4 * i + 1] = v4.y; wt[4 * i + 2] = v4.z; wt[4 * i + 3] = v4.w;
+        }
+        wt[12] = __builtin_amdgcn_raw_buffer_load_b32(grs, wa + 48, 0, 0);
+    };
+    // the step's push, scan and value CRCs (records [qa, qb) take theirs into vcrc)
+    auto finish_step = [&](uint32_t raw, uint32_t q_s, uint32_t p_s, const Geo &g, uint32_t qa, uint32_t qb) {
         const bool first = g.act && g.pv == 0u;
         const bool comp = g.act && g.pv == P - 1u;
         const uint32_t dl = P - 1u - g.pv, dr = 63u - (uint32_t)lane;
         const uint32_t dd = g.act ? (dl < dr ? dl : dr) : 0u;
-        const uint32_t pushed = kmul_col<KR_OFF, KR_PITCH>(dd ? raw : 0u, S, dd ? 4u * (dd - 1u) : 0u);
-        const uint32_t v = seg_xscan(dd ? pushed : raw, first ? N32 : 0u);
+        uint32_t v = raw;
+        if (!(KVR_PABLATE & 2)) {
+            const uint32_t pushed = kmul_col<KR_OFF, KR_PITCH>(dd ? raw : 0u, S, dd ? 4u * (dd - 1u) : 0u);
+            v = seg_xscan(dd ? pushed : raw, first ? N32 : 0u);
+        }
         cont = ((__ballot(g.act && !comp) >> 63) & 1ull) != 0ull;
         creg = rl32(v, 63);
-        const uint64_t cmk = __ballot(comp);
-        if (cmk) {   // records [qa, qb) complete in this step
-            const uint32_t qa = q_s + rl32(g.dq, (int)__builtin_ctzll(cmk));
-            const uint32_t qb = q_s + rl32(g.dq, 63 - (int)__builtin_clzll(cmk)) + 1u;
-            if (qb - qg > 64u) {   // the group is full: its records (all before qa) first
-                flush(qa - qg);
-                if (ustop) return false;
-            }
+        if (qb > qa) {
             const uint32_t qj = qg + (uint32_t)lane;
             const bool in = qj >= qa && qj < qb;
             const int32_t src = (int32_t)((qj - q_s) * P + (P - 1u) - p_s);
             const uint32_t cv = (uint32_t)__builtin_amdgcn_ds_bpermute(in ? 4 * src : 0, (int)~v);
             vcrc = in ? cv : vcrc;
-            if (in) {
-                const int32_t wo = lane * (int32_t)L + (int32_t)gadj, wa = wo & ~3;
-                wsh = (uint32_t)wo & 3u;
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(grs, wa + 16 * i, 0, 0);
-                    win[4 * i] = a.x; win[4 * i + 1] = a.y; win[4 * i + 2] = a.z; win[4 * i + 3] = a.w;
-                }
-                win[12] = __builtin_amdgcn_raw_buffer_load_b32(grs, wa + 48, 0, 0);
-            }
-            if (early) {   // (waits for these windows once)
-                early = false;
-                flush(qb - qg);
-                if (ustop) return false;
-            }
+            qdone = qb;
         }
-        return true;
     };
     uint32_t q0 = 0, p0 = 0;
     Geo g0 = geo(q0, p0);
     issue(w, q0, p0, g0);
-#if KVR_PDB
-    // two piece buffers: step s + 1's pieces are loaded before step s is processed
-    uint32_t wb[UW + 1];
-#pragma unroll 1
-    for (;;) {
-        uint32_t q1 = q0 + adv_q, p1 = p0 + adv_p;
-        if (p1 >= P) { p1 -= P; ++q1; }
-        const bool h1 = q1 < q_end;
-        Geo g1 = g0;
-        if (h1) { g1 = geo(q1, p1); issue(wb, q1, p1, g1); }
-        if (!finish_step(crc_step(w, g0), q0, p0, g0) || !h1) break;
-        uint32_t q2 = q1 + adv_q, p2 = p1 + adv_p;
-        if (p2 >= P) { p2 -= P; ++q2; }
-        const bool h2 = q2 < q_end;
-        Geo g2 = g1;
-        if (h2) { g2 = geo(q2, p2); issue(w, q2, p2, g2); }
-        if (!finish_step(crc_step(wb, g1), q1, p1, g1) || !h2) break;
-        q0 = q2; p0 = p2; g0 = g2;
-    }
-#else
     // one piece buffer: the next step's pieces are loaded as soon as the CRC has read this step's
+    KVR_PSTAMP(0);
 #pragma unroll 1
     for (;;) {
+        uint32_t qa, qb;
+        pre_step(q0, g0, qa, qb);   // (a stop found here ends the loop after this step: no exit between
+                                    // the window loads and the next pieces, so the waits stay exact)
+        KVR_PSTAMP(4);
         const uint32_t raw = crc_step(w, g0);
+        KVR_PSTAMP(1);
+        KVR_PCOUNT(6);
         uint32_t q1 = q0 + adv_q, p1 = p0 + adv_p;
         if (p1 >= P) { p1 -= P; ++q1; }
         const bool h1 = q1 < q_end;
-        Geo g1 = g0;
-        if (h1) { g1 = geo(q1, p1); issue(w, q1, p1, g1); }
-        if (!finish_step(raw, q0, p0, g0) || !h1) break;
+        Geo g1 = geo(q1, p1);
+        if (!h1) { g1.act = false; g1.o = 0x7FFFFF00; }
+        issue(w, q1, p1, g1);   // (issued on every path, the last step's reading nothing: exact wait counts)
+        KVR_PSTAMP(2);
+        finish_step(raw, q0, p0, g0, qa, qb);
+        KVR_PSTAMP(3);
+        if (!h1 || ustop) break;
         q0 = q1; p0 = p1; g0 = g1;
     }
-#endif
-    if (!ustop && qg < q_end) flush(q_end - qg);
+    merge_windows();
+    if (!ustop && qg < qdone) flush(qdone - qg);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (a prefetched step the stop left unused)
+    if (!ustop && qg != q_end) ustop = true;   // (defensive: every record of the stripe completes)
     if (!ustop) {
         close_tiles(sd.t_end, seg_n);
         total += qg;
         finish(Pe + (uint64_t)q_end * L);
+        KVR_PSTAMP(5);
+        KVR_PFLUSH();
         return;
     }
     // hand back at record qg: its tile's records emitted here are `ah`, the last slots claimed

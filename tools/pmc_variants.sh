@@ -1,5 +1,5 @@
 #!/bin/bash
-# Per-tile PMC counters of k_replay's first pass for ablation variants / A/B builds (tools/ablate.py
+# Per-tile PMC counters of k_piece and k_replay's first pass for ablation variants / A/B builds (tools/ablate.py
 # $PCFG, default cfg2): three rocprofv3 --pmc passes per variant (counter groups within the gfx950
 # per-pass limits).
 #   usage: [PCFG=cfg4] tools/pmc_variants.sh <outdir> [masks or build names...]
@@ -25,13 +25,14 @@ tiles = 524288
 for d in sorted(glob.glob(out + "/a*/")):
     agg = collections.defaultdict(list)
     for f in glob.glob(d + "**/*counter_collection.csv", recursive=True):
-        rows = [r for r in csv.DictReader(open(f)) if "k_replay" in r["Kernel_Name"]]
-        if not rows: continue
-        big = max(int(r["Grid_Size"]) for r in rows)
-        for r in rows:
-            if int(r["Grid_Size"]) == big:
-                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for kern in ("k_piece", "k_replay"):
+            rows = [r for r in csv.DictReader(open(f)) if kern in r["Kernel_Name"]]
+            if not rows: continue
+            big = max(int(r["Grid_Size"]) for r in rows)
+            for r in rows:
+                if int(r["Grid_Size"]) == big:
+                    agg[(kern, r["Counter_Name"])].append(float(r["Counter_Value"]))
     print(os.path.basename(d.rstrip("/")))
-    for c, v in sorted(agg.items()):
-        print(f"   {c:24s} total {sum(v)/len(v):16.0f}   per tile {sum(v)/len(v)/tiles:10.1f}")
+    for (kern, c), v in sorted(agg.items()):
+        print(f"   {kern:9s} {c:24s} total {sum(v)/len(v):16.0f}   per tile {sum(v)/len(v)/tiles:10.1f}")
 PY

@@ -1,5 +1,6 @@
 """Diagnostic: per-phase cycle breakdown of k_replay's tile loop (build with -DKVR_PROF into
-lib/libkvreplay_prof.so).  Usage: python tools/prof_phases.py [cfg2|cfg3|...] [n_segments]"""
+lib/libkvreplay_prof.so).  Usage: python tools/prof_phases.py [cfg2|cfg3|...] [n_segments]
+(k_piece's phases when it ran; KVR_NO_PIECE=1 for k_replay's tile loop)"""
 import ctypes as C
 import os
 import sys
@@ -57,6 +58,16 @@ for it in range(3):
     lib.kvr_last_stats(ctx, C.byref(st))
     lib.kvr_prof_read(prof, 0)
 # KVR_STAMP slots of kvr_replay_kernel.hip (unused slots print 0)
+if os.environ.get("KVR_NO_PIECE") is None and st.n_tiles and prof[6]:   # k_piece's slots (kvr_replay_kernel.hip KVR_PSTAMP)
+    steps, flushes = prof[6], prof[7]
+    tot_c = sum(prof[i] for i in range(6))
+    print(f"{cfg} (k_piece): rc={rc} n={n.value}/{nrec} stripes={st.n_stripes} ms_replay={st.ms_replay:.3f} "
+          f"steps={steps} flushes={flushes}")
+    for i, nm in enumerate(["setup (search, prediction)", "crc_step (incl. load wait)", "issue", "finish_step",
+                            "flush", "close"]):
+        print(f"  {nm:28s} {prof[i] / steps:10.0f} cycles/step  {100 * prof[i] / max(tot_c, 1):5.1f}%")
+    print(f"  total {tot_c / steps:10.0f} cycles/step (per wave, lane 0); {tot_c / st.n_stripes:.0f} cycles/stripe")
+    sys.exit(0)
 names = ["setup(load)", "stride-decode", "hop-loop+rest", "finalize", "bookkeep", "wait(vmcnt)", "stride-emit",
          "cand-swar", "crc-entry", "unit-loop+kmul", "scan", "cand-decode", "cand-walk", "cand-emit", "spec tiles", "batched tiles"]
 tiles = st.n_tiles
