@@ -33,7 +33,7 @@ using namespace kvr;
 // the replay kernel (kvr_replay_kernel.hip): KR_WPB = stripes per workgroup,
 // KR_TILE = tile bytes
 #define KR_KERNEL k_replay
-static constexpr int KR_RT = RT, KR_WPB = WPB, KR_TILE = TILE;
+static constexpr int KR_RT = RT, KR_WPB = WPB, KR_TILE = TILE, RW_WPB = RT_REWALK / 64;
 
 namespace {
 
@@ -811,7 +811,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             continue;
         }
         while (c->h_link->status == 3 && guard++ < n_stripes + 4) {
-            hipLaunchKernelGGL(k_rewalk, dim3((std::max(1u, std::min(c->h_link->n_redo, (uint32_t)c->redo.n)) + KR_WPB - 1) / KR_WPB), dim3(KR_RT),
+            hipLaunchKernelGGL(k_rewalk, dim3((std::max(1u, std::min(c->h_link->n_redo, (uint32_t)c->redo.n)) + RW_WPB - 1) / RW_WPB), dim3(RT_REWALK),
                                0, st, c->segs.p, c->stripes.p, n_stripes, c->sres.p, c->tres.p, c->pool.p, pool_cap, c->ctr.p,
                                tb, c->redo.p, c->link.p, pool_chunk, kp);
             hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes,
@@ -1382,6 +1382,17 @@ int kvr_prof_read(unsigned long long *out, int reset) {
     return KVR_OK;
 #else
     (void)out; (void)reset;
+    return KVR_EINVAL;
+#endif
+}
+
+// diagnostic build only: k_piece's per-stripe (start, end, HW_ID, XCC_ID), 4 x n words (not in the header)
+int kvr_prof_stripes(unsigned long long *out, int n) {
+#ifdef KVR_PROF
+    if (n > 16384) n = 16384;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pst), (size_t)n * 32) == hipSuccess ? KVR_OK : KVR_EHIP;
+#else
+    (void)out; (void)n;
     return KVR_EINVAL;
 #endif
 }

@@ -48,6 +48,7 @@ namespace kvr {
 constexpr int RT = KVR_RT;
 constexpr int NWAVE = RT / 64;            // waves per workgroup
 constexpr int WPB = NWAVE;                // stripes per workgroup (one per wave)
+constexpr int RT_REWALK = RT / 2;         // k_rewalk's workgroup
 constexpr int UW = SC / 4;                // dwords of a lane's unit
 constexpr int SC_LOG = 7;
 static_assert(SC == 1 << SC_LOG, "unit size");
@@ -115,6 +116,12 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #ifndef KVR_PABLATE   // diagnostic builds of k_piece only (results wrong): 1 no CRC, 2 no push + scan, 8 no
 #define KVR_PABLATE 0   // realignment
 #endif
+#ifndef KVR_PBAL   // k_piece: 1 = wave priorities from each wave's progress against its workgroup's mean
+#define KVR_PBAL 1     // (without, oldest-first issue finishes a CU's 16 stripes in 4 waves of 4)
+#endif
+#ifndef KVR_PBAL_D   // the progress band (1/4096 of a run) around the mean of priorities 1 and 2
+#define KVR_PBAL_D 64
+#endif
 #ifndef KVR_UMIN    // the shortest value the piece mode takes (pieces are 128 B: shorter values waste lanes)
 #define KVR_UMIN 128
 #endif
@@ -139,6 +146,9 @@ constexpr int UKEYW = 9;                 // ... and longest key: 4 UKEYW bytes, 
 
 #ifdef KVR_PROF
 __device__ unsigned long long g_prof[16];
+#ifdef KVR_PROF
+__device__ unsigned long long g_pst[4 * 16384];   // (k_piece, per stripe: start, end, HW_ID, XCC_ID)
+#endif
 #define KVR_STAMP(i)                                                        \
     do {                                                                    \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();         \
@@ -924,24 +934,25 @@ __device__ inline uint64_t find_entry(const uint32_t (&w)[UW], const TileSeg &ts
 }
 
 // the CRC and multiply tables, global -> LDS (every workgroup of k_replay, k_rewalk and k_piece)
+template <int NT = RT>
 __device__ __forceinline__ void stage_tables(Smem &S, const Tables &tb, int tid) {
-    for (int i = tid; i < 256 * 64; i += RT) S.C2[i] = tb.crc8[c2_table(i & 63) * 256 + (i >> 6)];
-    for (int i = tid; i < 8 * 16 * KR_PITCH; i += RT) {
+    for (int i = tid; i < 256 * 64; i += NT) S.C2[i] = tb.crc8[c2_table(i & 63) * 256 + (i >> 6)];
+    for (int i = tid; i < 8 * 16 * KR_PITCH; i += NT) {
         const int row = i / KR_PITCH, kk = i - row * KR_PITCH;   // row = 16 i + n
         S.KR[i] = kk < 64 ? tb.kmul[((KSET_R + kk) * 8 + (row >> 4)) * 16 + (row & 15)] : 0u;
     }
-    for (int i = tid; i < 8 * 16 * KQL_PITCH; i += RT) {
+    for (int i = tid; i < 8 * 16 * KQL_PITCH; i += NT) {
         const int row = i / KQL_PITCH, q = i - row * KQL_PITCH;   // row = 16 i + n
         S.KQL[i] = q < NQ ? tb.kmul[((KSET_Q + q) * 8 + (row >> 4)) * 16 + (row & 15)] : 0u;
     }
-    for (int i = tid; i < 2 * 8 * 16; i += RT) S.KQ2[i] = tb.kmul[(KSET_Q + (i < 128 ? SC / 8 : SC / 4)) * 8 * 16 + (i & 127)];
-    for (int i = tid; i < 2 * 8 * 16; i += RT) S.KQ4[i] = tb.kmul[(KSET_Q + (i < 128 ? SC / 16 : 3 * SC / 16)) * 8 * 16 + (i & 127)];
+    for (int i = tid; i < 2 * 8 * 16; i += NT) S.KQ2[i] = tb.kmul[(KSET_Q + (i < 128 ? SC / 8 : SC / 4)) * 8 * 16 + (i & 127)];
+    for (int i = tid; i < 2 * 8 * 16; i += NT) S.KQ4[i] = tb.kmul[(KSET_Q + (i < 128 ? SC / 16 : 3 * SC / 16)) * 8 * 16 + (i & 127)];
     if (tid < NIX) S.IX[tid] = tb.initx[tid];
 }
 
 // REDO: the re-walk pass (k_rewalk) over k_link's list, with the walk-on into later stripes; the
-// first pass (k_replay) walks every stripe once
-template <bool REDO>
+// first pass (k_replay) walks every stripe once.  NT threads a workgroup, one stripe a wave.
+template <bool REDO, int NT = RT>
 __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                                             const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
                                             StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
@@ -954,17 +965,17 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
     __shared__ Smem S;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     if (!REDO && hand) {   // after k_piece: a workgroup whose stripes it all finished has nothing to do
-        const uint32_t g = blockIdx.x * WPB + (uint32_t)wv;
+        const uint32_t g = blockIdx.x * (NT / 64) + (uint32_t)wv;
         if (!__syncthreads_or(g < n_stripes && !hand[g].done)) return;
     }
-    stage_tables(S, tb, tid);
+    stage_tables<NT>(S, tb, tid);
     __syncthreads();   // the only workgroup barrier: from here on every wave is on its own
     uint32_t *const MK = S.MK[wv];   // this wave's long-value marks
 
     Crc K;
     crc_init(K, S.C2, (uint32_t)lane);
     // the stripe index is wave-uniform: say so, so that the whole stripe state lives in SGPRs
-    const uint32_t gw = blockIdx.x * WPB + (uint32_t)__builtin_amdgcn_readfirstlane(wv);
+    const uint32_t gw = blockIdx.x * (NT / 64) + (uint32_t)__builtin_amdgcn_readfirstlane(wv);
     uint32_t si;
     uint64_t forced = NONE;
     if (redo_mode) {
@@ -1918,14 +1929,16 @@ __global__ __launch_bounds__(RT) void k_replay(const SegDesc *__restrict__ segs,
                        scnt, hand);
 }
 
-__global__ __launch_bounds__(RT) void k_rewalk(const SegDesc *__restrict__ segs,
+// (half the workgroup of k_replay: two waves a SIMD, so the REDO body's state fits 256 VGPRs unspilled;
+// the fallback re-walks few stripes, occupancy does not matter there)
+__global__ __launch_bounds__(RT_REWALK) void k_rewalk(const SegDesc *__restrict__ segs,
                                                const StripeDesc *__restrict__ stripes, uint32_t n_stripes,
                                                StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
                                                kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
                                                Tables tb, const RedoEnt *__restrict__ redo,
                                                const LinkResult *__restrict__ link, uint32_t pool_chunk,
                                                uint4 *__restrict__ kpool) {
-    replay_body<true>(segs, stripes, n_stripes, sres, tres, pool, pool_cap, ctr, tb, redo, link, pool_chunk, kpool,
+    replay_body<true, RT_REWALK>(segs, stripes, n_stripes, sres, tres, pool, pool_cap, ctr, tb, redo, link, pool_chunk, kpool,
                       nullptr, nullptr);
 }
 
@@ -1953,15 +1966,19 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     __shared__ Smem S;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     stage_tables(S, tb, tid);
+    uint32_t *const bal = &S.MK[0][0];   // [0] the progress of the waves in their step loop, [1] their number
+    if (tid == 0) { bal[0] = 0u; bal[1] = 0u; }
     __syncthreads();
     Crc K;
     crc_init(K, S.C2, (uint32_t)lane);
     const uint32_t si = blockIdx.x * WPB + (uint32_t)__builtin_amdgcn_readfirstlane(wv);
     if (si >= n_stripes) return;
 #ifdef KVR_PROF
-    // (diagnostic build: cycles per phase into g_prof 0-5, counts in 6-7; tools/prof_phases.py piece)
+    // (diagnostic build: cycles per phase into g_prof 0-5, 8-9, counts in 6-7, s_memrealtime 12-14;
+    // tools/prof_phases.py)
     unsigned long long pt_last = __builtin_amdgcn_s_memtime();
-    unsigned long long pacc[8] = {};
+    const unsigned long long prt0 = __builtin_amdgcn_s_memrealtime();   // (100 MHz: the clock's rate)
+    unsigned long long pacc[10] = {};
 #define KVR_PSTAMP(i)                                                       \
     do {                                                                    \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();         \
@@ -1971,8 +1988,19 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
 #define KVR_PCOUNT(i) (pacc[i] += 1)
 #define KVR_PFLUSH()                                                        \
     do {                                                                    \
-        if (lane == 0)                                                      \
-            for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_prof[i_], pacc[i_]); \
+        if (lane == 0) {                                                    \
+            for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_prof[i_], pacc[i_]); \
+            const unsigned long long prt1 = __builtin_amdgcn_s_memrealtime(); \
+            atomicAdd(&g_prof[12], prt1 - prt0);                            \
+            atomicMax(&g_prof[13], prt1);                                   \
+            atomicMax(&g_prof[14], ~prt0);                                 \
+            if (si < 16384u) {                                              \
+                g_pst[4 * si] = prt0;                                       \
+                g_pst[4 * si + 1] = prt1;                                   \
+                g_pst[4 * si + 2] = __builtin_amdgcn_s_getreg(0xF804);      \
+                g_pst[4 * si + 3] = __builtin_amdgcn_s_getreg(0xF814);      \
+            }                                                               \
+        }                                                                   \
     } while (0)
 #else
 #define KVR_PSTAMP(i) do { } while (0)
@@ -2251,6 +2279,7 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     };
     auto pre_step = [&](uint32_t q_s, const Geo &g, uint32_t &qa, uint32_t &qb) {
         merge_windows();
+        KVR_PSTAMP(8);
         if (early && qdone > qg) {
             early = false;
             flush(qdone - qg);
@@ -2264,6 +2293,7 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
         }
         // (issued on every step, a step that completes nothing reading nothing: a conditional load
         // would leave the piece waits below conservative)
+        KVR_PSTAMP(4);
         const uint32_t qj = qg + (uint32_t)lane;
         wpend = qj >= qa && qj < qb;
         const int32_t wo = lane * (int32_t)L + (int32_t)gadj, wa = wpend ? (wo & ~3) : 0x7FFFFF00;
@@ -2300,6 +2330,29 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     uint32_t q0 = 0, p0 = 0;
     Geo g0 = geo(q0, p0);
     issue(w, q0, p0, g0);
+    // The 16 waves of a CU share its issue slots oldest first: left alone, the oldest wave of each
+    // SIMD finishes its stripe in 55 % of the time of the youngest, and the CU's last quarter runs on
+    // 4 waves.  A wave ahead of the mean progress (records done, 1/4096 of its run) drops its priority,
+    // one behind raises it, so the 16 stripes end together.
+    const uint64_t pscale = (4096ull << 32) / q_end;
+    uint32_t pown = 0;
+    if (KVR_PBAL && lane == 0) atomicAdd(&bal[1], 1u);
+    auto balance = [&](uint32_t q_now) {
+        const uint32_t pn = (uint32_t)(((uint64_t)q_now * pscale) >> 32);
+        uint32_t sum = 0, cnt = 1;
+        if (lane == 0) {
+            sum = atomicAdd(&bal[0], pn - pown) + (pn - pown);
+            cnt = bal[1];
+        }
+        pown = pn;
+        sum = uni32(sum);
+        cnt = uni32(cnt);
+        const int32_t d = (int32_t)(pn * cnt - sum), dl = (int32_t)(KVR_PBAL_D * cnt);
+        if (d < -dl) __builtin_amdgcn_s_setprio(3);
+        else if (d < 0) __builtin_amdgcn_s_setprio(2);
+        else if (d < dl) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+    };
     // one piece buffer: the next step's pieces are loaded as soon as the CRC has read this step's
     KVR_PSTAMP(0);
 #pragma unroll 1
@@ -2307,7 +2360,7 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
         uint32_t qa, qb;
         pre_step(q0, g0, qa, qb);   // (a stop found here ends the loop after this step: no exit between
                                     // the window loads and the next pieces, so the waits stay exact)
-        KVR_PSTAMP(4);
+        KVR_PSTAMP(9);
         const uint32_t raw = crc_step(w, g0);
         KVR_PSTAMP(1);
         KVR_PCOUNT(6);
@@ -2319,9 +2372,14 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
         issue(w, q1, p1, g1);   // (issued on every path, the last step's reading nothing: exact wait counts)
         KVR_PSTAMP(2);
         finish_step(raw, q0, p0, g0, qa, qb);
+        if (KVR_PBAL) balance(q1 < q_end ? q1 : q_end);
         KVR_PSTAMP(3);
         if (!h1 || ustop) break;
         q0 = q1; p0 = p1; g0 = g1;
+    }
+    if (KVR_PBAL) {   // out of the mean
+        if (lane == 0) { atomicSub(&bal[0], pown); atomicSub(&bal[1], 1u); }
+        __builtin_amdgcn_s_setprio(0);
     }
     merge_windows();
     if (!ustop && qg < qdone) flush(qdone - qg);

@@ -60,13 +60,43 @@ for it in range(3):
 # KVR_STAMP slots of kvr_replay_kernel.hip (unused slots print 0)
 if os.environ.get("KVR_NO_PIECE") is None and st.n_tiles and prof[6]:   # k_piece's slots (kvr_replay_kernel.hip KVR_PSTAMP)
     steps, flushes = prof[6], prof[7]
-    tot_c = sum(prof[i] for i in range(6))
+    tot_c = sum(prof[i] for i in (0, 1, 2, 3, 4, 5, 8, 9))
     print(f"{cfg} (k_piece): rc={rc} n={n.value}/{nrec} stripes={st.n_stripes} ms_replay={st.ms_replay:.3f} "
           f"steps={steps} flushes={flushes}")
-    for i, nm in enumerate(["setup (search, prediction)", "crc_step (incl. load wait)", "issue", "finish_step",
-                            "flush", "close"]):
+    for i, nm in [(0, "setup (search, prediction)"), (8, "window merge (wait)"), (4, "flush"), (9, "window issue"),
+                  (1, "crc_step (incl. load wait)"), (2, "issue"), (3, "finish_step"), (5, "close")]:
         print(f"  {nm:28s} {prof[i] / steps:10.0f} cycles/step  {100 * prof[i] / max(tot_c, 1):5.1f}%")
     print(f"  total {tot_c / steps:10.0f} cycles/step (per wave, lane 0); {tot_c / st.n_stripes:.0f} cycles/stripe")
+    if prof[12]:   # s_memrealtime (100 MHz) over the same stretches, and the span of all k_piece waves
+        span = (prof[13] - (~prof[14] & (2**64 - 1))) / 100.0
+        print(f"  clock {tot_c / prof[12] * 100:.0f} MHz (s_memtime / s_memrealtime); stripe mean "
+              f"{prof[12] / st.n_stripes / 100:.1f} us; first wave start to last wave end {span:.1f} us")
+    ns = min(st.n_stripes, 16384)
+    pst = (C.c_ulonglong * (4 * ns))()
+    lib.kvr_prof_stripes.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    if lib.kvr_prof_stripes(pst, ns) == 0:
+        import numpy as np
+        a = np.frombuffer(pst, dtype=np.uint64).reshape(ns, 4).astype(np.int64)
+        t0 = a[:, 0].min()
+        beg, end = (a[:, 0] - t0) / 100.0, (a[:, 1] - t0) / 100.0
+        dur = end - beg
+        hw = a[:, 2]
+        wave, simd, cu, se = hw & 15, (hw >> 4) & 3, (hw >> 8) & 15, (hw >> 13) & 7
+        xcc = a[:, 3] & 15
+        q = np.percentile(dur, [0, 10, 50, 90, 100])
+        print(f"  stripe us: start max {beg.max():.1f}; duration min/p10/p50/p90/max "
+              + " ".join(f"{v:.0f}" for v in q) + f"; end p50 {np.median(end):.0f} max {end.max():.0f}")
+        wl = np.arange(ns) % 16
+        print("  mean duration by wave of the workgroup: " + " ".join(f"{dur[wl == i].mean():.0f}" for i in range(16)))
+        print("  mean duration by XCC: " + " ".join(f"{dur[xcc == i].mean():.0f}" for i in range(8) if (xcc == i).any()))
+        print("  mean duration by SIMD: " + " ".join(f"{dur[simd == i].mean():.0f}" for i in range(4)))
+        # per CU (xcc, se, cu): the spread of CU means, and of the spread inside a CU
+        key = (xcc * 8 + se) * 16 + cu
+        cus = np.unique(key)
+        cm = np.array([dur[key == k].mean() for k in cus])
+        cs = np.array([dur[key == k].max() - dur[key == k].min() for k in cus])
+        print(f"  CUs {len(cus)}: CU-mean duration min/p50/max {cm.min():.0f} {np.median(cm):.0f} {cm.max():.0f}; "
+              f"in-CU max-min p50 {np.median(cs):.0f} max {cs.max():.0f}")
     sys.exit(0)
 names = ["setup(load)", "stride-decode", "hop-loop+rest", "finalize", "bookkeep", "wait(vmcnt)", "stride-emit",
          "cand-swar", "crc-entry", "unit-loop+kmul", "scan", "cand-decode", "cand-walk", "cand-emit", "spec tiles", "batched tiles"]
