@@ -78,6 +78,7 @@ struct __align__(16) Smem {
     uint32_t KQ4[2 * 8 * 16];             // the same for x^(8*32) (h 0) and x^(8*96) (h 1): k_piece's 4-chain combine
     uint32_t IX[NIX + 3];                 // 0xFFFFFFFF * x^(8j): initial register pushed through j bytes
     uint32_t MK[NWAVE][64];               // per wave: long-value marks by unit (framing)
+    uint32_t BAL[4];                      // the workgroup's progress sum and wave count (KVR_PBAL / KVR_RBAL)
     uint32_t C2[256 * 64];                // byte tables, row b = 256 B (64 KiB), see Crc
     uint32_t KR[8 * 16 * KR_PITCH];       // [i][n][k]: (n << 4i) * x^(8*SC*(k+1)), k < 64  (above 64 KiB,
     uint32_t KQL[8 * 16 * KQL_PITCH];     // [i][n][q]: (n << 4i) * x^(8*4q), q per lane (columns > SC/4: 0)  see kmul_col)
@@ -89,15 +90,27 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 // wave priority (s_setprio) of the serial phases: the framing and the records phase are the
 // tile's critical path and share the CU with 15 other waves, so they issue ahead of waves in
 // their bulk CRC; the scan + finalize chain is raised too
+// (0 with KVR_RBAL 2: the progress balance sets the priority, one level for every phase)
 #ifndef KVR_HOP_PRIO
-#define KVR_HOP_PRIO 2
+#define KVR_HOP_PRIO 0
 #endif
 #ifndef KVR_REC_PRIO
-#define KVR_REC_PRIO 1
+#define KVR_REC_PRIO 0
 #endif
 #ifndef KVR_FIN_PRIO
-#define KVR_FIN_PRIO 1
+#define KVR_FIN_PRIO 0
 #endif
+// k_replay's progress balance (as k_piece's KVR_PBAL): 2 = four priority levels from the wave's
+// progress against its workgroup's mean, per tile (cfg4 -3 %, cfg5 -3.5 % against none); 1 = the
+// phase priorities above, one level up for a wave behind the mean
+#ifndef KVR_RBAL
+#define KVR_RBAL 2
+#endif
+#define KVR_SETPRIO(p)                                                                   \
+    do {                                                                                 \
+        if (KVR_RBAL && rbal_up) __builtin_amdgcn_s_setprio((p) + 1 > 3 ? 3 : (p) + 1); \
+        else __builtin_amdgcn_s_setprio(p);                                              \
+    } while (0)
 #ifndef KVR_LANEFRAME   // 1: lane-parallel framing (0: the exact scalar hop loop for every record)
 #define KVR_LANEFRAME 1
 #endif
@@ -969,6 +982,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
         if (!__syncthreads_or(g < n_stripes && !hand[g].done)) return;
     }
     stage_tables<NT>(S, tb, tid);
+    if (tid == 0) { S.BAL[0] = 0u; S.BAL[1] = 0u; }
     __syncthreads();   // the only workgroup barrier: from here on every wave is on its own
     uint32_t *const MK = S.MK[wv];   // this wave's long-value marks
 
@@ -1047,8 +1061,39 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
 #ifdef KVR_PROF
     unsigned long long t_last = __builtin_amdgcn_s_memtime();
     unsigned long long prof_acc[16] = {};
+    const unsigned long long rrt0 = __builtin_amdgcn_s_memrealtime();
 #endif
+    // progress balance (KVR_RBAL): as k_piece's, over the stripe's tiles; a wave more than
+    // KVR_PBAL_D / 4096 of its stripe behind the workgroup's mean runs one priority up
+    bool rbal_up = false;
+    const uint32_t rb_t0 = sd.t_begin, rb_n = sd.t_end > sd.t_begin ? sd.t_end - sd.t_begin : 1u;
+    const uint64_t rb_scale = (4096ull << 32) / rb_n;
+    uint32_t rb_own = 0;
+    const bool rb_on = KVR_RBAL && !REDO;
+    if (rb_on && lane == 0) atomicAdd(&S.BAL[1], 1u);
     for (;; ++k) {
+        if (rb_on) {
+            const uint32_t kd = k > rb_t0 ? k - rb_t0 : 0u;
+            const uint32_t pn = (uint32_t)(((uint64_t)(kd < rb_n ? kd : rb_n) * rb_scale) >> 32);
+            uint32_t sum = 0, cnt = 1;
+            if (lane == 0) {
+                sum = atomicAdd(&S.BAL[0], pn - rb_own) + (pn - rb_own);
+                cnt = S.BAL[1];
+            }
+            rb_own = pn;
+            sum = uni32(sum);
+            cnt = uni32(cnt);
+            const int32_t d = (int32_t)(pn * cnt - sum), dl = (int32_t)(KVR_PBAL_D * cnt);
+            rbal_up = d < -dl;
+            if (KVR_RBAL == 2) {   // (the phases at one priority: four levels from the progress alone)
+                if (d < -dl) __builtin_amdgcn_s_setprio(3);
+                else if (d < 0) __builtin_amdgcn_s_setprio(2);
+                else if (d < dl) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            } else {
+                KVR_SETPRIO(0);
+            }
+        }
         if (KVR_TOPWAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         KVR_STAMP(5);
         const bool in_stripe = k < sd.t_end;
@@ -1291,7 +1336,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
         struct Fold { uint32_t lmark; int kind; };   // kind 0: none, 1: fold_uniform, 2: fold_views
         auto emit = [&](const Dec &d, int32_t c, bool on, uint32_t rk, uint32_t n_on, int lead, int lastl,
                         bool strided, uint32_t slot0) -> Fold {
-            if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
+            if (KVR_REC_PRIO != KVR_HOP_PRIO) KVR_SETPRIO(KVR_REC_PRIO);
             const uint32_t klen = d.klen, op = d.op, vlen = d.vlen, vb = d.vb, s = d.s;
             Fold fo{0u, 0};
             // one key length for the batch (the first record's, ku): no per-lane byte masks
@@ -1378,7 +1423,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 err_aux = rl64(raux, el);
                 err_pos = (uint64_t)(lo + (int64_t)(int32_t)rl32((uint32_t)c, el));
             }
-            if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
+            if (KVR_REC_PRIO != KVR_HOP_PRIO) KVR_SETPRIO(KVR_HOP_PRIO);
             return fo;
         };
 #endif
@@ -1389,7 +1434,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             int64_t p = (int64_t)entry - lo;
             bool broke = false;              // the chain broke at the last record walked
             if (KVR_ABLATE & 4) p = vhi_r;
-            if (KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
+            if (KVR_HOP_PRIO) KVR_SETPRIO(KVR_HOP_PRIO);
 #if KVR_LANEFRAME
             bool round_broke = false;        // a lane-parallel round ended on a broken record
             if (!huge && p < vhi_r && fast_skip == 0u) {
@@ -1640,7 +1685,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                 uint32_t rerr = N32, rkind = 0;
                 uint64_t raux = 0;
                 const uint32_t j = nrec + (uint32_t)lane;
-                if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_REC_PRIO);
+                if (KVR_REC_PRIO != KVR_HOP_PRIO) KVR_SETPRIO(KVR_REC_PRIO);
                 if (!(KVR_ABLATE & 1) && myrec >= 0) {
                     if (broke && lane == (int)nb - 1) {   // the record that broke the chain: every check
                         const RecRes r = do_record(ts, K, myrec, j, slot, sd.seg, pool, kpool);
@@ -1695,11 +1740,11 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
                     err_pos = (uint64_t)(lo + (int64_t)(int32_t)rl32((uint32_t)myrec, el));
                 }
                 nrec = err_rec != N32 ? err_rec : nrec + nb;
-                if (KVR_REC_PRIO != KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(KVR_HOP_PRIO);
+                if (KVR_REC_PRIO != KVR_HOP_PRIO) KVR_SETPRIO(KVR_HOP_PRIO);
             }
             if (lastq >= 0 && !broke && !huge) stride = (uint32_t)(p - lastq);
             }
-            if (KVR_HOP_PRIO) __builtin_amdgcn_s_setprio(0);
+            if (KVR_HOP_PRIO) KVR_SETPRIO(0);
             tile_exit = broke ? ERRP : (uint64_t)(lo + p);
         }
         // the tile's result record, stored ahead of the next tile's load, so that the wait for that
@@ -1793,7 +1838,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             // the piece of the value crossing the unit end: A pushed through B's bytes, then B
             // (A does not count when that value starts in B's half); the raw CRC of the first
             // 4 qm bytes: A's snapshot, or all of A pushed through 4 (qm - H) bytes, then B's
-            if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(KVR_FIN_PRIO);
+            if (KVR_FIN_PRIO) KVR_SETPRIO(KVR_FIN_PRIO);
             const uint32_t pa = kmul(ca, S.KQ2);
             const uint32_t c = qa >= H ? cb : (pa ^ cb);
             KVR_STAMP(9);
@@ -1853,7 +1898,7 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
             }
         }
 
-        if (KVR_FIN_PRIO) __builtin_amdgcn_s_setprio(0);
+        if (KVR_FIN_PRIO) KVR_SETPRIO(0);
         // the tile's registers are dead from here on: the next tile's load overlaps the rest
         if (!loaded && err_pos == NONE && k + 1 < sg.n_tiles && (k + 1 < sd.t_end || n_carry)) {
             load_unit(abase, d0, len, k + 1, lane, w);
@@ -1874,9 +1919,20 @@ __device__ __forceinline__ void replay_body(const SegDesc *__restrict__ segs,
         KVR_STAMP(4);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain an unused next-tile load
+    if (rb_on) {   // out of the mean
+        if (lane == 0) { atomicSub(&S.BAL[0], rb_own); atomicSub(&S.BAL[1], 1u); }
+        __builtin_amdgcn_s_setprio(0);
+    }
 #ifdef KVR_PROF
-    if (lane == 0)
+    if (lane == 0) {
         for (int i = 0; i < 16; ++i) atomicAdd(&g_prof[i], prof_acc[i]);
+        if (!REDO && !hand && si < 16384u) {   // (per stripe, as k_piece's: k_replay alone, KVR_NO_PIECE)
+            g_pst[4 * si] = rrt0;
+            g_pst[4 * si + 1] = __builtin_amdgcn_s_memrealtime();
+            g_pst[4 * si + 2] = __builtin_amdgcn_s_getreg(0xF804);
+            g_pst[4 * si + 3] = __builtin_amdgcn_s_getreg(0xF814);
+        }
+    }
 #endif
     // tiles of the stripe that were never reached (error stop / pass-through) hold no tuples
     const uint32_t kfirst = k < sd.t_end ? k : sd.t_end;
@@ -1966,7 +2022,7 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     __shared__ Smem S;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     stage_tables(S, tb, tid);
-    uint32_t *const bal = &S.MK[0][0];   // [0] the progress of the waves in their step loop, [1] their number
+    uint32_t *const bal = S.BAL;   // [0] the progress of the waves in their step loop, [1] their number
     if (tid == 0) { bal[0] = 0u; bal[1] = 0u; }
     __syncthreads();
     Crc K;

@@ -57,20 +57,8 @@ for it in range(3):
     st = K.Stats()
     lib.kvr_last_stats(ctx, C.byref(st))
     lib.kvr_prof_read(prof, 0)
-# KVR_STAMP slots of kvr_replay_kernel.hip (unused slots print 0)
-if os.environ.get("KVR_NO_PIECE") is None and st.n_tiles and prof[6]:   # k_piece's slots (kvr_replay_kernel.hip KVR_PSTAMP)
-    steps, flushes = prof[6], prof[7]
-    tot_c = sum(prof[i] for i in (0, 1, 2, 3, 4, 5, 8, 9))
-    print(f"{cfg} (k_piece): rc={rc} n={n.value}/{nrec} stripes={st.n_stripes} ms_replay={st.ms_replay:.3f} "
-          f"steps={steps} flushes={flushes}")
-    for i, nm in [(0, "setup (search, prediction)"), (8, "window merge (wait)"), (4, "flush"), (9, "window issue"),
-                  (1, "crc_step (incl. load wait)"), (2, "issue"), (3, "finish_step"), (5, "close")]:
-        print(f"  {nm:28s} {prof[i] / steps:10.0f} cycles/step  {100 * prof[i] / max(tot_c, 1):5.1f}%")
-    print(f"  total {tot_c / steps:10.0f} cycles/step (per wave, lane 0); {tot_c / st.n_stripes:.0f} cycles/stripe")
-    if prof[12]:   # s_memrealtime (100 MHz) over the same stretches, and the span of all k_piece waves
-        span = (prof[13] - (~prof[14] & (2**64 - 1))) / 100.0
-        print(f"  clock {tot_c / prof[12] * 100:.0f} MHz (s_memtime / s_memrealtime); stripe mean "
-              f"{prof[12] / st.n_stripes / 100:.1f} us; first wave start to last wave end {span:.1f} us")
+def stripe_spread():
+    """k_piece / k_replay per-stripe (start, end, HW_ID, XCC_ID) from the diagnostic build."""
     ns = min(st.n_stripes, 16384)
     pst = (C.c_ulonglong * (4 * ns))()
     lib.kvr_prof_stripes.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
@@ -97,6 +85,23 @@ if os.environ.get("KVR_NO_PIECE") is None and st.n_tiles and prof[6]:   # k_piec
         cs = np.array([dur[key == k].max() - dur[key == k].min() for k in cus])
         print(f"  CUs {len(cus)}: CU-mean duration min/p50/max {cm.min():.0f} {np.median(cm):.0f} {cm.max():.0f}; "
               f"in-CU max-min p50 {np.median(cs):.0f} max {cs.max():.0f}")
+
+
+# KVR_STAMP slots of kvr_replay_kernel.hip (unused slots print 0)
+if os.environ.get("KVR_NO_PIECE") is None and st.n_tiles and prof[6]:   # k_piece's slots (kvr_replay_kernel.hip KVR_PSTAMP)
+    steps, flushes = prof[6], prof[7]
+    tot_c = sum(prof[i] for i in (0, 1, 2, 3, 4, 5, 8, 9))
+    print(f"{cfg} (k_piece): rc={rc} n={n.value}/{nrec} stripes={st.n_stripes} ms_replay={st.ms_replay:.3f} "
+          f"steps={steps} flushes={flushes}")
+    for i, nm in [(0, "setup (search, prediction)"), (8, "window merge (wait)"), (4, "flush"), (9, "window issue"),
+                  (1, "crc_step (incl. load wait)"), (2, "issue"), (3, "finish_step"), (5, "close")]:
+        print(f"  {nm:28s} {prof[i] / steps:10.0f} cycles/step  {100 * prof[i] / max(tot_c, 1):5.1f}%")
+    print(f"  total {tot_c / steps:10.0f} cycles/step (per wave, lane 0); {tot_c / st.n_stripes:.0f} cycles/stripe")
+    if prof[12]:   # s_memrealtime (100 MHz) over the same stretches, and the span of all k_piece waves
+        span = (prof[13] - (~prof[14] & (2**64 - 1))) / 100.0
+        print(f"  clock {tot_c / prof[12] * 100:.0f} MHz (s_memtime / s_memrealtime); stripe mean "
+              f"{prof[12] / st.n_stripes / 100:.1f} us; first wave start to last wave end {span:.1f} us")
+    stripe_spread()
     sys.exit(0)
 names = ["setup(load)", "stride-decode", "hop-loop+rest", "finalize", "bookkeep", "wait(vmcnt)", "stride-emit",
          "cand-swar", "crc-entry", "unit-loop+kmul", "scan", "cand-decode", "cand-walk", "cand-emit", "spec tiles", "batched tiles"]
@@ -110,3 +115,4 @@ for i, nm in enumerate(names):
         continue
     print(f"  {nm:10s} {prof[i] / tiles:10.0f} cycles/tile  {100 * prof[i] / max(tot_c, 1):5.1f}%")
 print(f"  total      {tot_c / tiles:10.0f} cycles/tile (wave-0 lane-0 view)")
+stripe_spread()
