@@ -141,7 +141,8 @@ static void run(const uint8_t *d, uint64_t bytes, int cus, int delay, uint32_t *
     printf("%-8s depth %d delay %4d VALU: %.3f ms  %7.1f GB/s\n", nm[PAT], DEPTH, delay, best, bytes / best / 1e6);
 }
 
-int main() {
+int main(int argc, char **argv) {
+    const bool calib = argc > 1 && strcmp(argv[1], "calib") == 0;   // (tools/pmc_traffic.py: piece-a only)
     // 1. correctness of unaligned 16-B buffer loads
     uint8_t *d8; uint32_t *dout;
     CK(hipMalloc(&d8, 4096)); CK(hipMalloc(&dout, 16 * 8 * 4));
@@ -169,6 +170,13 @@ int main() {
     if (hipMalloc(&d, bytes) != hipSuccess) { printf("alloc failed\n"); return 1; }
     CK(hipMalloc(&sink, RT * 4));
     CK(hipMemset(d, 1, bytes));
+    if (calib) {   // the byte count FETCH_SIZE is calibrated against: every step's 8 records, once
+        const uint32_t n_stripes = cus * 16;
+        const uint64_t bps = bytes / n_stripes, n_steps = (bps - 1100) / (8u * 1049u);
+        run<2, 2>(d, bytes, cus, 0, sink);
+        printf("calib_bytes_per_dispatch=%llu\n", (unsigned long long)(n_stripes * n_steps * 8u * 1049u));
+        return 0;
+    }
     for (int delay : {0, 256, 512}) {
         run<0, 1>(d, bytes, cus, delay, sink);
         run<1, 1>(d, bytes, cus, delay, sink);

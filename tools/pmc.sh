@@ -23,8 +23,9 @@ for f in glob.glob(out + "/p*/**/*counter_collection.csv", recursive=True):
         k = row["Kernel_Name"].split("(")[0]
         agg[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
 for k, d in agg.items():
-    if "k_replay" not in k and "k_compact" not in k and "k_etag" not in k: continue
+    if "k_replay" not in k and "k_piece" not in k and "k_compact" not in k and "k_etag" not in k: continue
     print(k)
     for c, v in sorted(d.items()):
-        print(f"   {c:28s} mean/dispatch {sum(v)/len(v):16.1f}  (n={len(v)})")
+        # (per 8-KiB tile of a 4-GiB shard: 524288 tiles; SQ_*_CYCLES in quad-cycles)
+        print(f"   {c:28s} mean/dispatch {sum(v)/len(v):16.1f}  per tile {sum(v)/len(v)/524288:10.1f}  (n={len(v)})")
 PY
