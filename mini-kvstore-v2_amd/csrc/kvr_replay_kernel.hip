@@ -127,7 +127,8 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #define KVR_PCHAINS 2
 #endif
 #ifndef KVR_PABLATE   // diagnostic builds of k_piece only (results wrong): 1 no CRC, 2 no push + scan, 8 no
-#define KVR_PABLATE 0   // realignment
+#define KVR_PABLATE 0   // realignment, 16 no verification or emission (flush only advances), 32 window loads
+                        // past the resource (no memory access), 64 no window load instructions (32, 64 only with 16)
 #endif
 #ifndef KVR_PBAL   // k_piece: 1 = wave priorities from each wave's progress against its workgroup's mean
 #define KVR_PBAL 1     // (without, oldest-first issue finishes a CU's 16 stripes in 4 waves of 4)
@@ -2205,6 +2206,11 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     // verify and emit the group's first n records; a record not as predicted stops the run there
     auto flush = [&](uint32_t n) {
         KVR_PCOUNT(7);
+        if (KVR_PABLATE & 16) {   // (diagnostic: the run's bookkeeping only)
+            qg += n;
+            grs = seg_rsrc_a(sg.base, Pe + (uint64_t)qg * L, len, gadj);
+            return;
+        }
         const uint64_t GB = Pe + (uint64_t)qg * L;
         const bool on = (uint32_t)lane < n;
         uint32_t x[12];   // the record's first 48 bytes
@@ -2352,14 +2358,16 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
         KVR_PSTAMP(4);
         const uint32_t qj = qg + (uint32_t)lane;
         wpend = qj >= qa && qj < qb;
-        const int32_t wo = lane * (int32_t)L + (int32_t)gadj, wa = wpend ? (wo & ~3) : 0x7FFFFF00;
+        const int32_t wo = lane * (int32_t)L + (int32_t)gadj, wa = wpend && !(KVR_PABLATE & 32) ? (wo & ~3) : 0x7FFFFF00;
         wtsh = (uint32_t)wo & 3u;
+        if (!(KVR_PABLATE & 64)) {
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const u32x4 v4 = __builtin_amdgcn_raw_buffer_load_b128(grs, wa + 16 * i, 0, 0);
-            wt[4 * i] = v4.x; wt[4 * i + 1] = v4.y; wt[4 * i + 2] = v4.z; wt[4 * i + 3] = v4.w;
+            for (int i = 0; i < 3; ++i) {
+                const u32x4 v4 = __builtin_amdgcn_raw_buffer_load_b128(grs, wa + 16 * i, 0, 0);
+                wt[4 * i] = v4.x; wt[4 * i + 1] = v4.y; wt[4 * i + 2] = v4.z; wt[4 * i + 3] = v4.w;
+            }
+            wt[12] = __builtin_amdgcn_raw_buffer_load_b32(grs, wa + 48, 0, 0);
         }
-        wt[12] = __builtin_amdgcn_raw_buffer_load_b32(grs, wa + 48, 0, 0);
     };
     // the step's push, scan and value CRCs (records [qa, qb) take theirs into vcrc)
     auto finish_step = [&](uint32_t raw, uint32_t q_s, uint32_t p_s, const Geo &g, uint32_t qa, uint32_t qb) {

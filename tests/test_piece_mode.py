@@ -122,13 +122,23 @@ def test_piece_shapes(gctx, shape, tps):
 CHANGES = ["del", "vlen", "klen", "opcode", "utf8_ok", "keylen_huge"] + list(BAD_UTF8)
 
 
+@pytest.fixture(params=["piece", "tiles"])
+def engine(request, monkeypatch):
+    """piece: k_piece first (the default pipeline); tiles: k_replay's tile loop alone
+    (KVR_NO_PIECE=1), whose lane-parallel stride round takes the same equal records."""
+    if request.param == "tiles":
+        monkeypatch.setenv("KVR_NO_PIECE", "1")
+    return request.param
+
+
 @pytest.mark.parametrize("tps", [0, 16])
 @pytest.mark.parametrize("change", CHANGES)
-def test_piece_hand_back(gctx, change, tps):
+def test_piece_hand_back(gctx, change, tps, engine):
     """A record not as predicted at several indices of a run -- the first record, inside the first
     group, at group boundaries (63, 64, 65), deep in a stripe: k_piece hands the stripe back at
     that record (with the records of its tile already emitted) and k_replay gives the oracle's
-    tuples, or its first error with aux for every UTF-8 failure kind."""
+    tuples, or its first error with aux for every UTF-8 failure kind.  The same stores through
+    k_replay alone (engine "tiles")."""
     n_rec = 2300                                        # ~2.4 MB of 1033-B records
     gctx.set_tiles_per_stripe(tps)
     try:
@@ -140,7 +150,7 @@ def test_piece_hand_back(gctx, change, tps):
 
 
 @pytest.mark.parametrize("unit", ["é", "€", "😀"])
-def test_piece_multibyte_keys(gctx, unit):
+def test_piece_multibyte_keys(gctx, unit, engine):
     """Equal-length keys of valid 2-, 3- and 4-byte UTF-8 (the key's high bytes send the stripe to
     k_replay's full UTF-8 check), and the same with one invalid sequence mid-store."""
     u = unit.encode()
@@ -155,7 +165,7 @@ def test_piece_multibyte_keys(gctx, unit):
 
 
 @pytest.mark.parametrize("where", ["value", "header", "key"])
-def test_piece_truncated(gctx, where):
+def test_piece_truncated(gctx, where, engine):
     """A segment cut inside the run's last record (its value, its header, its key): the record
     does not fit, k_piece hands back there and k_replay reports engine.rs's VAL / KEY_LEN / KEY."""
     seg = _uniform(2100, 16, 1024)
@@ -163,6 +173,15 @@ def test_piece_truncated(gctx, where):
     for i in [3, 1500, 2099]:
         cut = i * rec + {"value": 600, "header": 3, "key": 11}[where]
         check_parity(gctx, [seg[:cut], _uniform(50, 16, 1024)])
+
+
+@pytest.mark.parametrize("klen", [25, 36, 37, 64, 300])
+@pytest.mark.parametrize("bad", [None, "surrogate", "fourth", "truncated"])
+def test_long_keys(gctx, klen, bad, engine):
+    """Equal records with keys past the 16-B records fast path and the 36-B window (up to 300 B),
+    valid and with a UTF-8 failure 700 records in: the oracle's tuples or first error with aux."""
+    segs = [_uniform(1500, klen, 1000, change=(700, bad) if bad else None)]
+    check_parity(gctx, segs)
 
 
 def test_piece_many_chunks(gctx):
