@@ -136,6 +136,9 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #ifndef KVR_PBAL_D   // the progress band (1/4096 of a run) around the mean of priorities 1 and 2
 #define KVR_PBAL_D 64
 #endif
+#ifndef KVR_PCHECK   // k_piece: records whose headers are checked before a run starts (1: none)
+#define KVR_PCHECK 8
+#endif
 #ifndef KVR_UMIN    // the shortest value the piece mode takes (pieces are 128 B: shorter values waste lanes)
 #define KVR_UMIN 128
 #endif
@@ -2000,6 +2003,27 @@ __global__ __launch_bounds__(RT_REWALK) void k_rewalk(const SegDesc *__restrict_
 }
 
 
+// k_piece's check before a run: records 1 .. KVR_PCHECK - 1 after the one at Pe (those starting
+// before s_hi) are SETs of key length ku and value length vu that fit the segment, one lane each
+// (out of line: inlined, its registers changed the allocation of the step loop, cfg2 +8 %)
+__device__ __attribute__((noinline)) bool run_heads_equal(const uint8_t *base, uint64_t len, uint64_t Pe, uint32_t L,
+                                                          uint32_t ku, uint32_t vu, uint64_t s_hi, int lane) {
+    const uint64_t pj = Pe + (uint64_t)lane * L;
+    bool bad = false;
+    if (lane > 0 && lane < KVR_PCHECK && pj < s_hi) {
+        if (pj + L > len) {
+            bad = true;
+        } else {
+            const __amdgpu_buffer_rsrc_t rj = seg_rsrc(base, pj, len);
+            const uint32_t a = __builtin_amdgcn_raw_buffer_load_b32(rj, 0, 0, 0);   // (unaligned)
+            const uint32_t b = __builtin_amdgcn_raw_buffer_load_b32(rj, 4, 0, 0);
+            const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rj, 5 + (int)ku, 0, 0);
+            bad = (a & 255u) != 0u || ((a >> 8) | (b << 24)) != ku || v != vu;
+        }
+    }
+    return __ballot(bad) == 0ull;
+}
+
 // ---------------------------------------------------------------------------------------
 // k_piece: the piece mode, first over every stripe.
 // ---------------------------------------------------------------------------------------
@@ -2161,6 +2185,9 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     }
     const uint32_t L = 9u + ku + vu;
     const uint32_t P = (vu + (uint32_t)SC - 1u) >> SC_LOG, r = vu - (uint32_t)SC * (P - 1u);
+    // a run shorter than KVR_PCHECK records is not worth the run's setup (a SET/DEL mix like cfg4's
+    // ends most runs at the second record): the next records' headers, one lane each, before it
+    if (uni && KVR_PCHECK > 1) uni = run_heads_equal(sg.base, len, Pe, L, ku, vu, s_hi, lane);
     // (a first piece's window starts 128 - r bytes before its value: inside the segment)
     if (!uni || Pe + 9u + ku + r < (uint64_t)SC || !KVR_UMODE) {
         for (uint32_t t = sd.t_begin + (uint32_t)lane; t < k; t += 64u) {   // the tiles the search passed
