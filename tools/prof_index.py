@@ -29,6 +29,11 @@ for s, (ln, nr), o in zip(range(nseg), sizes, offs):
     eo += nr
 torch.cuda.synchronize()
 segs = [(data.data_ptr() + o, ln) for (ln, _), o in zip(sizes, offs)]
+if len(sys.argv) > 3 and sys.argv[3] == "plain":   # plain replays first (no key prefixes): k_piece with and without
+    out = torch.empty((n_rec + 1024) * 32, dtype=torch.uint8, device="cuda")
+    for i in range(reps):
+        r = ctx.replay(segs, on_device=True, out_ptr=out.data_ptr(), cap=n_rec + 1024)
+        print(f"{cfg} plain replay: ms_replay {r.stats.ms_replay:.3f} ms_total {r.stats.ms_total:.3f}", flush=True)
 for i in range(reps):
     ix = ctx.replay_index(segs, on_device=True)
     st = ix.stats
