@@ -133,6 +133,9 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #ifndef KVR_PBAL   // k_piece: 1 = wave priorities from each wave's progress against its workgroup's mean
 #define KVR_PBAL 1     // (without, oldest-first issue finishes a CU's 16 stripes in 4 waves of 4)
 #endif
+#ifndef KVR_PBAL_EVERY   // k_piece: steps between two balance updates (a power of two)
+#define KVR_PBAL_EVERY 1
+#endif
 #ifndef KVR_PBAL_D   // the progress band (1/4096 of a run) around the mean of priorities 1 and 2
 #define KVR_PBAL_D 64
 #endif
@@ -2428,6 +2431,7 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     const uint64_t pscale = (4096ull << 32) / q_end;
     uint32_t pown = 0;
     if (KVR_PBAL && lane == 0) atomicAdd(&bal[1], 1u);
+    uint32_t bstep = 0;   // (the balance runs every KVR_PBAL_EVERY steps)
     auto balance = [&](uint32_t q_now) {
         const uint32_t pn = (uint32_t)(((uint64_t)q_now * pscale) >> 32);
         uint32_t sum = 0, cnt = 1;
@@ -2463,7 +2467,7 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
         issue(w, q1, p1, g1);   // (issued on every path, the last step's reading nothing: exact wait counts)
         KVR_PSTAMP(2);
         finish_step(raw, q0, p0, g0, qa, qb);
-        if (KVR_PBAL) balance(q1 < q_end ? q1 : q_end);
+        if (KVR_PBAL && (++bstep & (KVR_PBAL_EVERY - 1u)) == 0u) balance(q1 < q_end ? q1 : q_end);
         KVR_PSTAMP(3);
         if (!h1 || ustop) break;
         q0 = q1; p0 = p1; g0 = g1;
