@@ -139,6 +139,9 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #ifndef KVR_PBAL_D   // the progress band (1/4096 of a run) around the mean of priorities 1 and 2
 #define KVR_PBAL_D 64
 #endif
+#ifndef KVR_PSEARCH   // k_piece: tiles it searches for the stripe's entry before handing the search on
+#define KVR_PSEARCH 2
+#endif
 #ifndef KVR_PCHECK   // k_piece: records whose headers are checked before a run starts (1: none)
 #define KVR_PCHECK 8
 #endif
@@ -2104,7 +2107,7 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     uint32_t k = sd.t_begin;
     if (entry == NONE) {
 #pragma unroll 1
-        for (; k < sd.t_end && k < sg.n_tiles; ++k) {
+        for (; k < sd.t_end && k < sg.n_tiles && k < sd.t_begin + KVR_PSEARCH; ++k) {
             load_unit(abase, d0, len, k, lane, w);
             const int64_t lo = (int64_t)k * TILE - d0;
             const int64_t vlo_r = lo < 0 ? -lo : 0;
@@ -2161,6 +2164,17 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
             hand[si] = h;
         }
     };
+    if (entry == NONE && k < sd.t_end && k < sg.n_tiles) {
+        // no record start in the first KVR_PSEARCH tiles (a long value crosses them): k_replay searches
+        // on from tile k (a serial walk over a 1-MiB value here held its whole launch back, cfg5)
+        for (uint32_t t = sd.t_begin + (uint32_t)lane; t < k; t += 64u) {
+            TileRes tr;
+            tr.pool_off = 0; tr.pool_off2 = 0; tr.count = 0; tr.count1 = 0;
+            tres[sg.tile0 + t] = tr;
+        }
+        hand_back(NONE, k, 0u, 0u);
+        return;
+    }
     if (entry == NONE) {   // no record starts in the stripe (or the search ran past its tiles)
         for (uint32_t t = sd.t_begin + (uint32_t)lane; t < sd.t_end; t += 64u) {
             TileRes tr;

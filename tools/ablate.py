@@ -33,6 +33,8 @@ for mask in masks:
     path = os.path.join(ABL, f"libkvreplay_a{mask}.so") if isinstance(mask, int) else os.path.join(VAR, f"libkvreplay_{mask}.so")
     if not isinstance(mask, int) and os.path.exists(os.path.join(AB, f"libkvreplay_{mask}.so")):
         path = os.path.join(AB, f"libkvreplay_{mask}.so")   # an A/B build (tools/build_ab.sh)
+    if mask == "main":   # the shipped library itself
+        path = os.path.join(ROOT, "mini-kvstore-v2_amd", "lib", "libkvreplay.so")
     lib = C.CDLL(path)   # the only kvreplay library in this process
     lib.kvr_ctx_create.argtypes = [C.c_int, C.POINTER(P)]
     lib.kvr_replay.argtypes = [P, C.POINTER(K.Segment), SZ, U32, P, SZ, P, SZ, C.POINTER(SZ), C.POINTER(K.Error)]
