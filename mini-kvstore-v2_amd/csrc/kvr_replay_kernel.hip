@@ -140,7 +140,7 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #define KVR_PBAL_D 64
 #endif
 #ifndef KVR_PSEARCH   // k_piece: tiles it searches for the stripe's entry before handing the search on
-#define KVR_PSEARCH 2
+#define KVR_PSEARCH 16
 #endif
 #ifndef KVR_PCHECK   // k_piece: records whose headers are checked before a run starts (1: none)
 #define KVR_PCHECK 8
