@@ -100,7 +100,7 @@ def _uniform(n_rec, klen, vlen, unit=b"", change=None):
 # (key length, value length): P = ceil(v / 128) pieces a value, the first of r = v - 128 (P - 1)
 # bytes; keys up to 36 B are read from the 48-B header window
 SHAPES = [(16, 1024), (0, 128), (1, 129), (7, 200), (24, 1000), (33, 4096), (36, 8192), (5, 10000),
-          (16, 65536), (37, 1024), (16, 127), (3, 131072)]
+          (16, 65536), (37, 1024), (16, 127), (3, 131072), (9, 300000)]   # (300 KB: entries past KVR_PSEARCH tiles)
 
 
 @pytest.mark.parametrize("tps", [0, 2, 8, 64])
@@ -108,7 +108,9 @@ SHAPES = [(16, 1024), (0, 128), (1, 129), (7, 200), (24, 1000), (33, 4096), (36,
 def test_piece_shapes(gctx, shape, tps):
     """Equal records of every piece geometry (one piece, a one-byte first piece, values of 64 and
     more pieces, keys at the window's limit and past it, values below KVR_UMIN), over stripes of
-    2 to 64 tiles and the automatic layout, and a second segment of another shape behind it."""
+    2 to 64 tiles and the automatic layout, and a second segment of another shape behind it.  With
+    300-KB values most stripes start inside a value more than KVR_PSEARCH tiles from the next record:
+    k_piece hands the entry search on to k_replay."""
     klen, vlen = shape
     n_rec = max(8, (2_400_000 if vlen < 60000 else 6_000_000) // (9 + klen + vlen))
     segs = [_uniform(n_rec, klen, vlen), _uniform(300, 9, 1500)]
