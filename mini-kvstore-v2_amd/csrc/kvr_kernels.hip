@@ -332,8 +332,17 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
         if (ov) return;
         const uint32_t s = blockIdx.x;
         if (threadIdx.x == 0) s_ok = stripe_links(segs, stripes, sres, s, tile) ? 1u : 0u;
+        // (16-B loads, four counts each, unrolled: one or two round trips at 4096 stripes instead
+        // of one per 256 counts)
         unsigned long long a = 0;
-        for (uint32_t i = threadIdx.x; i < s; i += CT) a += scnt[i];
+        const uint32_t s4 = s >> 2;
+        const uint4 *const sc4 = reinterpret_cast<const uint4 *>(scnt);
+#pragma unroll 4
+        for (uint32_t i = threadIdx.x; i < s4; i += CT) {
+            const uint4 v = sc4[i];
+            a += (unsigned long long)v.x + v.y + v.z + v.w;
+        }
+        for (uint32_t i = (s4 << 2) + threadIdx.x; i < s; i += CT) a += scnt[i];
         for (int d = 32; d >= 1; d >>= 1) a += __shfl_xor(a, d, 64);
         if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = a;
         __syncthreads();
