@@ -732,12 +732,51 @@ __global__ void k_live_ent(const FoldEnt *__restrict__ ent, const uint32_t *__re
 // tuple: the flags are nt bytes, against 8 B a tuple for the packed scan this replaces.
 constexpr int DL_T = 256, DL_PER = 16, DL_CH = DL_T * DL_PER;   // tuples per block: 4096
 __device__ __forceinline__ uint64_t rec_size(const kvr_tuple &t) { return 9ull + t.key_len + t.val_len; }   // engine.rs:169-173
+#ifndef KVR_DL_BATCH   // 1: the dense-list kernels load their live tuples four at a time (A/B knob, round 5)
+#define KVR_DL_BATCH 0
+#endif
+// the thread's 16 flags as a bit mask (bit k: tuple i0 + k is live)
+__device__ __forceinline__ uint32_t dl_bits(const uint4 f) {
+    const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
+    uint32_t b = 0;
+#pragma unroll
+    for (int k = 0; k < DL_PER; ++k) b |= ((fw[k >> 2] >> (8 * (k & 3))) & 255u) ? 1u << k : 0u;
+    return b;
+}
+// the next four live tuples of the mask (-1: none), taken off it
+__device__ __forceinline__ void dl_next4(uint32_t &bits, int (&kk)[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        kk[q] = bits ? __builtin_ctz(bits) : -1;
+        bits &= bits ? bits - 1u : 0u;
+    }
+}
 // (flags of the thread's 16 tuples: flag8 holds nt bytes rounded up to DL_CH, zero past nt)
 __device__ __forceinline__ uint4 dl_flags(const uint8_t *flag8, uint64_t i0) {
     return *reinterpret_cast<const uint4 *>(flag8 + i0);
 }
 // the thread's live count and bytes over its 16 tuples (tup null: the count alone)
 __device__ __forceinline__ void dl_sums(const uint4 f, const kvr_tuple *tup, uint64_t i0, uint32_t &c, uint64_t &by) {
+#if KVR_DL_BATCH
+    uint32_t bits = dl_bits(f);
+    c = (uint32_t)__builtin_popcount(bits);
+    by = 0;
+    if (!tup) return;
+    while (bits) {   // (the live tuples' lengths four at a time, their loads issued together)
+        int kk[4];
+        dl_next4(bits, kk);
+        uint32_t kl[4], vl[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const kvr_tuple *t = tup + i0 + (uint64_t)(kk[q] >= 0 ? kk[q] : kk[0]);
+            kl[q] = t->key_len;
+            vl[q] = t->val_len;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) by += kk[q] >= 0 ? 9ull + kl[q] + vl[q] : 0ull;   // engine.rs:169-173
+    }
+    return;
+#endif
     const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
     c = 0;
     by = 0;
@@ -844,6 +883,29 @@ __global__ void __launch_bounds__(DL_T) k_dl_fill(const uint8_t *__restrict__ fl
     dl_block_scan(c, by, tc, tby);
     if (tc == 0) return;
     uint64_t d = (uint64_t)bcnt[blockIdx.x] + c, o = bbytes[blockIdx.x] + by;
+#if KVR_DL_BATCH
+    uint32_t bits = dl_bits(f);
+    while (bits) {   // (four live tuples at a time, their loads issued together ahead of the branches)
+        int kk[4];
+        dl_next4(bits, kk);
+        kvr_tuple t[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[q] = tup[i0 + (uint64_t)(kk[q] >= 0 ? kk[q] : kk[0])];
+        asm volatile("" ::"v"(t[0].rec_off), "v"(t[0].seg_idx), "v"(t[0].key_len), "v"(t[0].val_len),
+                     "v"(t[1].rec_off), "v"(t[1].seg_idx), "v"(t[1].key_len), "v"(t[1].val_len),
+                     "v"(t[2].rec_off), "v"(t[2].seg_idx), "v"(t[2].key_len), "v"(t[2].val_len),
+                     "v"(t[3].rec_off), "v"(t[3].seg_idx), "v"(t[3].key_len), "v"(t[3].val_len));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (kk[q] < 0) break;
+            l_src[d] = reinterpret_cast<uint64_t>(segs[t[q].seg_idx].base + t[q].rec_off);
+            l_off[d] = o;
+            ++d;
+            o += rec_size(t[q]);
+        }
+    }
+    return;
+#endif
     const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
 #pragma unroll
     for (int k = 0; k < DL_PER; ++k) {
@@ -872,6 +934,32 @@ __global__ void __launch_bounds__(DL_T) k_dl_fill_tup(const uint8_t *__restrict_
     dl_block_scan(c, by, tc, tby);
     if (tc == 0) return;
     uint32_t d = bcnt[blockIdx.x] + c;
+#if KVR_DL_BATCH
+    uint32_t bits = dl_bits(f);
+    while (bits) {   // (four live tuples at a time, their loads issued together ahead of the branches)
+        int kk[4];
+        dl_next4(bits, kk);
+        u32x4 t[4][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const u32x4 *src = reinterpret_cast<const u32x4 *>(tup + i0 + (uint64_t)(kk[q] >= 0 ? kk[q] : kk[0]));
+            t[q][0] = src[0];
+            t[q][1] = src[1];
+        }
+        asm volatile("" ::"v"(t[0][0]), "v"(t[0][1]), "v"(t[1][0]), "v"(t[1][1]), "v"(t[2][0]), "v"(t[2][1]),
+                     "v"(t[3][0]), "v"(t[3][1]));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (kk[q] < 0) break;
+            u32x4 *dst = reinterpret_cast<u32x4 *>(out + d);
+            dst[0] = t[q][0];
+            dst[1] = t[q][1];
+            pos[i0 + kk[q]] = d;
+            ++d;
+        }
+    }
+    return;
+#endif
     const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
 #pragma unroll
     for (int k = 0; k < DL_PER; ++k) {
