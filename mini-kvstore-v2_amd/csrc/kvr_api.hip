@@ -766,6 +766,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
                 HIPCHK(hipEventRecord(c->ev[4], st));
                 launch_compact(false, c->ev[3]);
                 HIPCHK(hipGetLastError());
+                if (markers) HIPCHK(hipEventRecord(c->ev[3], st));   // (no dispatch stamp in markers mode)
                 HIPCHK(wait_stream(st, c->ev[5]));
                 relinked = true;
             } else {

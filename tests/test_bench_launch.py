@@ -35,6 +35,17 @@ def test_gpus2_spawns_two_ranks_and_reports_slowest():
     assert res["ms_per_step"] >= 2.0
 
 
+def test_gpus8_spawns_eight_ranks():
+    """The driver's widest launch (--gpus 8, one rank per GPU of a node), dry-run on CPU."""
+    r = _bench("--gpus", "8", "--dry-run", "--steps", "5", "--warmup", "1")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 8 and sorted(p["rank"] for p in res["per_rank"]) == list(range(8))
+    assert res["ms_per_step"] >= 8.0             # rank 7 sleeps 8 ms a step
+
+
 def test_single_gpu_default_and_world_mismatch():
     r = _bench("--dry-run", "--steps", "3", "--warmup", "0")
     assert r.returncode == 0, r.stderr[-2000:]

@@ -185,3 +185,35 @@ def test_live_multi_device_resident_with_keys(devices):
         m.close()
         for g in gens.values():
             g.close()
+
+
+@pytest.mark.parametrize("devices", device_lists(8))
+def test_eight_way_cfg4_shape(devices):
+    """The target width (BASELINE cfg4: segments dealt round-robin over 8 GPUs, 50 % tombstones):
+    16 segments over 8 contexts, so each shard holds two segments and a key SET in one shard is
+    deleted in others.  kvr_replay_live_multi equals the oracle's fold of the whole store
+    (engine.rs:137 / :141), kvr_replay_multi its tuples, and the store's first error is the
+    minimum (segment, offset) over the shards (engine.rs:56)."""
+    spec = K.GenSpec(seed=0xC4F8, seg_bytes=200_000, key_space_log2=10, val_min=0, val_max=1024, del_permille=500)
+    n = 16
+    ids = [3 * i + 1 for i in range(n)]
+    segs = [K.gen_segment_cpu(spec, s)[0].tobytes() for s in range(n)]
+    rc, t, _ = O.replay(segs, seg_ids=ids)
+    live, nk, tb = O.fold_live(segs, t)
+    assert rc == 0 and tb > 0
+    m = K.MultiContext(devices)
+    try:
+        r = m.replay(segs, seg_ids=ids, live=True)
+        assert r.status == 0 and r.n == nk and np.array_equal(r.tuples, t[live])
+        assert r.stats.n_shards == 8
+        r = m.replay(segs, seg_ids=ids)
+        assert r.status == 0 and np.array_equal(r.tuples, t)
+        bad = list(segs)
+        bad[13] = bad[13][:-2]     # shard 5
+        bad[6] = bad[6][:-1]       # shard 6, earlier in the store: the store's error
+        rcb, _, err = O.replay(bad, seg_ids=ids)
+        r = m.replay(bad, seg_ids=ids, live=True)
+        assert r.status == rcb == K.CORRUPTED and err.seg_idx == 6
+        assert (r.error.kind, r.error.seg_idx, r.error.rec_off, r.error.aux) == (err.kind, err.seg_idx, err.rec_off, err.aux)
+    finally:
+        m.close()

@@ -80,6 +80,15 @@ def test_two_rank_gloo_merge_matches_single(tmp_path):
     assert float(rest.split()[-1]) == 0.5                     # max over ranks, not rank 0's own time
 
 
+def test_eight_rank_gloo_merge_matches_single(tmp_path):
+    """The target width (8 ranks, one per GPU of a node) with fewer segments than ranks would leave
+    ranks empty: N_SEGS = 7 over 8 ranks, so rank 7 owns nothing and still joins the gather."""
+    st, merged, rest = _run(8, (), tmp_path)
+    rc, ref, _ = O.replay(_segments())
+    assert st == K.OK and rc == K.OK and np.array_equal(merged, ref)
+    assert float(rest.split()[-1]) == 2.0                     # the slowest of 8 ranks (0.25 * 8)
+
+
 def test_two_rank_gloo_first_error_is_global_minimum(tmp_path):
     # segment 3 (rank 1) and segment 4 (rank 0) are both torn: the store's error is segment 3's
     st, _, rest = _run(2, (3, 4), tmp_path)
@@ -124,7 +133,7 @@ def _expected_split(segs, world):
     return [bytes(b) for b in out]
 
 
-@pytest.mark.parametrize("world,target", [(2, 0), (2, 5000), (3, 0)])
+@pytest.mark.parametrize("world,target", [(2, 0), (2, 5000), (3, 0), (8, 0)])
 def test_sharded_compaction_gloo(world, target, tmp_path):
     mp.start_processes(_compact_rank_main, args=(world, _free_port(), target, str(tmp_path)), nprocs=world,
                        join=True, start_method="spawn")

@@ -226,3 +226,71 @@ def test_piece_index_and_keys(gctx):
     rc, t, _ = O.replay(segs)
     live, nk, _ = O.fold_live(segs, t)
     assert rc == 0 and len(ix.live) == nk and np.array_equal(ix.live, t[live])
+
+
+# ---- k_piece at device bases of every alignment (KVR_SEGS_ON_DEVICE: the caller's pointers) ----
+ALIGN_SHAPES = [(16, 1024), (0, 128), (36, 8192), (16, 65536)]
+
+
+def _dev_place(segs, base_off):
+    """Copy segs into one device buffer, segment i at an address = base_off (mod 256)."""
+    torch = pytest.importorskip("torch")
+    tot = sum((len(s) + 511) & ~255 for s in segs) + 512
+    buf = torch.zeros(tot, dtype=torch.uint8, device="cuda")
+    ptrs, off = [], base_off
+    for s in segs:
+        if len(s):
+            buf[off: off + len(s)] = torch.from_numpy(np.frombuffer(s, dtype=np.uint8).copy()).cuda()
+        ptrs.append((buf.data_ptr() + off, len(s)))
+        off = ((off + len(s) + 255) & ~255) + base_off
+    torch.cuda.synchronize()
+    return buf, ptrs
+
+
+def check_parity_dev(ctx, segs, base_off):
+    buf, ptrs = _dev_place(segs, base_off)
+    assert all(p % 256 == base_off % 256 for p, _ in ptrs)
+    ro = O.replay(segs)
+    rg = ctx.replay(ptrs, on_device=True)
+    assert rg.status == ro[0], (base_off, rg.status, ro[0], ro[2].kind, ro[2].rec_off)
+    if ro[0] == 0:
+        a, b = rg.tuples, ro[1]
+        assert rg.n == len(b)
+        if not np.array_equal(a, b):
+            bad = np.nonzero(a != b)[0][:5]
+            raise AssertionError(f"base+{base_off}: tuple mismatch at {bad}: gpu={a[bad]} oracle={b[bad]}")
+    else:
+        eo, eg = ro[2], rg.error
+        assert (eg.kind, eg.seg_idx, eg.rec_off, eg.aux) == (eo.kind, eo.seg_idx, eo.rec_off, eo.aux), base_off
+    del buf
+
+
+@functools.lru_cache(maxsize=None)
+def _align_store(klen, vlen):
+    """Uniform segments of one shape: clean, and with a record not as predicted (a DEL, another
+    value length) at records 0, 64 and 530 (every index inside the store)."""
+    n_rec = max(600, 2_400_000 // (9 + klen + vlen))
+    segs = [_uniform(n_rec, klen, vlen)]
+    for i, kind in [(0, "del"), (64, "vlen"), (530, "del")]:
+        segs.append(_uniform(n_rec, klen, vlen, change=(i, kind)))
+    return segs
+
+
+@pytest.mark.parametrize("tps", [0, 2, 64])
+@pytest.mark.parametrize("shape", ALIGN_SHAPES, ids=[f"k{k}v{v}" for k, v in ALIGN_SHAPES])
+@pytest.mark.parametrize("base_off", [1, 2, 3, 5, 13, 255])
+def test_piece_device_alignment(gctx, shape, tps, base_off, engine):
+    """Uniform stores replayed from device buffers whose base is base_off bytes past a 256-B
+    boundary (SegDesc.d0 and the piece windows' dword realignment at every residue): clean, with
+    hand-backs at records 0, 64 and 530, and cut inside the last record (the first error).  The
+    tiles of a stripe and k_piece's hand-back tile depend on the base, so each case runs over
+    stripes of 2 and 64 tiles and the automatic layout, under both engines."""
+    klen, vlen = shape
+    segs = _align_store(klen, vlen)
+    gctx.set_tiles_per_stripe(tps)
+    try:
+        check_parity_dev(gctx, list(segs), base_off)
+        cut = segs[0][: len(segs[0]) - (vlen // 2)]        # the last record's value cut in half
+        check_parity_dev(gctx, [segs[1], cut], base_off)
+    finally:
+        gctx.set_tiles_per_stripe(0)

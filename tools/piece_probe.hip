@@ -74,13 +74,13 @@ __device__ __forceinline__ uint32_t fold(const uint32_t (&w)[33], int off) {
     return x;
 }
 
-template <int PAT, int DEPTH>
-__global__ __launch_bounds__(RT) void k_pat(const uint8_t *__restrict__ buf, uint64_t bytes_per_stripe,
+template <int PAT, int DEPTH, int NT = RT>
+__global__ __launch_bounds__(NT) void k_pat(const uint8_t *__restrict__ buf, uint64_t bytes_per_stripe,
                                             uint32_t n_stripes, int delay, uint32_t *sink) {
     __shared__ uint32_t pin[130 * 1024 / 4];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (threadIdx.x == 0) pin[0] = 0;
-    const uint32_t si = blockIdx.x * (RT / 64) + __builtin_amdgcn_readfirstlane(wv);
+    const uint32_t si = blockIdx.x * (NT / 64) + __builtin_amdgcn_readfirstlane(wv);
     if (si >= n_stripes) return;
     const uint8_t *p = buf + (uint64_t)si * bytes_per_stripe;
     // a step: 64 pieces.  tile: 8 KiB.  piece: 8 records of 1049 B (8 pieces each)
@@ -88,12 +88,30 @@ __global__ __launch_bounds__(RT) void k_pat(const uint8_t *__restrict__ buf, uin
     const int off = PAT == 0 ? 128 * lane : (lane >> 3) * 1049 + 25 + 128 * (lane & 7);
     const uint64_t n_steps = (bytes_per_stripe - 1100) / step_bytes;
     uint32_t acc = 0;
-    uint32_t a[33], b[33];
+    uint32_t a[33], b[33], c[33];
     auto rsrc = [&](uint64_t s) {   // (a step past the stripe re-reads the last one: never out of the buffer)
         s = s < n_steps ? s : n_steps - 1;
         return __builtin_amdgcn_make_buffer_rsrc((void *)(p + s * step_bytes), (short)0, (int)(step_bytes + 1100), 0x00020000);
     };
     load_step<PAT>(rsrc(0), off, a);
+    if (DEPTH == 3) {   // three buffers: two steps in flight while one is worked on
+        load_step<PAT>(rsrc(1), off, b);
+#pragma unroll 1
+        for (uint64_t s = 0; s < n_steps; s += 3) {
+            load_step<PAT>(rsrc(s + 2), off, c);
+            asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+            acc ^= spin(fold<PAT>(a, off), acc, delay);
+            load_step<PAT>(rsrc(s + 3), off, a);
+            asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+            acc ^= spin(fold<PAT>(b, off), acc, delay);
+            load_step<PAT>(rsrc(s + 4), off, b);
+            asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+            acc ^= spin(fold<PAT>(c, off), acc, delay);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (acc == 0x12345678u) sink[threadIdx.x] = acc + pin[0];
+        return;
+    }
 #pragma unroll 1
     for (uint64_t s = 0; s < n_steps; s += 2) {
         if (DEPTH == 2) {
@@ -119,16 +137,16 @@ __global__ __launch_bounds__(RT) void k_pat(const uint8_t *__restrict__ buf, uin
     if (acc == 0x12345678u) sink[threadIdx.x] = acc + pin[0];
 }
 
-template <int PAT, int DEPTH>
+template <int PAT, int DEPTH, int NT = RT>
 static void run(const uint8_t *d, uint64_t bytes, int cus, int delay, uint32_t *sink) {
-    const uint32_t n_stripes = cus * 16;
+    const uint32_t n_stripes = cus * (NT / 64);
     const uint64_t bps = bytes / n_stripes;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     float best = 1e9f;
     for (int it = 0; it < 6; ++it) {
         CK(hipEventRecord(e0));
-        k_pat<PAT, DEPTH><<<cus, RT>>>(d, bps, n_stripes, delay, sink);
+        k_pat<PAT, DEPTH, NT><<<cus, NT>>>(d, bps, n_stripes, delay, sink);
         const hipError_t le = hipGetLastError();
         if (le != hipSuccess) { printf("launch: %s\n", hipGetErrorString(le)); return; }
         CK(hipEventRecord(e1));
@@ -138,7 +156,7 @@ static void run(const uint8_t *d, uint64_t bytes, int cus, int delay, uint32_t *
         if (it > 0 && ms < best) best = ms;
     }
     const char *nm[] = {"tile", "piece-u", "piece-a"};
-    printf("%-8s depth %d delay %4d VALU: %.3f ms  %7.1f GB/s\n", nm[PAT], DEPTH, delay, best, bytes / best / 1e6);
+    printf("%-8s waves %2d depth %d delay %4d VALU: %.3f ms  %7.1f GB/s\n", nm[PAT], NT / 64, DEPTH, delay, best, bytes / best / 1e6);
 }
 
 int main(int argc, char **argv) {
@@ -175,6 +193,17 @@ int main(int argc, char **argv) {
         const uint64_t bps = bytes / n_stripes, n_steps = (bps - 1100) / (8u * 1049u);
         run<2, 2>(d, bytes, cus, 0, sink);
         printf("calib_bytes_per_dispatch=%llu\n", (unsigned long long)(n_stripes * n_steps * 8u * 1049u));
+        return 0;
+    }
+    if (argc > 1 && strcmp(argv[1], "waves") == 0) {   // waves per CU x pieces in flight (round 6)
+        for (int delay : {256, 512, 1024, 1536}) {
+            run<2, 1>(d, bytes, cus, delay, sink);
+            run<2, 2>(d, bytes, cus, delay, sink);
+            run<2, 2, 768>(d, bytes, cus, delay, sink);
+            run<2, 3, 768>(d, bytes, cus, delay, sink);
+            run<2, 2, 512>(d, bytes, cus, delay, sink);
+            run<2, 3, 512>(d, bytes, cus, delay, sink);
+        }
         return 0;
     }
     for (int delay : {0, 256, 512}) {
