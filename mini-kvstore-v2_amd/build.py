@@ -107,6 +107,17 @@ VARIANTS = {
     "u1": ["-DKVR_FP_U=1"],      # k_fold_lds: one record per thread and step
     "u2": ["-DKVR_FP_U=2"],
     "fp4": ["-DKVR_FP_PER=4"],   # k_fold_part: 4 tuples per thread (4096-record regions; neutral)
+    # k_piece's workgroup x piece buffers (round 6): 16 waves x 1 buffer is round 5's kernel
+    "p1024x1": ["-DKVR_PNT=1024", "-DKVR_PNB=1"],
+    "p1024x2": ["-DKVR_PNT=1024", "-DKVR_PNB=2"],
+    "p512x2": ["-DKVR_PNT=512", "-DKVR_PNB=2"],
+    "p512x3": ["-DKVR_PNT=512", "-DKVR_PNB=3"],
+    # k_piece ablations (KVR_PABLATE: results wrong by design, timing only)
+    "pa1": ["-DKVR_PABLATE=1"], "pa2": ["-DKVR_PABLATE=2"], "pa11": ["-DKVR_PABLATE=11"],
+    "pa16": ["-DKVR_PABLATE=16"], "pa59": ["-DKVR_PABLATE=59"], "pnb": ["-DKVR_PBAL=0"],
+    "pa128": ["-DKVR_PABLATE=128"], "pa256": ["-DKVR_PABLATE=256"], "pa512": ["-DKVR_PABLATE=512"],
+    "pa1536": ["-DKVR_PABLATE=1536"], "pa1920": ["-DKVR_PABLATE=1920"],
+    "pa2048": ["-DKVR_PABLATE=2048"], "pa4096": ["-DKVR_PABLATE=4096"], "pw1": ["-DKVR_PWIDE=1", "-DKVR_PRUNFORM=0"], "prf0": ["-DKVR_PRUNFORM=0"], "pa8192": ["-DKVR_PABLATE=8192"], "pa16384": ["-DKVR_PABLATE=16384"],
 }
 
 

@@ -130,6 +130,8 @@ struct kvr_ctx {
     DevBuf<uint64_t> soff;                 // each stripe's output offset (k_link, for k_compact_s)
     DevBuf<uint32_t> scnt;                 // each stripe's record count, dense (k_replay, for linked k_compact_s)
     DevBuf<PieceHand> hand;                // k_piece -> k_replay: where each stripe's tile loop resumes
+    DevBuf<PieceRun> prun;                 // k_piece -> k_compact_s: each stripe's records in run form
+    DevBuf<uint2> pcrc;                    // ... their value CRCs and key tags, by pool slot
     DevBuf<uint32_t> crc, kmul, initx;
     DevBuf<GenRecDev> gen;
     // compaction (kvr_compact)
@@ -627,7 +629,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
 
     if (c->segs.ensure(n) || c->stripes.ensure(n_stripes) || c->sres.ensure(n_stripes) ||
         c->tres.ensure(n_tiles) || c->redo.ensure(std::max<uint32_t>(n_stripes, REDO_GRID)) ||
-        c->seg_bad.ensure(n) || c->seg_err.ensure(n) || c->soff.ensure(n_stripes) || c->scnt.ensure(n_stripes) || c->hand.ensure(n_stripes))
+        c->seg_bad.ensure(n) || c->seg_err.ensure(n) || c->soff.ensure(n_stripes) || c->scnt.ensure(n_stripes) || c->hand.ensure(n_stripes) || c->prun.ensure(n_stripes))
         return KVR_ENOMEM;
     // (the same segments as the last call: the descriptors on the device are still these)
     if (c->up_segs_p != c->segs.p || c->up_segs.size() != n ||
@@ -669,7 +671,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             c->pool_need = pool_cap;
             return KVR_ENOMEM;
         }
-        if (c->pool.ensure(pool_cap + POOL_SLACK)) return KVR_ENOMEM;
+        if (c->pool.ensure(pool_cap + POOL_SLACK) || c->pcrc.ensure(pool_cap + POOL_SLACK)) return KVR_ENOMEM;
         uint4 *kp = nullptr;               // key prefixes (calls that fold, device output only)
         if (c->kout && (flags & KVR_OUT_ON_DEVICE)) {
             if (c->kpool.ensure(pool_cap + POOL_SLACK)) return KVR_ENOMEM;
@@ -700,13 +702,17 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         // rocprofv3 reads them) time k_replay and the pipeline: no marker packets between the
         // kernels.  KVR_EVENT_MARKERS=1 records separate events instead (timing knob)
         const bool markers = getenv_flag("KVR_EVENT_MARKERS");
+        // k_piece takes every stripe first (runs of equal SETs, value-aligned) and hands the rest of a
+        // stripe to k_replay's tile loop; ms_replay spans both
+        const bool piece = !getenv_flag("KVR_NO_PIECE");
         auto launch_compact = [&](bool lk, hipEvent_t stop) {
             hipExtLaunchKernelGGL(k_compact_s, dim3(n_stripes), dim3(CT), 0, st, nullptr, markers ? nullptr : stop, 0u,
                                c->segs.p, c->stripes.p, c->sres.p, c->soff.p,
                                c->tres.p, c->pool.p, pool_cap, d_out, out_cap, d_exp,
                                (uint64_t)(d_exp ? n_expected : 0), c->ctr.p, c->link.p, kp, kp ? c->kout : nullptr,
                                kp ? reinterpret_cast<uint32_t *>(ktk) : nullptr, c->h_ctr,
-                               lk ? c->scnt.p : nullptr, n_stripes, (uint32_t)KR_TILE, lc_next);
+                               lk ? c->scnt.p : nullptr, n_stripes, (uint32_t)KR_TILE, lc_next,
+                               piece ? c->prun.p : nullptr, c->pcrc.p);
         };
         auto launch_link = [&]() {
             hipLaunchKernelGGL(k_link, dim3(1), dim3(LT), 0, st, c->segs.p, (uint32_t)n, c->stripes.p, n_stripes, c->sres.p,
@@ -723,13 +729,11 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             c->h_ctr->overflow = 0;
         }
         if (markers) HIPCHK(hipEventRecord(c->ev[0], st));
-        // k_piece takes every stripe first (runs of equal SETs, value-aligned) and hands the rest of a
-        // stripe to k_replay's tile loop; ms_replay spans both
-        const bool piece = !getenv_flag("KVR_NO_PIECE");
         if (piece) {
-            hipExtLaunchKernelGGL(k_piece, dim3((n_stripes + KR_WPB - 1) / KR_WPB), dim3(KR_RT), 0, st,
+            hipExtLaunchKernelGGL(k_piece, dim3((n_stripes + KR_WPB - 1) / KR_WPB), dim3(PNT), 0, st,
                                   markers ? nullptr : c->ev[0], nullptr, 0u, c->segs.p, c->stripes.p, n_stripes, c->sres.p,
-                                  c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, pool_chunk, kp, c->scnt.p, c->hand.p);
+                                  c->tres.p, c->pool.p, pool_cap, c->ctr.p, tb, pool_chunk, kp, c->scnt.p, c->hand.p,
+                                  c->pcrc.p, c->prun.p);
             HIPCHK(hipGetLastError());
         }
         hipExtLaunchKernelGGL(KR_KERNEL, dim3((n_stripes + KR_WPB - 1) / KR_WPB), dim3(KR_RT), 0, st,

@@ -87,6 +87,16 @@ struct PieceHand {        // k_piece -> k_replay, one per stripe: where the tile
 };
 static_assert(sizeof(PieceHand) == 56, "PieceHand layout");
 
+// k_piece -> k_compact_s, one per stripe: the records of the stripe's run that k_piece left in the pool
+// in run form.  Pool slots [first, first + n) hold record q = slot - first of the run, a SET at
+// Pe + q L with key length ku and value length vu in segment seg; its value CRC and key tag are in
+// pcrc[slot] (8 B), no 32-B tuple is written for it (k_compact_s builds the tuple)
+struct PieceRun {
+    uint64_t Pe;
+    uint32_t L, first, n, ku, vu, seg;
+};
+static_assert(sizeof(PieceRun) == 32, "PieceRun layout");
+
 struct LinkResult {
     int32_t  status;      // 0 ok, 1 corrupted, 3 unresolved (re-walk needed)
     uint32_t n_redo;

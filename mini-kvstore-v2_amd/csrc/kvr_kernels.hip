@@ -318,7 +318,8 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
                                                   const uint4 *__restrict__ kpool, uint4 *__restrict__ kout,
                                                   uint32_t *__restrict__ ktk, Counters *hctr,
                                                   const uint32_t *__restrict__ scnt, uint32_t n_stripes, uint32_t tile,
-                                                  uint4 *__restrict__ lc_next) {
+                                                  uint4 *__restrict__ lc_next, const PieceRun *__restrict__ prun,
+                                                  const uint2 *__restrict__ pcrc) {
     __shared__ uint64_t off[CB + 1];
     __shared__ uint64_t part[CT];
     __shared__ uint32_t s_ok;
@@ -360,9 +361,23 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
     uint32_t fails = 0;
     // the tuple of output slot o from pool slot src: half k2 & 1 per thread, the manifest check
     // on the second half (a SET: op in byte 0 of w), the key prefix beside it
+    // (the stripe's records k_piece left in run form: the tuple from the run and pcrc)
+    const PieceRun pr = prun ? prun[blockIdx.x] : PieceRun{0ull, 0u, 0u, 0u, 0u, 0u, 0u};
     auto move = [&](uint64_t src, uint64_t o, uint32_t half) {
         if (src >= pool_cap) return;
-        uint4 v = reinterpret_cast<const uint4 *>(pool + src)[half];
+        uint4 v;
+        const uint64_t q = src - pr.first;
+        if (q < pr.n) {
+            if (half) {
+                const uint2 c = pcrc[src];
+                v = make_uint4(pr.vu, c.x, c.y, 0u);
+            } else {
+                const uint64_t ro = pr.Pe + q * pr.L;
+                v = make_uint4((uint32_t)ro, (uint32_t)(ro >> 32), pr.seg, pr.ku);
+            }
+        } else {
+            v = reinterpret_cast<const uint4 *>(pool + src)[half];
+        }
         if (half && expected && o < n_expected && (v.w & 255u) == 0u) {
             v.w |= KVR_TF_VERIFIED << 8;
             if (expected[o] != v.y) { v.w |= KVR_TF_CRC_FAIL << 8; ++fails; }

@@ -84,6 +84,25 @@ struct __align__(16) Smem {
     uint32_t KQL[8 * 16 * KQL_PITCH];     // [i][n][q]: (n << 4i) * x^(8*4q), q per lane (columns > SC/4: 0)  see kmul_col)
 };
 constexpr uint32_t KR_OFF = (uint32_t)offsetof(Smem, KR), KQL_OFF = (uint32_t)offsetof(Smem, KQL);
+// k_piece's LDS: the tables it reads (no KQL, no MK) and, per wave, the header windows of
+// the records in its group (WROW[wave][dword][lane]: lane j holds record qg + j's window, written when
+// it has landed, read back by the group's flush), so the windows hold no registers across the CRC
+#ifndef KVR_PWMAX   // k_piece's waves per workgroup the LDS is laid out for
+#define KVR_PWMAX 16
+#endif
+constexpr int PWIN = 13;                  // dwords of a header window (48 B from its first byte, realigned)
+struct __align__(16) SmemP {
+    uint32_t KQ2[2 * 8 * 16];
+    uint32_t KQ4[2 * 8 * 16];
+    uint32_t IX[NIX + 3];
+    uint32_t BAL[4];
+    uint32_t C2[256 * 64];
+    uint32_t KR[8 * 16 * KR_PITCH];
+    uint32_t WROW[KVR_PWMAX][PWIN][64];
+};
+constexpr uint32_t KR_OFF_P = (uint32_t)offsetof(SmemP, KR);
+static_assert(offsetof(SmemP, C2) < 65536 && KR_OFF_P >= 65536, "k_piece's tables: ds_read immediates, kmul_col's 64-KiB bit");
+static_assert(sizeof(SmemP) <= 163840, "k_piece's LDS");
 static_assert(offsetof(Smem, C2) < 65536, "the byte tables' base fits a ds_read immediate");
 static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit");
 
@@ -128,7 +147,9 @@ static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit
 #endif
 #ifndef KVR_PABLATE   // diagnostic builds of k_piece only (results wrong): 1 no CRC, 2 no push + scan, 8 no
 #define KVR_PABLATE 0   // realignment, 16 no verification or emission (flush only advances), 32 window loads
-                        // past the resource (no memory access), 64 no window load instructions (32, 64 only with 16)
+                        // past the resource (no memory access), 64 no window load instructions (32, 64 only with 16),
+                        // 128 no tuple stores, 256 no key CRC, 512 every record as predicted, 1024 no window reads
+                        // from LDS (with 512)
 #endif
 #ifndef KVR_PBAL   // k_piece: 1 = wave priorities from each wave's progress against its workgroup's mean
 #define KVR_PBAL 1     // (without, oldest-first issue finishes a CU's 16 stripes in 4 waves of 4)
@@ -404,8 +425,8 @@ __device__ __forceinline__ uint32_t kmul(uint32_t v, const uint32_t *K) {
 // the nibble, so lanes that share a column (the pieces of different values pushed the same
 // distance, KR) conflict; PITCH 66 puts entry (n, k) in bank 2 n + k: one v_perm (the row byte)
 // and one v_mad_u32_u24 a lookup.
-template <uint32_t OFF, int PITCH = 64>
-__device__ __forceinline__ uint32_t kmul_col(uint32_t v, const Smem &S, uint32_t k4) {
+template <uint32_t OFF, int PITCH = 64, class SM = Smem>
+__device__ __forceinline__ uint32_t kmul_col(uint32_t v, const SM &S, uint32_t k4) {
     const uint32_t L4k = k4 | 0x10000u;
     // plane 0: nibbles i = 0, 2, 4, 6 (byte j: i = 2j), plane 1: i = 1, 3, 5, 7
     uint32_t pl[2] = {(v & 0x0F0F0F0Fu) | 0x60402000u, ((v >> 4) & 0x0F0F0F0Fu) | 0x70503010u};
@@ -847,7 +868,8 @@ __device__ __forceinline__ void piece_align(uint32_t (&w)[UW + 1], int o) {
 // leading zeros leave a register of 0 unchanged, so such a lane restarts its chain at word zb / 4 with
 // that word's leading bytes masked (the uniform step index makes the restart one select), and the
 // chain over words 0-15 contributes nothing when the restart is in the second half.
-__device__ __forceinline__ uint32_t piece_raw(const uint32_t (&w)[UW + 1], const Crc &K, const Smem &S, bool on,
+template <class SM>
+__device__ __forceinline__ uint32_t piece_raw(const uint32_t (&w)[UW + 1], const Crc &K, const SM &S, bool on,
                                               uint32_t zb) {
     constexpr int H = UW / 2;
     const uint32_t zw = zb >> 2, pm = ~0u << (8u * (zb & 3u));
@@ -871,7 +893,8 @@ __device__ __forceinline__ uint32_t piece_raw(const uint32_t (&w)[UW + 1], const
 }
 // piece_raw with four chains of eight words (half the dependent LDS steps of two chains of sixteen),
 // combined as c0 x^(8*96) ^ c1 x^(8*64) ^ c2 x^(8*32) ^ c3
-__device__ __forceinline__ uint32_t piece_raw4(const uint32_t (&w)[UW + 1], const Crc &K, const Smem &S) {
+template <class SM>
+__device__ __forceinline__ uint32_t piece_raw4(const uint32_t (&w)[UW + 1], const Crc &K, const SM &S) {
     constexpr int Q = UW / 4;
     uint32_t x0 = w[0], x1 = w[Q], x2 = w[2 * Q], x3 = w[3 * Q], c0 = 0, c1 = 0, c2 = 0, c3 = 0;
 #pragma unroll
@@ -967,6 +990,18 @@ __device__ __forceinline__ void stage_tables(Smem &S, const Tables &tb, int tid)
     for (int i = tid; i < 8 * 16 * KQL_PITCH; i += NT) {
         const int row = i / KQL_PITCH, q = i - row * KQL_PITCH;   // row = 16 i + n
         S.KQL[i] = q < NQ ? tb.kmul[((KSET_Q + q) * 8 + (row >> 4)) * 16 + (row & 15)] : 0u;
+    }
+    for (int i = tid; i < 2 * 8 * 16; i += NT) S.KQ2[i] = tb.kmul[(KSET_Q + (i < 128 ? SC / 8 : SC / 4)) * 8 * 16 + (i & 127)];
+    for (int i = tid; i < 2 * 8 * 16; i += NT) S.KQ4[i] = tb.kmul[(KSET_Q + (i < 128 ? SC / 16 : 3 * SC / 16)) * 8 * 16 + (i & 127)];
+    if (tid < NIX) S.IX[tid] = tb.initx[tid];
+}
+
+template <int NT>
+__device__ __forceinline__ void stage_tables_p(SmemP &S, const Tables &tb, int tid) {
+    for (int i = tid; i < 256 * 64; i += NT) S.C2[i] = tb.crc8[c2_table(i & 63) * 256 + (i >> 6)];
+    for (int i = tid; i < 8 * 16 * KR_PITCH; i += NT) {
+        const int row = i / KR_PITCH, kk = i - row * KR_PITCH;   // row = 16 i + n
+        S.KR[i] = kk < 64 ? tb.kmul[((KSET_R + kk) * 8 + (row >> 4)) * 16 + (row & 15)] : 0u;
     }
     for (int i = tid; i < 2 * 8 * 16; i += NT) S.KQ2[i] = tb.kmul[(KSET_Q + (i < 128 ? SC / 8 : SC / 4)) * 8 * 16 + (i & 127)];
     for (int i = tid; i < 2 * 8 * 16; i += NT) S.KQ4[i] = tb.kmul[(KSET_Q + (i < 128 ? SC / 16 : 3 * SC / 16)) * 8 * 16 + (i & 127)];
@@ -2044,22 +2079,41 @@ __device__ __attribute__((noinline)) bool run_heads_equal(const uint8_t *base, u
 // emitted with their value CRCs.  The first record not as predicted ends the run, and the stripe is
 // handed to k_replay's tile loop at that record (PieceHand); so is a stripe that does not start with
 // such a record, or whose entry the search has not found in its first tiles.
-__global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, const StripeDesc *__restrict__ stripes,
-                                              uint32_t n_stripes, StripeRes *__restrict__ sres,
-                                              TileRes *__restrict__ tres, kvr_tuple *__restrict__ pool,
-                                              uint64_t pool_cap, Counters *ctr, Tables tb, uint32_t pool_chunk,
-                                              uint4 *__restrict__ kpool, uint32_t *__restrict__ scnt,
-                                              PieceHand *__restrict__ hand) {
-    __shared__ Smem S;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    stage_tables(S, tb, tid);
+// k_piece's workgroup (KVR_PNT threads: 8 waves, two per SIMD, with up to 256 VGPRs) and its piece
+// buffers a wave keeps (KVR_PNB: the step being worked on and KVR_PNB - 1 loading behind it).  A
+// workgroup takes the WPB stripes k_replay's workgroup of the same index takes, WPB / (KVR_PNT / 64)
+// consecutive ones a wave, one after the other.
+#ifndef KVR_PNT
+#define KVR_PNT 1024
+#endif
+#ifndef KVR_PNB
+#define KVR_PNB 2
+#endif
+#ifndef KVR_PRUNFORM   // 1: a run's first pool chunk in run form (PieceRun, 8 B a record: the tuples' writes,
+#define KVR_PRUNFORM 1     // mixed into k_piece's read stream, cost it 0.05-0.15 ms on cfg2)
+#endif
+#ifndef KVR_PWIDE   // 1: a flush writes its tuples as whole 128-B lines (0: one tuple a lane, two 16-B halves)
+#define KVR_PWIDE 0
+#endif
+#ifndef KVR_PWROW   // 1: the header windows of a group wait in the wave's LDS row (0: in registers)
+#define KVR_PWROW 1
+#endif
+constexpr int PNT = KVR_PNT, PNB = KVR_PNB, PSPW = WPB / (PNT / 64);
+static_assert(PNT / 64 <= KVR_PWMAX, "one LDS window row per wave");
+static_assert(PSPW * (PNT / 64) == WPB && PNB >= 1 && PNB <= 3, "k_piece layout");
+
+// one stripe of k_piece (the kernel below): j = the wave's j-th stripe (progress balance)
+template <int NB>
+__device__ __forceinline__ void piece_stripe(const uint32_t si, const uint32_t j, SmemP &S, const Crc &K, const int lane,
+                                             const int wv,
+                                             const SegDesc *__restrict__ segs, const StripeDesc *__restrict__ stripes,
+                                             StripeRes *__restrict__ sres, TileRes *__restrict__ tres,
+                                             kvr_tuple *__restrict__ pool, uint64_t pool_cap, Counters *ctr,
+                                             uint32_t pool_chunk, uint4 *__restrict__ kpool, uint32_t *__restrict__ scnt,
+                                             PieceHand *__restrict__ hand, uint2 *__restrict__ pcrc,
+                                             PieceRun *__restrict__ prun) {
     uint32_t *const bal = S.BAL;   // [0] the progress of the waves in their step loop, [1] their number
-    if (tid == 0) { bal[0] = 0u; bal[1] = 0u; }
-    __syncthreads();
-    Crc K;
-    crc_init(K, S.C2, (uint32_t)lane);
-    const uint32_t si = blockIdx.x * WPB + (uint32_t)__builtin_amdgcn_readfirstlane(wv);
-    if (si >= n_stripes) return;
+    if (prun && lane == 0) prun[si] = PieceRun{0ull, 0u, 0u, 0u, 0u, 0u, 0u};   // (no run form yet)
 #ifdef KVR_PROF
     // (diagnostic build: cycles per phase into g_prof 0-5, 8-9, counts in 6-7, s_memrealtime 12-14;
     // tools/prof_phases.py)
@@ -2241,12 +2295,15 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     // the group: records qg .. in lanes 0 .. (their header windows and value CRCs)
     uint32_t qg = 0, vcrc = 0;
     bool early = true;   // the first completed records are verified at once: a stripe that is not uniform
+#if !KVR_PWROW
     uint32_t win[13], wsh = 0;   // hands back after one step's work.  (A record's window: the 13 dwords
 #pragma unroll                 // from the one holding its first byte, wsh bytes in.)
     for (int i = 0; i < 13; ++i) win[i] = 0u;
+#endif
     uint32_t gadj;
     __amdgpu_buffer_rsrc_t grs = seg_rsrc_a(sg.base, Pe, len, gadj);
     bool ustop = false;
+    uint32_t rf_n = 0;   // records of the run in run form (PieceRun): the first chunk's
     // verify and emit the group's first n records; a record not as predicted stops the run there
     auto flush = [&](uint32_t n) {
         KVR_PCOUNT(7);
@@ -2258,8 +2315,20 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
         const uint64_t GB = Pe + (uint64_t)qg * L;
         const bool on = (uint32_t)lane < n;
         uint32_t x[12];   // the record's first 48 bytes
+#if KVR_PWROW
+        {   // the window from the wave's LDS row, realigned by its byte offset in the dword it was loaded
+            // from (the same group base gadj as at its load: the group moves only in a flush)
+            uint32_t wr[PWIN];
+#pragma unroll
+            for (int i = 0; i < PWIN; ++i) wr[i] = (KVR_PABLATE & 1024) ? 0u : S.WROW[wv][i][lane];
+            const uint32_t wsh = ((uint32_t)lane * L + gadj) & 3u;
+#pragma unroll
+            for (int i = 0; i < 12; ++i) x[i] = __builtin_amdgcn_alignbyte(wr[i + 1], wr[i], wsh);
+        }
+#else
 #pragma unroll
         for (int i = 0; i < 12; ++i) x[i] = __builtin_amdgcn_alignbyte(win[i + 1], win[i], wsh);
+#endif
         const uint32_t op = x[0] & 255u, klen = (x[0] >> 8) | (x[1] << 24);
         uint32_t vl;
         {   // the value length at byte 5 + ku of the window
@@ -2276,8 +2345,9 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
 #pragma unroll
         for (int i = 0; i <= UKEYW; ++i) kr[i] = x[i + 1];
         uint32_t bad = 0;
-        const uint32_t kc = crc_words_u<UKEYW>(kr, K, 1u, ku, &bad);
-        const bool ok = on && op == 0u && klen == ku && vl == vu && bad == 0u && qg + (uint32_t)lane < q_fit;
+        const uint32_t kc = (KVR_PABLATE & 256) ? kr[0] : crc_words_u<UKEYW>(kr, K, 1u, ku, &bad);
+        const bool ok = on && (((KVR_PABLATE & 512) != 0) || (op == 0u && klen == ku && vl == vu && bad == 0u)) &&
+                        qg + (uint32_t)lane < q_fit;
         const uint64_t bm = __ballot(on && !ok);
         const uint32_t f = bm ? (uint32_t)__builtin_ctzll(bm) : n;
         // slots from the wave's chunk; a fresh chunk only where a tile starts, so that every tile's
@@ -2305,11 +2375,47 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
             m = f;
         }
         if (m != 0u && run_first == N32) run_first = chunk_base;
-        if ((uint32_t)lane < m) {   // the 32-B tuple as two 16-B stores (kvr_tuple's layout: op, flags 0)
+        const uint32_t cmx_r = pool_chunk > TILE_RECS ? pool_chunk : TILE_RECS;
+        if (KVR_PRUNFORM && prun && m != 0u && chunk_base - run_first < cmx_r && !(KVR_PABLATE & 128)) {
+            // the run's first chunk: run form, the value CRC and key tag only (8 B a record; the rest
+            // of the tuple follows from the run, k_compact_s writes it)
+            if ((uint32_t)lane < m) pcrc[chunk_base + (uint32_t)lane] = make_uint2(vcrc, ~kc);
+            if (kpool && (uint32_t)lane < m) kpool[chunk_base + (uint32_t)lane] = key_prefix_words(&x[1], 1u, ku);
+            rf_n += m;
+        } else if (KVR_PWIDE && !(KVR_PABLATE & (128 | 2048 | 4096))) {
+            // the m tuples as whole lines: store i writes tuples 32 i .. 32 i + 31, lane l the half l & 1
+            // of tuple 32 i + (l >> 1) (kvr_tuple's layout: op, flags 0), its CRCs from that tuple's lane
+            const uint32_t ckc = ~kc;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint32_t t = 32u * (uint32_t)i + ((uint32_t)lane >> 1), hf = (uint32_t)lane & 1u;
+                const uint32_t cv = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (int)t, (int)vcrc);
+                const uint32_t ck = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (int)t, (int)ckc);
+                if (32u * (uint32_t)i < m) {
+                    const uint64_t ro = GB + (uint64_t)t * L;
+                    const u32x4 v = hf ? u32x4{vu, cv, ck, 0u} : u32x4{(uint32_t)ro, (uint32_t)(ro >> 32), sd.seg, ku};
+                    // ((KVR_PABLATE & 8192): diagnostic, every wave's tuples into one 256-KiB stretch of the pool)
+                    // ((KVR_PABLATE & 16384): diagnostic, the k-th flush of every stripe side by side)
+                    const uint32_t slot = (KVR_PABLATE & 8192)    ? ((chunk_base + t) & 8191u)
+                                          : (KVR_PABLATE & 16384) ? (uint32_t)(((uint64_t)(qg >> 6) * 4096u + si) * 64u + t) % (uint32_t)(pool_cap - 64)
+                                                                  : chunk_base + t;
+                    if (t < m) reinterpret_cast<u32x4 *>(pool + slot)[hf] = v;
+                }
+            }
+            if (kpool && (uint32_t)lane < m) kpool[chunk_base + (uint32_t)lane] = key_prefix_words(&x[1], 1u, ku);
+        } else if ((uint32_t)lane < m && !(KVR_PABLATE & 128)) {   // the 32-B tuple as two 16-B stores (kvr_tuple's layout: op, flags 0)
             const uint64_t ro = GB + (uint64_t)lane * L;
             uint4 *const tp = reinterpret_cast<uint4 *>(pool + chunk_base + (uint32_t)lane);
-            tp[0] = make_uint4((uint32_t)ro, (uint32_t)(ro >> 32), sd.seg, ku);
-            tp[1] = make_uint4(vu, vcrc, ~kc, 0u);
+            if (KVR_PABLATE & 2048) {   // (diagnostic: 8 B a record)
+                reinterpret_cast<uint2 *>(pool)[chunk_base + (uint32_t)lane] = make_uint2(vcrc, ~kc);
+            } else if (KVR_PABLATE & 4096) {   // (diagnostic: non-temporal stores)
+                u32x4 *const tq = reinterpret_cast<u32x4 *>(tp);
+                __builtin_nontemporal_store(u32x4{(uint32_t)ro, (uint32_t)(ro >> 32), sd.seg, ku}, tq);
+                __builtin_nontemporal_store(u32x4{vu, vcrc, ~kc, 0u}, tq + 1);
+            } else {
+                tp[0] = make_uint4((uint32_t)ro, (uint32_t)(ro >> 32), sd.seg, ku);
+                tp[1] = make_uint4(vu, vcrc, ~kc, 0u);
+            }
             if (kpool) kpool[chunk_base + (uint32_t)lane] = key_prefix_words(&x[1], 1u, ku);
         }
         chunk_base += m;
@@ -2378,28 +2484,22 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
 #pragma unroll
     for (int i = 0; i < 13; ++i) wt[i] = 0u;
     auto merge_windows = [&]() {
+#if KVR_PWROW
+        if (wpend) {   // (the lanes whose records completed: their slots of the wave's row)
+#pragma unroll
+            for (int i = 0; i < PWIN; ++i) S.WROW[wv][i][lane] = wt[i];
+        }
+        (void)wtsh;
+#else
 #pragma unroll
         for (int i = 0; i < 13; ++i) win[i] = wpend ? wt[i] : win[i];
         wsh = wpend ? wtsh : wsh;
+#endif
         wpend = false;
     };
-    auto pre_step = [&](uint32_t q_s, const Geo &g, uint32_t &qa, uint32_t &qb) {
-        merge_windows();
-        KVR_PSTAMP(8);
-        if (early && qdone > qg) {
-            early = false;
-            flush(qdone - qg);
-        }
-        const uint64_t cmk = __ballot(g.act && g.pv == P - 1u);
-        qa = qb = 0;
-        if (cmk) {
-            qa = q_s + rl32(g.dq, (int)__builtin_ctzll(cmk));
-            qb = q_s + rl32(g.dq, 63 - (int)__builtin_clzll(cmk)) + 1u;
-            if (qb - qg > 64u && !ustop) flush(qa - qg);   // the group is full: its records (all before qa) first
-        }
-        // (issued on every step, a step that completes nothing reading nothing: a conditional load
-        // would leave the piece waits below conservative)
-        KVR_PSTAMP(4);
+    // (issued on every step, a step that completes nothing reading nothing: a conditional load would
+    // leave the piece waits conservative)
+    auto load_windows = [&](uint32_t qa, uint32_t qb) {
         const uint32_t qj = qg + (uint32_t)lane;
         wpend = qj >= qa && qj < qb;
         const int32_t wo = lane * (int32_t)L + (int32_t)gadj, wa = wpend && !(KVR_PABLATE & 32) ? (wo & ~3) : 0x7FFFFF00;
@@ -2413,6 +2513,23 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
             wt[12] = __builtin_amdgcn_raw_buffer_load_b32(grs, wa + 48, 0, 0);
         }
     };
+    auto pre_step = [&](uint32_t q_s, const Geo &g, uint32_t &qa, uint32_t &qb, bool load_now = true) {
+        merge_windows();
+        KVR_PSTAMP(8);
+        if (early && qdone > qg) {
+            early = false;
+            flush(qdone - qg);
+        }
+        const uint64_t cmk = __ballot(g.act && g.pv == P - 1u);
+        qa = qb = 0;
+        if (cmk) {
+            qa = q_s + rl32(g.dq, (int)__builtin_ctzll(cmk));
+            qb = q_s + rl32(g.dq, 63 - (int)__builtin_clzll(cmk)) + 1u;
+            if (qb - qg > 64u && !ustop) flush(qa - qg);   // the group is full: its records (all before qa) first
+        }
+        KVR_PSTAMP(4);
+        if (load_now) load_windows(qa, qb);
+    };
     // the step's push, scan and value CRCs (records [qa, qb) take theirs into vcrc)
     auto finish_step = [&](uint32_t raw, uint32_t q_s, uint32_t p_s, const Geo &g, uint32_t qa, uint32_t qb) {
         const bool first = g.act && g.pv == 0u;
@@ -2421,7 +2538,7 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
         const uint32_t dd = g.act ? (dl < dr ? dl : dr) : 0u;
         uint32_t v = raw;
         if (!(KVR_PABLATE & 2)) {
-            const uint32_t pushed = kmul_col<KR_OFF, KR_PITCH>(dd ? raw : 0u, S, dd ? 4u * (dd - 1u) : 0u);
+            const uint32_t pushed = kmul_col<KR_OFF_P, KR_PITCH>(dd ? raw : 0u, S, dd ? 4u * (dd - 1u) : 0u);
             v = seg_xscan(dd ? pushed : raw, first ? N32 : 0u);
         }
         cont = ((__ballot(g.act && !comp) >> 63) & 1ull) != 0ull;
@@ -2435,19 +2552,31 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
             qdone = qb;
         }
     };
+    // the steps: lane 0 at piece p0 of record q0; the next NB - 1 steps' pieces are in flight behind
+    // the one being worked on (issued before its window loads and CRC), each in buffers of its own
     uint32_t q0 = 0, p0 = 0;
     Geo g0 = geo(q0, p0);
-    issue(w, q0, p0, g0);
+    auto next_qp = [&](uint32_t q, uint32_t p, uint32_t &qn, uint32_t &pn) {
+        qn = q + adv_q;
+        pn = p + adv_p;
+        if (pn >= P) { pn -= P; ++qn; }
+    };
+    auto geo_or_none = [&](uint32_t q, uint32_t p) -> Geo {   // (a step past the run reads nothing)
+        Geo g = geo(q, p);
+        if (!(q < q_end)) { g.act = false; g.o = 0x7FFFFF00; }
+        return g;
+    };
     // The 16 waves of a CU share its issue slots oldest first: left alone, the oldest wave of each
     // SIMD finishes its stripe in 55 % of the time of the youngest, and the CU's last quarter runs on
-    // 4 waves.  A wave ahead of the mean progress (records done, 1/4096 of its run) drops its priority,
-    // one behind raises it, so the 16 stripes end together.
-    const uint64_t pscale = (4096ull << 32) / q_end;
+    // 4 waves.  A wave ahead of the mean progress (records done, 1/4096 of its PSPW runs) drops its
+    // priority, one behind raises it, so the workgroup's stripes end together.
+    const uint64_t pscale = (4096ull << 32) / ((uint64_t)q_end * PSPW);
+    const uint32_t pbase = j * (4096u / PSPW);
     uint32_t pown = 0;
     if (KVR_PBAL && lane == 0) atomicAdd(&bal[1], 1u);
     uint32_t bstep = 0;   // (the balance runs every KVR_PBAL_EVERY steps)
     auto balance = [&](uint32_t q_now) {
-        const uint32_t pn = (uint32_t)(((uint64_t)q_now * pscale) >> 32);
+        const uint32_t pn = pbase + (uint32_t)(((uint64_t)q_now * pscale) >> 32);
         uint32_t sum = 0, cnt = 1;
         if (lane == 0) {
             sum = atomicAdd(&bal[0], pn - pown) + (pn - pown);
@@ -2462,29 +2591,87 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
         else if (d < dl) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
     };
-    // one piece buffer: the next step's pieces are loaded as soon as the CRC has read this step's
     KVR_PSTAMP(0);
+    if constexpr (NB == 1) {
+        // one piece buffer: the next step's pieces are loaded as soon as the CRC has read this step's
+        issue(w, q0, p0, g0);
 #pragma unroll 1
-    for (;;) {
-        uint32_t qa, qb;
-        pre_step(q0, g0, qa, qb);   // (a stop found here ends the loop after this step: no exit between
-                                    // the window loads and the next pieces, so the waits stay exact)
-        KVR_PSTAMP(9);
-        const uint32_t raw = crc_step(w, g0);
-        KVR_PSTAMP(1);
-        KVR_PCOUNT(6);
-        uint32_t q1 = q0 + adv_q, p1 = p0 + adv_p;
-        if (p1 >= P) { p1 -= P; ++q1; }
-        const bool h1 = q1 < q_end;
-        Geo g1 = geo(q1, p1);
-        if (!h1) { g1.act = false; g1.o = 0x7FFFFF00; }
-        issue(w, q1, p1, g1);   // (issued on every path, the last step's reading nothing: exact wait counts)
-        KVR_PSTAMP(2);
-        finish_step(raw, q0, p0, g0, qa, qb);
-        if (KVR_PBAL && (++bstep & (KVR_PBAL_EVERY - 1u)) == 0u) balance(q1 < q_end ? q1 : q_end);
-        KVR_PSTAMP(3);
-        if (!h1 || ustop) break;
-        q0 = q1; p0 = p1; g0 = g1;
+        for (;;) {
+            uint32_t qa, qb;
+            pre_step(q0, g0, qa, qb);   // (a stop found here ends the loop after this step: no exit between
+                                        // the window loads and the next pieces, so the waits stay exact)
+            KVR_PSTAMP(9);
+            const uint32_t raw = crc_step(w, g0);
+            KVR_PSTAMP(1);
+            KVR_PCOUNT(6);
+            uint32_t q1, p1;
+            next_qp(q0, p0, q1, p1);
+            const bool h1 = q1 < q_end;
+            Geo g1 = geo_or_none(q1, p1);
+            issue(w, q1, p1, g1);   // (issued on every path, the last step's reading nothing: exact wait counts)
+            KVR_PSTAMP(2);
+            finish_step(raw, q0, p0, g0, qa, qb);
+            if (KVR_PBAL && (++bstep & (KVR_PBAL_EVERY - 1u)) == 0u) balance(q1 < q_end ? q1 : q_end);
+            KVR_PSTAMP(3);
+            if (!h1 || ustop) break;
+            q0 = q1; p0 = p1; g0 = g1;
+        }
+    } else {
+        // NB buffers, a ring: step s + NB - 1 is issued into the buffer step s - 1 freed, before step
+        // s's window loads and CRC (every load unconditional, a step past the run reading nothing, so
+        // the waits stay exact: the CRC waits for its own pieces only).  A step in flight is only its
+        // (q, p); its geometry is computed again where it is worked on (registers for the buffers).
+        uint32_t wb[UW + 1], wc[UW + 1];
+        uint32_t q1, p1, q2 = 0, p2 = 0;
+        next_qp(q0, p0, q1, p1);
+        issue(w, q0, p0, g0);
+        if constexpr (NB == 3) {
+            issue(wb, q1, p1, geo_or_none(q1, p1));
+            next_qp(q1, p1, q2, p2);
+        }
+        // the step in cur; the newest in flight goes into nx
+        // (the window loads and a flush come first: a flush holds many registers, and the buffer the
+        // next pieces go into is free until they are issued)
+        auto body = [&](uint32_t (&cur)[UW + 1], uint32_t (&nx)[UW + 1]) -> bool {
+            const bool h1 = q1 < q_end;
+            uint32_t qa, qb;
+            pre_step(q0, g0, qa, qb, false);
+            KVR_PSTAMP(9);
+            if constexpr (NB == 3) issue(nx, q2, p2, geo_or_none(q2, p2));
+            else issue(nx, q1, p1, geo_or_none(q1, p1));
+            KVR_PSTAMP(2);
+            const uint32_t raw = crc_step(cur, g0);
+            KVR_PSTAMP(1);
+            KVR_PCOUNT(6);
+            // the windows of the records this step completes, behind the next step's pieces (their
+            // registers are not held across the CRC); merged at the next step, whose CRC waits for its
+            // pieces issued before them anyway
+            load_windows(qa, qb);
+            finish_step(raw, q0, p0, g0, qa, qb);
+            if (KVR_PBAL && (++bstep & (KVR_PBAL_EVERY - 1u)) == 0u) balance(h1 ? q1 : q_end);
+            KVR_PSTAMP(3);
+            if (!h1 || ustop) return true;
+            q0 = q1; p0 = p1;
+            if constexpr (NB == 3) {
+                q1 = q2; p1 = p2;
+                next_qp(q1, p1, q2, p2);
+            } else {
+                next_qp(q0, p0, q1, p1);
+            }
+            g0 = geo(q0, p0);   // (q0 < q_end here)
+            return false;
+        };
+#pragma unroll 1
+        for (;;) {
+            if constexpr (NB == 3) {
+                if (body(w, wc)) break;
+                if (body(wb, w)) break;
+                if (body(wc, wb)) break;
+            } else {
+                if (body(w, wb)) break;
+                if (body(wb, w)) break;
+            }
+        }
     }
     if (KVR_PBAL) {   // out of the mean
         if (lane == 0) { atomicSub(&bal[0], pown); atomicSub(&bal[1], 1u); }
@@ -2494,6 +2681,7 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     if (!ustop && qg < qdone) flush(qdone - qg);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (a prefetched step the stop left unused)
     if (!ustop && qg != q_end) ustop = true;   // (defensive: every record of the stripe completes)
+    if (prun && lane == 0 && rf_n) prun[si] = PieceRun{Pe, L, run_first, rf_n, ku, vu, sd.seg};
     if (!ustop) {
         close_tiles(sd.t_end, seg_n);
         total += qg;
@@ -2510,6 +2698,30 @@ __global__ __launch_bounds__(RT) void k_piece(const SegDesc *__restrict__ segs, 
     close_tiles(k_res, seg_n - (seg_tile < k_res ? ah : seg_n));
     total += qg - ah;
     hand_back(Pe + (uint64_t)qg * L, k_res, ah, L);
+}
+
+
+__global__ __launch_bounds__(PNT) void k_piece(const SegDesc *__restrict__ segs, const StripeDesc *__restrict__ stripes,
+                                               uint32_t n_stripes, StripeRes *__restrict__ sres,
+                                               TileRes *__restrict__ tres, kvr_tuple *__restrict__ pool,
+                                               uint64_t pool_cap, Counters *ctr, Tables tb, uint32_t pool_chunk,
+                                               uint4 *__restrict__ kpool, uint32_t *__restrict__ scnt,
+                                               PieceHand *__restrict__ hand, uint2 *__restrict__ pcrc,
+                                               PieceRun *__restrict__ prun) {
+    __shared__ SmemP S;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    stage_tables_p<PNT>(S, tb, tid);
+    if (tid == 0) { S.BAL[0] = 0u; S.BAL[1] = 0u; }
+    __syncthreads();
+    Crc K;
+    crc_init(K, S.C2, (uint32_t)lane);
+    const uint32_t s0 = blockIdx.x * WPB + (uint32_t)__builtin_amdgcn_readfirstlane(wv) * PSPW;
+#pragma unroll 1
+    for (uint32_t j = 0; j < (uint32_t)PSPW; ++j) {
+        if (s0 + j >= n_stripes) return;
+        piece_stripe<PNB>(s0 + j, j, S, K, lane, __builtin_amdgcn_readfirstlane(wv), segs, stripes, sres, tres, pool,
+                          pool_cap, ctr, pool_chunk, kpool, scnt, hand, pcrc, prun);
+    }
 }
 
 }  // namespace kvr

@@ -33,6 +33,9 @@ for mask in masks:
     path = os.path.join(ABL, f"libkvreplay_a{mask}.so") if isinstance(mask, int) else os.path.join(VAR, f"libkvreplay_{mask}.so")
     if not isinstance(mask, int) and os.path.exists(os.path.join(AB, f"libkvreplay_{mask}.so")):
         path = os.path.join(AB, f"libkvreplay_{mask}.so")   # an A/B build (tools/build_ab.sh)
+    vp = os.path.join(ROOT, "mini-kvstore-v2_amd", "lib", "vpair", str(mask), "libkvreplay.so")
+    if not isinstance(mask, int) and os.path.exists(vp):
+        path = vp   # a variant pair (build.py build_variant_pair)
     if mask == "main":   # the shipped library itself
         path = os.path.join(ROOT, "mini-kvstore-v2_amd", "lib", "libkvreplay.so")
     lib = C.CDLL(path)   # the only kvreplay library in this process

@@ -74,7 +74,29 @@ __device__ __forceinline__ uint32_t fold(const uint32_t (&w)[33], int off) {
     return x;
 }
 
-template <int PAT, int DEPTH, int NT = RT>
+// the 52-B header windows k_piece loads beside its pieces: 3 dwordx4 + 1 dword a step, WIN lanes
+// reading (1049-B records apart), the others out of the resource (WMASK 0) or exec-masked off (1)
+// (loaded in one step, consumed at the next: the wait for them never covers the pieces issued after)
+template <int WIN, int WMASK>
+__device__ __forceinline__ void windows(__amdgpu_buffer_rsrc_t rs, int lane, uint32_t (&wv)[13]) {
+    if (WIN < 0) return;
+    const int o = lane < WIN ? lane * 1049 + 3 : 0x7FFFFF00;
+    if (WMASK && lane >= WIN) return;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (o & ~3) + 16 * i, 0, 0);
+        wv[4 * i] = v.x; wv[4 * i + 1] = v.y; wv[4 * i + 2] = v.z; wv[4 * i + 3] = v.w;
+    }
+    wv[12] = __builtin_amdgcn_raw_buffer_load_b32(rs, (o & ~3) + 48, 0, 0);
+}
+__device__ __forceinline__ uint32_t wfold(uint32_t (&wv)[13]) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 13; ++i) x ^= wv[i];
+    return x;
+}
+
+template <int PAT, int DEPTH, int NT = RT, int WIN = -1, int WMASK = 0>
 __global__ __launch_bounds__(NT) void k_pat(const uint8_t *__restrict__ buf, uint64_t bytes_per_stripe,
                                             uint32_t n_stripes, int delay, uint32_t *sink) {
     __shared__ uint32_t pin[130 * 1024 / 4];
@@ -88,7 +110,7 @@ __global__ __launch_bounds__(NT) void k_pat(const uint8_t *__restrict__ buf, uin
     const int off = PAT == 0 ? 128 * lane : (lane >> 3) * 1049 + 25 + 128 * (lane & 7);
     const uint64_t n_steps = (bytes_per_stripe - 1100) / step_bytes;
     uint32_t acc = 0;
-    uint32_t a[33], b[33], c[33];
+    uint32_t a[33], b[33], c[33], wn[13] = {};
     auto rsrc = [&](uint64_t s) {   // (a step past the stripe re-reads the last one: never out of the buffer)
         s = s < n_steps ? s : n_steps - 1;
         return __builtin_amdgcn_make_buffer_rsrc((void *)(p + s * step_bytes), (short)0, (int)(step_bytes + 1100), 0x00020000);
@@ -121,6 +143,8 @@ __global__ __launch_bounds__(NT) void k_pat(const uint8_t *__restrict__ buf, uin
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        acc ^= wfold(wn);
+        windows<WIN, WMASK>(rsrc(s), lane, wn);
         acc ^= spin(fold<PAT>(a, off), acc, delay);
         if (DEPTH == 1) load_step<PAT>(rsrc(s + 1), off, b);
         if (DEPTH == 2) {
@@ -130,6 +154,8 @@ __global__ __launch_bounds__(NT) void k_pat(const uint8_t *__restrict__ buf, uin
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        acc ^= wfold(wn);
+        windows<WIN, WMASK>(rsrc(s + 1), lane, wn);
         acc ^= spin(fold<PAT>(b, off), acc, delay);
         if (DEPTH == 1) load_step<PAT>(rsrc(s + 2), off, a);
     }
@@ -137,7 +163,7 @@ __global__ __launch_bounds__(NT) void k_pat(const uint8_t *__restrict__ buf, uin
     if (acc == 0x12345678u) sink[threadIdx.x] = acc + pin[0];
 }
 
-template <int PAT, int DEPTH, int NT = RT>
+template <int PAT, int DEPTH, int NT = RT, int WIN = -1, int WMASK = 0>
 static void run(const uint8_t *d, uint64_t bytes, int cus, int delay, uint32_t *sink) {
     const uint32_t n_stripes = cus * (NT / 64);
     const uint64_t bps = bytes / n_stripes;
@@ -146,7 +172,7 @@ static void run(const uint8_t *d, uint64_t bytes, int cus, int delay, uint32_t *
     float best = 1e9f;
     for (int it = 0; it < 6; ++it) {
         CK(hipEventRecord(e0));
-        k_pat<PAT, DEPTH, NT><<<cus, NT>>>(d, bps, n_stripes, delay, sink);
+        k_pat<PAT, DEPTH, NT, WIN, WMASK><<<cus, NT>>>(d, bps, n_stripes, delay, sink);
         const hipError_t le = hipGetLastError();
         if (le != hipSuccess) { printf("launch: %s\n", hipGetErrorString(le)); return; }
         CK(hipEventRecord(e1));
@@ -156,7 +182,8 @@ static void run(const uint8_t *d, uint64_t bytes, int cus, int delay, uint32_t *
         if (it > 0 && ms < best) best = ms;
     }
     const char *nm[] = {"tile", "piece-u", "piece-a"};
-    printf("%-8s waves %2d depth %d delay %4d VALU: %.3f ms  %7.1f GB/s\n", nm[PAT], NT / 64, DEPTH, delay, best, bytes / best / 1e6);
+    printf("%-8s waves %2d depth %d win %2d mask %d delay %4d VALU: %.3f ms  %7.1f GB/s\n", nm[PAT], NT / 64, DEPTH, WIN, WMASK,
+           delay, best, bytes / best / 1e6);
 }
 
 int main(int argc, char **argv) {
@@ -193,6 +220,21 @@ int main(int argc, char **argv) {
         const uint64_t bps = bytes / n_stripes, n_steps = (bps - 1100) / (8u * 1049u);
         run<2, 2>(d, bytes, cus, 0, sink);
         printf("calib_bytes_per_dispatch=%llu\n", (unsigned long long)(n_stripes * n_steps * 8u * 1049u));
+        return 0;
+    }
+    if (argc > 1 && strcmp(argv[1], "win") == 0) {   // the header-window loads beside the pieces (round 6)
+        for (int delay : {0, 512}) {
+            run<2, 1>(d, bytes, cus, delay, sink);
+            run<2, 1, RT, 0, 0>(d, bytes, cus, delay, sink);
+            run<2, 1, RT, 8, 0>(d, bytes, cus, delay, sink);
+            run<2, 1, RT, 8, 1>(d, bytes, cus, delay, sink);
+            run<2, 1, RT, 64, 0>(d, bytes, cus, delay, sink);
+            run<2, 2>(d, bytes, cus, delay, sink);
+            run<2, 2, RT, 0, 0>(d, bytes, cus, delay, sink);
+            run<2, 2, RT, 8, 0>(d, bytes, cus, delay, sink);
+            run<2, 2, RT, 8, 1>(d, bytes, cus, delay, sink);
+            run<2, 2, RT, 64, 0>(d, bytes, cus, delay, sink);
+        }
         return 0;
     }
     if (argc > 1 && strcmp(argv[1], "waves") == 0) {   // waves per CU x pieces in flight (round 6)

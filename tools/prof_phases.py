@@ -15,7 +15,7 @@ from bench import CONFIGS  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg2"
 nseg_override = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-lib = C.CDLL(os.path.join(ROOT, "mini-kvstore-v2_amd", "lib", "libkvreplay_prof.so"))
+lib = C.CDLL(os.environ.get("KVR_PROF_LIB") or os.path.join(ROOT, "mini-kvstore-v2_amd", "lib", "libkvreplay_prof.so"))
 P, U64, U32, SZ = C.c_void_p, C.c_uint64, C.c_uint32, C.c_size_t
 lib.kvr_ctx_create.argtypes = [C.c_int, C.POINTER(P)]
 lib.kvr_replay.argtypes = [P, C.POINTER(K.Segment), SZ, U32, P, SZ, P, SZ, C.POINTER(SZ), C.POINTER(K.Error)]
