@@ -733,7 +733,7 @@ __global__ void k_live_ent(const FoldEnt *__restrict__ ent, const uint32_t *__re
 constexpr int DL_T = 256, DL_PER = 16, DL_CH = DL_T * DL_PER;   // tuples per block: 4096
 __device__ __forceinline__ uint64_t rec_size(const kvr_tuple &t) { return 9ull + t.key_len + t.val_len; }   // engine.rs:169-173
 #ifndef KVR_DL_BATCH   // 1: the dense-list kernels load their live tuples four at a time (A/B knob, round 5)
-#define KVR_DL_BATCH 0
+#define KVR_DL_BATCH 1
 #endif
 // the thread's 16 flags as a bit mask (bit k: tuple i0 + k is live)
 __device__ __forceinline__ uint32_t dl_bits(const uint4 f) {

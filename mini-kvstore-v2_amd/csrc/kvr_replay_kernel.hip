@@ -847,14 +847,17 @@ __device__ __forceinline__ TileSeg tile_seg(const uint8_t *abase, const uint8_t 
 // first byte, and the dword after them (byte-unaligned 16-B loads run at half the rate: tools/
 // piece_probe.hip); piece_align shifts the words into place once they have landed.  Offsets past the
 // resource read 0.
+#ifndef KVR_PAUX   // k_piece's piece loads: cache policy bits (2: nt, streamed past the caches; A/B knob)
+#define KVR_PAUX 0
+#endif
 __device__ __forceinline__ void load_piece(__amdgpu_buffer_rsrc_t rs, int o, uint32_t (&w)[UW + 1]) {
     const int a = o & ~3;
 #pragma unroll
     for (int i = 0; i < UW / 4; ++i) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, a + 16 * i, 0, 0);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, a + 16 * i, 0, KVR_PAUX);
         w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
     }
-    w[UW] = __builtin_amdgcn_raw_buffer_load_b32(rs, a + 4 * UW, 0, 0);
+    w[UW] = __builtin_amdgcn_raw_buffer_load_b32(rs, a + 4 * UW, 0, KVR_PAUX);
 }
 __device__ __forceinline__ void piece_align(uint32_t (&w)[UW + 1], int o) {
     const uint32_t sh = (uint32_t)o & 3u;
@@ -2303,7 +2306,6 @@ __device__ __forceinline__ void piece_stripe(const uint32_t si, const uint32_t j
     uint32_t gadj;
     __amdgpu_buffer_rsrc_t grs = seg_rsrc_a(sg.base, Pe, len, gadj);
     bool ustop = false;
-    uint32_t rf_n = 0;   // records of the run in run form (PieceRun): the first chunk's
     // verify and emit the group's first n records; a record not as predicted stops the run there
     auto flush = [&](uint32_t n) {
         KVR_PCOUNT(7);
@@ -2381,7 +2383,6 @@ __device__ __forceinline__ void piece_stripe(const uint32_t si, const uint32_t j
             // of the tuple follows from the run, k_compact_s writes it)
             if ((uint32_t)lane < m) pcrc[chunk_base + (uint32_t)lane] = make_uint2(vcrc, ~kc);
             if (kpool && (uint32_t)lane < m) kpool[chunk_base + (uint32_t)lane] = key_prefix_words(&x[1], 1u, ku);
-            rf_n += m;
         } else if (KVR_PWIDE && !(KVR_PABLATE & (128 | 2048 | 4096))) {
             // the m tuples as whole lines: store i writes tuples 32 i .. 32 i + 31, lane l the half l & 1
             // of tuple 32 i + (l >> 1) (kvr_tuple's layout: op, flags 0), its CRCs from that tuple's lane
@@ -2681,7 +2682,10 @@ __device__ __forceinline__ void piece_stripe(const uint32_t si, const uint32_t j
     if (!ustop && qg < qdone) flush(qdone - qg);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (a prefetched step the stop left unused)
     if (!ustop && qg != q_end) ustop = true;   // (defensive: every record of the stripe completes)
-    if (prun && lane == 0 && rf_n) prun[si] = PieceRun{Pe, L, run_first, rf_n, ku, vu, sd.seg};
+    if (KVR_PRUNFORM && prun && lane == 0 && qg) {   // (the first chunk is full before another is claimed)
+        const uint32_t cmx_r = pool_chunk > TILE_RECS ? pool_chunk : TILE_RECS;
+        prun[si] = PieceRun{Pe, L, run_first, qg < cmx_r ? qg : cmx_r, ku, vu, sd.seg};
+    }
     if (!ustop) {
         close_tiles(sd.t_end, seg_n);
         total += qg;
