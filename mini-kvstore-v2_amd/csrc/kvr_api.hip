@@ -93,6 +93,10 @@ bool getenv_flag(const char *name) {
     const char *e = getenv(name);
     return e && *e && *e != '0';
 }
+bool getenv_flag_off(const char *name) {   // set to 0
+    const char *e = getenv(name);
+    return e && *e == '0';
+}
 // tuples behind pool_cap that serve a claim past it (k_replay flags the overflow and writes there;
 // the host then grows the pool and runs again): one claim of the largest size
 constexpr uint64_t POOL_SLACK = (POOL_CHUNK > TILE_RECS ? POOL_CHUNK : TILE_RECS) + 64;
@@ -183,6 +187,7 @@ struct kvr_ctx {
     bool h_stripes_up = false;             // h_stripes holds exactly the uploaded stripes
     bool lc_zero = false;                  // lcbuf is known to be zero (cleared at the end of the last call)
     uint64_t pool_hint = 0;
+    uint32_t piece_skip = 0;               // calls left that skip k_piece (see replay_one: KVR_PIECE_ADAPT)
     uint64_t pool_need = 0;                // > 0: the last replay needed more than 32-bit pool slots
     uint32_t tps_override = 0;
     kvr_stats stats{};
@@ -602,6 +607,7 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         const SegDesc &a = c->h_segs[i], &b = c->up_segs[i];
         same_layout = a.base == b.base && a.len == b.len && a.d0 == b.d0 && a.n_tiles == b.n_tiles && a.tile0 == b.tile0;
     }
+    const bool same_layout_call = same_layout && (flags & KVR_SEGS_ON_DEVICE);
     if (same_layout) {
         for (size_t i = 0; i < n; ++i) {
             c->h_segs[i].stripe0 = c->up_segs[i].stripe0;
@@ -704,7 +710,12 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
         const bool markers = getenv_flag("KVR_EVENT_MARKERS");
         // k_piece takes every stripe first (runs of equal SETs, value-aligned) and hands the rest of a
         // stripe to k_replay's tile loop; ms_replay spans both
-        const bool piece = !getenv_flag("KVR_NO_PIECE");
+        // (a device-resident store that k_piece left entirely to k_replay on the last call with the same
+        // segment layout -- cfg4's SET/DEL mix, cfg5's mixed values -- skips it for the next 7 calls:
+        // its launch, table staging and entry checks cost such a store 2-3 %; KVR_PIECE_ADAPT=0 keeps
+        // it on every call.  Either way the tuples are the same: k_replay takes any stripe)
+        const bool piece = !getenv_flag("KVR_NO_PIECE") && !(c->piece_skip && same_layout_call);
+        if (c->piece_skip) --c->piece_skip;
         auto launch_compact = [&](bool lk, hipEvent_t stop) {
             hipExtLaunchKernelGGL(k_compact_s, dim3(n_stripes), dim3(CT), 0, st, nullptr, markers ? nullptr : stop, 0u,
                                c->segs.p, c->stripes.p, c->sres.p, c->soff.p,
@@ -882,6 +893,8 @@ static int replay_one(kvr_ctx *c, const kvr_segment *segs, size_t n, uint32_t fl
             return KVR_CORRUPTED;
         }
         const uint64_t total = c->h_ctr->total_tuples;
+        if (piece && linked && (flags & KVR_SEGS_ON_DEVICE) && !getenv_flag_off("KVR_PIECE_ADAPT"))
+            c->piece_skip = c->h_ctr->piece_done ? 0u : 7u;
         c->stats.n_records = total;
         c->stats.n_crc_fail = c->h_ctr->crc_fail;
         *n_out = total;

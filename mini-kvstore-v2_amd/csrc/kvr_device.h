@@ -114,7 +114,10 @@ struct Counters {         // device scratch, reset per call
     unsigned long long crc_fail;
     uint32_t overflow;
     uint32_t unlinked;    // host mirror: k_compact_s (linked mode) found a stripe it cannot link alone
+    uint32_t piece_done;  // stripes k_piece ran to their end (host mirror: copied by the gather / k_link)
+    uint32_t pad;
 };
+static_assert(sizeof(Counters) + 64 <= 128, "Counters in the link + counters block");
 
 constexpr uint32_t LC_BLOCK = 128;   // one link + counters block (LinkResult at 0, Counters at 64)
 

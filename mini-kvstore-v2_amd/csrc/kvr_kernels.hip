@@ -262,6 +262,7 @@ __global__ __launch_bounds__(LT) void k_link(const SegDesc *__restrict__ segs, u
             const uint32_t ov = ctr->overflow;
             hctr->pool_cursor = ctr->pool_cursor;
             hctr->overflow = ov;
+            hctr->piece_done = ctr->piece_done;
             hctr->total_tuples = (L.status == 0 && soff) ? all_recs : ctr->total_tuples;
             hctr->crc_fail = 0;   // (k_compact_s adds its failures here)
             if (L.status == 0 && ov == 0u) {   // a clean pass: the block is cleared for the next call
@@ -327,7 +328,7 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
     if (scnt) {
         const uint32_t ov = ctr->overflow;
         if (blockIdx.x == 0) {
-            if (threadIdx.x == 0) { hctr->pool_cursor = ctr->pool_cursor; hctr->overflow = ov; }
+            if (threadIdx.x == 0) { hctr->pool_cursor = ctr->pool_cursor; hctr->overflow = ov; hctr->piece_done = ctr->piece_done; }
             if (threadIdx.x < LC_BLOCK / 16) lc_next[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
         }
         if (ov) return;
@@ -402,6 +403,41 @@ __global__ __launch_bounds__(CT) void k_compact_s(const SegDesc *__restrict__ se
     const uint64_t run = sres[blockIdx.x].pool_run;
     if (run != NONE) {   // the stripe's tuples are one run of the pool: a straight copy
         const uint64_t n = sres[blockIdx.x].count, o0 = o_base;
+        if (n && pr.n == n && run == pr.first) {
+            // every record of the stripe in run form (k_piece ran it to its end): a thread builds
+            // whole tuples from the run and pcrc, with the manifest check
+            // (RF records a thread per round, their loads issued before any store: one round trip a round)
+            constexpr int RF = 4;
+            const uint64_t lim = o0 + n <= out_cap ? n : (out_cap > o0 ? out_cap - o0 : 0ull);
+            for (uint64_t k0 = threadIdx.x; k0 < lim; k0 += (uint64_t)CT * RF) {
+                uint2 c[RF];
+                uint32_t e[RF];
+#pragma unroll
+                for (int i = 0; i < RF; ++i) {
+                    const uint64_t k = k0 + (uint64_t)i * CT, o = o0 + k;
+                    c[i] = k < lim ? pcrc[run + k] : make_uint2(0u, 0u);
+                    e[i] = k < lim && expected && o < n_expected ? expected[o] : 0u;
+                }
+#pragma unroll
+                for (int i = 0; i < RF; ++i) {
+                    const uint64_t k = k0 + (uint64_t)i * CT, o = o0 + k;
+                    if (k >= lim) break;
+                    const uint64_t ro = pr.Pe + k * pr.L;
+                    uint32_t fw = 0;
+                    if (expected && o < n_expected) {
+                        fw = KVR_TF_VERIFIED << 8;
+                        if (e[i] != c[i].x) { fw |= KVR_TF_CRC_FAIL << 8; ++fails; }
+                    }
+                    uint4 *const dst = reinterpret_cast<uint4 *>(out + o);
+                    dst[0] = make_uint4((uint32_t)ro, (uint32_t)(ro >> 32), pr.seg, pr.ku);
+                    dst[1] = make_uint4(pr.vu, c[i].x, c[i].y, fw);
+                    if (kout) kout[o] = kpool[run + k];
+                    if (ktk) { ktk[2 * o] = c[i].y; ktk[2 * o + 1] = pr.ku; }
+                }
+            }
+            finish();
+            return;
+        }
         for (uint64_t k2 = threadIdx.x; k2 < 2 * n; k2 += CT) move(run + (k2 >> 1), o0 + (k2 >> 1), (uint32_t)k2 & 1u);
         finish();
         return;

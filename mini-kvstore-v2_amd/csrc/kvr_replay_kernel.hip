@@ -2689,6 +2689,7 @@ __device__ __forceinline__ void piece_stripe(const uint32_t si, const uint32_t j
     if (!ustop) {
         close_tiles(sd.t_end, seg_n);
         total += qg;
+        if (lane == 0) atomicAdd(&ctr->piece_done, 1u);   // (the host's k_piece-or-not heuristic)
         finish(Pe + (uint64_t)q_end * L);
         KVR_PSTAMP(5);
         KVR_PFLUSH();

@@ -294,3 +294,29 @@ def test_piece_device_alignment(gctx, shape, tps, base_off, engine):
         check_parity_dev(gctx, [segs[1], cut], base_off)
     finally:
         gctx.set_tiles_per_stripe(0)
+
+
+def test_piece_adaptive_skip(gctx):
+    """A device-resident store that k_piece hands back entirely (values of 1000 and 1001 B alternating:
+    no stripe starts a run of equal records) makes the library skip k_piece on the next calls with
+    the same segment layout (KVR_PIECE_ADAPT).  The tuples never depend on it: the same buffer then
+    refilled with a uniform store of the same length replays to the oracle's tuples whether k_piece
+    runs or not, call after call."""
+    torch = pytest.importorskip("torch")
+    a = bytearray()
+    for i in range(2000):
+        a += rec_set(_key(i, 16), _value(i, 1000 + (i & 1)))
+    b = bytearray()
+    for i in range(1000):
+        b += rec_set(_key(i, 16), _value(i, 2051 - 25))
+    assert len(a) == len(b)
+    buf = torch.zeros(len(a) + 512, dtype=torch.uint8, device="cuda")
+    ptrs = [(buf.data_ptr() + 64, len(a))]
+    for store in (bytes(a), bytes(b)):
+        buf[64: 64 + len(store)] = torch.from_numpy(np.frombuffer(store, dtype=np.uint8).copy()).cuda()
+        torch.cuda.synchronize()
+        rc, ref, _ = O.replay([store])
+        assert rc == 0
+        for _ in range(10):
+            rg = gctx.replay(ptrs, on_device=True)
+            assert rg.status == 0 and np.array_equal(rg.tuples, ref)
