@@ -2076,16 +2076,19 @@ __device__ __attribute__((noinline)) bool run_heads_equal(const uint8_t *base, u
 // byte (the first holds r = vu - 128 (P - 1) bytes behind 128 - r masked ones); lane l of a step CRCs
 // piece 64 s + l of the run from a zero register, pushes it by x^(8 128 d) to the lane that completes
 // the value (or carries it on, lane 63), and a segmented XOR scan sums each value there.  No value
-// boundary falls inside a lane's bytes: no snapshot, restart or finalize, ~300 VALU per 8 KiB.  A
-// record's 48-B header window is loaded in the step its value completes; groups of completed records
-// are verified against the prediction (opcode, key length, value length, segment end, UTF-8 key) and
-// emitted with their value CRCs.  The first record not as predicted ends the run, and the stripe is
-// handed to k_replay's tile loop at that record (PieceHand); so is a stripe that does not start with
-// such a record, or whose entry the search has not found in its first tiles.
-// k_piece's workgroup (KVR_PNT threads: 8 waves, two per SIMD, with up to 256 VGPRs) and its piece
-// buffers a wave keeps (KVR_PNB: the step being worked on and KVR_PNB - 1 loading behind it).  A
-// workgroup takes the WPB stripes k_replay's workgroup of the same index takes, WPB / (KVR_PNT / 64)
-// consecutive ones a wave, one after the other.
+// boundary falls inside a lane's bytes: no snapshot, restart or finalize (~400 VALU per 8 KiB,
+// profiles/r06/final_pmc_cfg2.txt).  A record's 48-B header window is loaded in the step its value
+// completes and waits in the wave's LDS row; groups of completed records are verified against the
+// prediction (opcode, key length, value length, segment end, UTF-8 key) and emitted with their value
+// CRCs, the run's first pool chunk in run form (PieceRun + 8 B a record).  The first record not as
+// predicted ends the run, and the stripe is handed to k_replay's tile loop at that record (PieceHand);
+// so is a stripe that does not start with such a record, or whose entry the search has not found in
+// its first tiles.
+// k_piece's workgroup (KVR_PNT threads: 16 waves, four per SIMD at up to 128 VGPRs; 512 = 8 waves at
+// up to 256, each wave then taking two stripes one after the other) and the piece buffers a wave keeps
+// (KVR_PNB: the step being worked on and KVR_PNB - 1 loading behind it).  A workgroup takes the WPB
+// stripes k_replay's workgroup of the same index takes (profiles/r06/ab_piece_layouts.txt: 16 waves x 2
+// buffers is the fastest that fits; 8 waves x 3 buffers and 16 x 1 were slower).
 #ifndef KVR_PNT
 #define KVR_PNT 1024
 #endif
