@@ -2101,6 +2101,9 @@ __device__ __attribute__((noinline)) bool run_heads_equal(const uint8_t *base, u
 #ifndef KVR_PWIDE   // 1: a flush writes its tuples as whole 128-B lines (0: one tuple a lane, two 16-B halves)
 #define KVR_PWIDE 0
 #endif
+#ifndef KVR_PWEARLY   // 1: a step's windows are loaded before its next pieces and CRC (their lines are still in
+#define KVR_PWEARLY 0    // L2 from the pieces; 0: after the CRC, no window registers across it)
+#endif
 #ifndef KVR_PWROW   // 1: the header windows of a group wait in the wave's LDS row (0: in registers)
 #define KVR_PWROW 1
 #endif
@@ -2639,7 +2642,7 @@ __device__ __forceinline__ void piece_stripe(const uint32_t si, const uint32_t j
         auto body = [&](uint32_t (&cur)[UW + 1], uint32_t (&nx)[UW + 1]) -> bool {
             const bool h1 = q1 < q_end;
             uint32_t qa, qb;
-            pre_step(q0, g0, qa, qb, false);
+            pre_step(q0, g0, qa, qb, KVR_PWEARLY != 0);
             KVR_PSTAMP(9);
             if constexpr (NB == 3) issue(nx, q2, p2, geo_or_none(q2, p2));
             else issue(nx, q1, p1, geo_or_none(q1, p1));
@@ -2650,7 +2653,7 @@ __device__ __forceinline__ void piece_stripe(const uint32_t si, const uint32_t j
             // the windows of the records this step completes, behind the next step's pieces (their
             // registers are not held across the CRC); merged at the next step, whose CRC waits for its
             // pieces issued before them anyway
-            load_windows(qa, qb);
+            if (!KVR_PWEARLY) load_windows(qa, qb);
             finish_step(raw, q0, p0, g0, qa, qb);
             if (KVR_PBAL && (++bstep & (KVR_PBAL_EVERY - 1u)) == 0u) balance(h1 ? q1 : q_end);
             KVR_PSTAMP(3);
