@@ -102,6 +102,7 @@ struct __align__(16) SmemP {
 };
 constexpr uint32_t KR_OFF_P = (uint32_t)offsetof(SmemP, KR);
 static_assert(offsetof(SmemP, C2) < 65536 && KR_OFF_P >= 65536, "k_piece's tables: ds_read immediates, kmul_col's 64-KiB bit");
+static_assert(offsetof(SmemP, WROW) % 16 == 0, "k_piece's window rows: 16-B slots (KVR_PWDMA)");
 static_assert(sizeof(SmemP) <= 163840, "k_piece's LDS");
 static_assert(offsetof(Smem, C2) < 65536, "the byte tables' base fits a ds_read immediate");
 static_assert(KR_OFF >= 65536 && KQL_OFF - 65536 < 65536, "kmul_col's 64-KiB bit");
@@ -2107,6 +2108,12 @@ __device__ __attribute__((noinline)) bool run_heads_equal(const uint8_t *base, u
 #ifndef KVR_PWROW   // 1: the header windows of a group wait in the wave's LDS row (0: in registers)
 #define KVR_PWROW 1
 #endif
+#ifndef KVR_PWDMA   // 1 (with KVR_PWROW): a step's header windows go straight from memory into the wave's LDS
+#define KVR_PWDMA 1     // row (buffer_load ... lds: no registers), issued before the step's next pieces while
+#endif                  // their lines are still in L2 from the step's own pieces (0: through registers, after the CRC)
+#ifndef KVR_PWDMA_VMC   // the flush's wait for its windows: 9 (the pieces issued behind them stay in flight) or 0
+#define KVR_PWDMA_VMC 9
+#endif
 constexpr int PNT = KVR_PNT, PNB = KVR_PNB, PSPW = WPB / (PNT / 64);
 static_assert(PNT / 64 <= KVR_PWMAX, "one LDS window row per wave");
 static_assert(PSPW * (PNT / 64) == WPB && PNB >= 1 && PNB <= 3, "k_piece layout");
@@ -2327,8 +2334,23 @@ __device__ __forceinline__ void piece_stripe(const uint32_t si, const uint32_t j
         {   // the window from the wave's LDS row, realigned by its byte offset in the dword it was loaded
             // from (the same group base gadj as at its load: the group moves only in a flush)
             uint32_t wr[PWIN];
+            if (KVR_PWDMA) {   // (the row as [3][64 lanes][4 dwords]: what the DMA loads wrote,
+                               // each landed once every load issued before it has: the group's are all older)
+                // (every flush runs where the last window loads it reads were followed by one step's
+                // pieces, 9 loads issued unconditionally: vmcnt(9) has them landed, the pieces in flight)
+                if (KVR_PWDMA_VMC == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const uint32_t *const rw = &S.WROW[wv][0][0];
 #pragma unroll
-            for (int i = 0; i < PWIN; ++i) wr[i] = (KVR_PABLATE & 1024) ? 0u : S.WROW[wv][i][lane];
+                for (int i = 0; i < 3; ++i) {
+                    const uint4 v4 = reinterpret_cast<const uint4 *>(rw + 256 * i)[lane];
+                    wr[4 * i] = v4.x; wr[4 * i + 1] = v4.y; wr[4 * i + 2] = v4.z; wr[4 * i + 3] = v4.w;
+                }
+                wr[12] = 0u;   // (bytes 48-51: past any byte the flush reads)
+            } else {
+#pragma unroll
+                for (int i = 0; i < PWIN; ++i) wr[i] = (KVR_PABLATE & 1024) ? 0u : S.WROW[wv][i][lane];
+            }
             const uint32_t wsh = ((uint32_t)lane * L + gadj) & 3u;
 #pragma unroll
             for (int i = 0; i < 12; ++i) x[i] = __builtin_amdgcn_alignbyte(wr[i + 1], wr[i], wsh);
@@ -2492,7 +2514,7 @@ __device__ __forceinline__ void piece_stripe(const uint32_t si, const uint32_t j
     for (int i = 0; i < 13; ++i) wt[i] = 0u;
     auto merge_windows = [&]() {
 #if KVR_PWROW
-        if (wpend) {   // (the lanes whose records completed: their slots of the wave's row)
+        if (!KVR_PWDMA && wpend) {   // (the lanes whose records completed: their slots of the wave's row)
 #pragma unroll
             for (int i = 0; i < PWIN; ++i) S.WROW[wv][i][lane] = wt[i];
         }
@@ -2511,6 +2533,51 @@ __device__ __forceinline__ void piece_stripe(const uint32_t si, const uint32_t j
         wpend = qj >= qa && qj < qb;
         const int32_t wo = lane * (int32_t)L + (int32_t)gadj, wa = wpend && !(KVR_PABLATE & 32) ? (wo & ~3) : 0x7FFFFF00;
         wtsh = (uint32_t)wo & 3u;
+        if (KVR_PWDMA) {
+            // LDS DMA into the wave's row: M0 = the LDS destination, lane l's 16 B land at M0 + 16 l,
+            // so only the lanes whose records completed run the loads.  The compiler does not count
+            // these loads: its own piece waits only grow by them (loads retire in order), and the flush
+            // waits for them itself (KVR_PWDMA_VMC before it reads the row).  M0 is saved and restored
+            // around them (the kernel uses it nowhere else).
+            if (wpend && !(KVR_PABLATE & 64)) {
+                const uint32_t rb = __builtin_amdgcn_readfirstlane(
+                    (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)&S.WROW[wv][0][0]);
+                // (the flush reads bytes [0, 12 + ku) of a window, realigned: 32 B for keys up to 20 B, 48 B
+                // up to 36; the row's other dwords are never read)
+                uint32_t m0s;
+                if (ku <= 20u) {
+                    asm volatile(
+                        "s_mov_b32 %[sv], m0\n\t"
+                        "s_mov_b32 m0, %[rb]\n\t"
+                        "s_nop 0\n\t"
+                        "buffer_load_dwordx4 %[o0], %[rs], 0 offen lds\n\t"
+                        "s_add_u32 m0, %[rb], 0x400\n\t"
+                        "s_nop 0\n\t"
+                        "buffer_load_dwordx4 %[o1], %[rs], 0 offen lds\n\t"
+                        "s_mov_b32 m0, %[sv]"
+                        : [sv] "=&s"(m0s)
+                        : [o0] "v"(wa), [o1] "v"(wa + 16), [rb] "s"(rb), [rs] "s"(grs)
+                        : "memory", "scc");
+                } else {
+                    asm volatile(
+                        "s_mov_b32 %[sv], m0\n\t"
+                        "s_mov_b32 m0, %[rb]\n\t"
+                        "s_nop 0\n\t"
+                        "buffer_load_dwordx4 %[o0], %[rs], 0 offen lds\n\t"
+                        "s_add_u32 m0, %[rb], 0x400\n\t"
+                        "s_nop 0\n\t"
+                        "buffer_load_dwordx4 %[o1], %[rs], 0 offen lds\n\t"
+                        "s_add_u32 m0, %[rb], 0x800\n\t"
+                        "s_nop 0\n\t"
+                        "buffer_load_dwordx4 %[o2], %[rs], 0 offen lds\n\t"
+                        "s_mov_b32 m0, %[sv]"
+                        : [sv] "=&s"(m0s)
+                        : [o0] "v"(wa), [o1] "v"(wa + 16), [o2] "v"(wa + 32), [rb] "s"(rb), [rs] "s"(grs)
+                        : "memory", "scc");
+                }
+            }
+            return;
+        }
         if (!(KVR_PABLATE & 64)) {
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
@@ -2642,7 +2709,7 @@ __device__ __forceinline__ void piece_stripe(const uint32_t si, const uint32_t j
         auto body = [&](uint32_t (&cur)[UW + 1], uint32_t (&nx)[UW + 1]) -> bool {
             const bool h1 = q1 < q_end;
             uint32_t qa, qb;
-            pre_step(q0, g0, qa, qb, KVR_PWEARLY != 0);
+            pre_step(q0, g0, qa, qb, KVR_PWEARLY != 0 || KVR_PWDMA != 0);
             KVR_PSTAMP(9);
             if constexpr (NB == 3) issue(nx, q2, p2, geo_or_none(q2, p2));
             else issue(nx, q1, p1, geo_or_none(q1, p1));
@@ -2653,7 +2720,7 @@ __device__ __forceinline__ void piece_stripe(const uint32_t si, const uint32_t j
             // the windows of the records this step completes, behind the next step's pieces (their
             // registers are not held across the CRC); merged at the next step, whose CRC waits for its
             // pieces issued before them anyway
-            if (!KVR_PWEARLY) load_windows(qa, qb);
+            if (!KVR_PWEARLY && !KVR_PWDMA) load_windows(qa, qb);
             finish_step(raw, q0, p0, g0, qa, qb);
             if (KVR_PBAL && (++bstep & (KVR_PBAL_EVERY - 1u)) == 0u) balance(h1 ? q1 : q_end);
             KVR_PSTAMP(3);
