@@ -2111,8 +2111,11 @@ __device__ __attribute__((noinline)) bool run_heads_equal(const uint8_t *base, u
 #ifndef KVR_PWDMA   // 1 (with KVR_PWROW): a step's header windows go straight from memory into the wave's LDS
 #define KVR_PWDMA 1     // row (buffer_load ... lds: no registers), issued before the step's next pieces while
 #endif                  // their lines are still in L2 from the step's own pieces (0: through registers, after the CRC)
+#ifndef KVR_PWDMA_AFTER   // 1: the DMA windows after the next pieces, before the CRC (timing A/B; the flush
+#define KVR_PWDMA_AFTER 0     // then waits vmcnt(0))
+#endif
 #ifndef KVR_PWDMA_VMC   // the flush's wait for its windows: 9 (the pieces issued behind them stay in flight) or 0
-#define KVR_PWDMA_VMC 9
+#define KVR_PWDMA_VMC (KVR_PWDMA_AFTER ? 0 : 9)
 #endif
 constexpr int PNT = KVR_PNT, PNB = KVR_PNB, PSPW = WPB / (PNT / 64);
 static_assert(PNT / 64 <= KVR_PWMAX, "one LDS window row per wave");
@@ -2709,10 +2712,11 @@ __device__ __forceinline__ void piece_stripe(const uint32_t si, const uint32_t j
         auto body = [&](uint32_t (&cur)[UW + 1], uint32_t (&nx)[UW + 1]) -> bool {
             const bool h1 = q1 < q_end;
             uint32_t qa, qb;
-            pre_step(q0, g0, qa, qb, KVR_PWEARLY != 0 || KVR_PWDMA != 0);
+            pre_step(q0, g0, qa, qb, KVR_PWEARLY != 0 || (KVR_PWDMA != 0 && !KVR_PWDMA_AFTER));
             KVR_PSTAMP(9);
             if constexpr (NB == 3) issue(nx, q2, p2, geo_or_none(q2, p2));
             else issue(nx, q1, p1, geo_or_none(q1, p1));
+            if (KVR_PWDMA && KVR_PWDMA_AFTER) load_windows(qa, qb);
             KVR_PSTAMP(2);
             const uint32_t raw = crc_step(cur, g0);
             KVR_PSTAMP(1);
