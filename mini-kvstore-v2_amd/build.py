@@ -118,7 +118,10 @@ VARIANTS = {
     "pa128": ["-DKVR_PABLATE=128"], "pch4": ["-DKVR_PCHAINS=4"], "pwe1": ["-DKVR_PWEARLY=1"], "pa256": ["-DKVR_PABLATE=256"], "pa512": ["-DKVR_PABLATE=512"],
     "pa1536": ["-DKVR_PABLATE=1536"], "pa1920": ["-DKVR_PABLATE=1920"],
     "pa2048": ["-DKVR_PABLATE=2048"], "pa4096": ["-DKVR_PABLATE=4096"], "pw1": ["-DKVR_PWIDE=1", "-DKVR_PRUNFORM=0"], "prf0": ["-DKVR_PRUNFORM=0"], "pdef0": ["-DKVR_PDEFER=0"], "pa32768": ["-DKVR_PABLATE=32768"],
-    "pbd32": ["-DKVR_PBAL_D=32"], "pbd128": ["-DKVR_PBAL_D=128"], "pbe2": ["-DKVR_PBAL_EVERY=2"], "pa128": ["-DKVR_PABLATE=128"], "pch4": ["-DKVR_PCHAINS=4"], "pwe1": ["-DKVR_PWEARLY=1"], "pa8192": ["-DKVR_PABLATE=8192"], "pa16384": ["-DKVR_PABLATE=16384"],
+    "pbd32": ["-DKVR_PBAL_D=32"], "pbd128": ["-DKVR_PBAL_D=128"], "pbe2": ["-DKVR_PBAL_EVERY=2"], "pa8192": ["-DKVR_PABLATE=8192"], "pa16384": ["-DKVR_PABLATE=16384"],
+    # header windows (round 6): through registers after the CRC (the form before KVR_PWDMA), the DMA
+    # windows after the next pieces, the flush waiting vmcnt(0) (profiles/r06/ab_windows_dma.txt)
+    "pwdma0": ["-DKVR_PWDMA=0"], "pwaft": ["-DKVR_PWDMA_AFTER=1"], "pwvmc0": ["-DKVR_PWDMA_VMC=0"],
 }
 
 
